@@ -1,0 +1,827 @@
+/*
+ * lfg_oracle.c -- CPU FP64 restatement of the CV eclipse light-curve model.
+ *
+ * TEST INFRASTRUCTURE ONLY (see lfg_oracle.h).  Written straight from
+ * MODEL_SPEC.md, loop by loop, with no GPU-oriented restructuring, so that the
+ * HIP kernels (lfit_python_amd/csrc) are checked against an independent
+ * implementation.  Parity vs the real lfit package is UNPINNED.
+ *
+ * Reference behaviour mirrored here:
+ *   lfit.CV.calcFlux(pars, x, w)      CVModel.py:138, README.md:21-48,63
+ *   roche.xl1 / findphi / findi / bspot  CVModel.py:222,288,460,561
+ *   SimpleEclipse.chisq / ln_like     CVModel.py:157-191
+ *   SimpleEclipse.ln_prior            CVModel.py:193-324
+ *   LCModel.ln_prior                  CVModel.py:440-491
+ *   Prior.ln_prob                     model.py:83-113
+ *   Node.ln_prior / ln_prob           model.py:426-498
+ */
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+#include "lfg_oracle.h"
+
+#define PI      3.14159265358979323846
+#define TWO_PI  6.28318530717958647693
+#define DEG     (PI / 180.0)
+
+/* MODEL_SPEC.md section 7: numerical constants */
+#define RAY_TOL        1e-13
+#define RAY_MAXIT      100
+#define TH_TOL         1e-13
+#define ROOT_MAXIT     100
+#define MIN_MAXIT      100
+#define BS_TAIL        16.0
+#define STREAM_DELTA   1e-5
+#define STREAM_KAPPA   0.1
+#define STREAM_DTMAX   0.1
+#define STREAM_MAXSTEP 4000
+#define DISC_MAX_A     0.46   /* CVModel.py:217 */
+#define AZ_SLOPE       80.0   /* CVModel.py:282 */
+#define DPHI_TOL       1e-6   /* CVModel.py:452 */
+
+typedef struct {
+    double q, cA, cB, mu, xl1, pl1, Rs, Rs2;
+} Roche;
+
+/* ---------------------------------------------------------------- potential */
+static double pot(const Roche* R, double x, double y, double z)
+{
+    double r1 = sqrt(x * x + y * y + z * z);
+    double dx = x - 1.0;
+    double r2 = sqrt(dx * dx + y * y + z * z);
+    double xc = x - R->mu;
+    return -R->cA / r1 - R->cB / r2 - xc * xc - y * y;
+}
+
+static void grad_pot(const Roche* R, double x, double y, double z, double g[3])
+{
+    double r1s = x * x + y * y + z * z;
+    double i1 = 1.0 / (r1s * sqrt(r1s));
+    double dx = x - 1.0;
+    double r2s = dx * dx + y * y + z * z;
+    double i2 = 1.0 / (r2s * sqrt(r2s));
+    g[0] = R->cA * x * i1 + R->cB * dx * i2 - 2.0 * (x - R->mu);
+    g[1] = R->cA * y * i1 + R->cB * y * i2 - 2.0 * y;
+    g[2] = R->cA * z * i1 + R->cB * z * i2;
+}
+
+static double xl1_solve(double q)
+{
+    double cA = 2.0 / (1.0 + q), cB = q * cA, mu = q / (1.0 + q);
+    double lo = 0.0, hi = 1.0;
+    double x = 1.0 - cbrt(q / (3.0 * (1.0 + q)));
+    for (int it = 0; it < 200; ++it) {
+        double omx = 1.0 - x;
+        double f = cA / (x * x) - cB / (omx * omx) - 2.0 * (x - mu);
+        double df = -2.0 * cA / (x * x * x) - 2.0 * cB / (omx * omx * omx) - 2.0;
+        if (f > 0.0) lo = x; else hi = x;
+        double xn = x - f / df;
+        if (!(xn > lo && xn < hi)) xn = 0.5 * (lo + hi);
+        double d = xn - x;
+        x = xn;
+        if (fabs(d) <= 1e-15) break;
+    }
+    return x;
+}
+
+static int roche_init(Roche* R, double q)
+{
+    if (!(q > 0.0) || !isfinite(q)) return LFO_BAD_Q;
+    R->q = q;
+    R->cA = 2.0 / (1.0 + q);
+    R->cB = q * R->cA;
+    R->mu = q / (1.0 + q);
+    R->xl1 = xl1_solve(q);
+    R->pl1 = pot(R, R->xl1, 0.0, 0.0);
+    R->Rs = 1.0 - R->xl1;
+    R->Rs2 = R->Rs * R->Rs;
+    return LFO_OK;
+}
+
+/* Eggleton (1983) volume radius: only an initial guess, never a result. */
+static double eggleton(double q)
+{
+    double q3 = cbrt(q), q23 = q3 * q3;
+    return 0.49 * q23 / (0.6 * q23 + log(1.0 + q3));
+}
+
+/* ------------------------------------------------------- ray minimum (4.2) */
+/* Minimum of Phi along P + t e over the chord inside the sphere |X-D| <= Rs.
+ * Returns 0 when the ray misses the sphere (in front of P).  *tw carries the
+ * warm start in and the minimiser out. */
+static int ray_min(const Roche* R, const double P[3], const double e[3],
+                   double* tw, double* fmin)
+{
+    double ux = 1.0 - P[0], uy = -P[1], uz = -P[2];
+    double tc = ux * e[0] + uy * e[1] + uz * e[2];
+    double b2 = ux * ux + uy * uy + uz * uz - tc * tc;
+    if (b2 >= R->Rs2) return 0;
+    double h = sqrt(R->Rs2 - b2);
+    double lo = tc - h, hi = tc + h;
+    if (hi <= 0.0) return 0;
+    if (lo < 0.0) lo = 0.0;
+    double t = *tw;
+    if (!(t > lo && t < hi)) t = (tc > lo && tc < hi) ? tc : 0.5 * (lo + hi);
+    for (int it = 0; it < RAY_MAXIT; ++it) {
+        double x = P[0] + t * e[0], y = P[1] + t * e[1], z = P[2] + t * e[2];
+        double r1s = x * x + y * y + z * z;
+        double i1 = 1.0 / (r1s * sqrt(r1s));
+        double dx = x - 1.0;
+        double r2s = dx * dx + y * y + z * z;
+        double i2 = 1.0 / (r2s * sqrt(r2s));
+        double p1 = x * e[0] + y * e[1] + z * e[2];
+        double p2 = dx * e[0] + y * e[1] + z * e[2];
+        double f1 = R->cA * p1 * i1 + R->cB * p2 * i2
+                  - 2.0 * ((x - R->mu) * e[0] + y * e[1]);
+        double f2 = R->cA * i1 * (1.0 - 3.0 * p1 * p1 / r1s)
+                  + R->cB * i2 * (1.0 - 3.0 * p2 * p2 / r2s)
+                  - 2.0 * (e[0] * e[0] + e[1] * e[1]);
+        if (f1 > 0.0) hi = t; else lo = t;
+        double tn = (f2 > 0.0) ? t - f1 / f2 : 0.5 * (lo + hi);
+        if (!(tn > lo && tn < hi)) tn = 0.5 * (lo + hi);
+        double d = tn - t;
+        t = tn;
+        if (fabs(d) <= RAY_TOL) break;
+    }
+    *tw = t;
+    *fmin = pot(R, P[0] + t * e[0], P[1] + t * e[1], P[2] + t * e[2]);
+    return 1;
+}
+
+/* g(theta) = min Phi - Phi_L1 along the line of sight at orbital angle theta;
+ * dg from the envelope theorem.  Ray missing the sphere: g = +1, dg = 0. */
+static int g_eval(const Roche* R, const double P[3], double s, double c,
+                  double th, double* tw, double* g, double* dg)
+{
+    double sn = sin(th), cs = cos(th);
+    double e[3] = {s * cs, -s * sn, c};
+    double fm;
+    if (!ray_min(R, P, e, tw, &fm)) {
+        *g = 1.0;
+        *dg = 0.0;
+        return 0;
+    }
+    double t = *tw;
+    double gr[3];
+    grad_pot(R, P[0] + t * e[0], P[1] + t * e[1], P[2] + t * e[2], gr);
+    *g = fm - R->pl1;
+    *dg = t * (gr[0] * (-s * sn) + gr[1] * (-s * cs));
+    return 1;
+}
+
+/* safeguarded Newton for g(theta) = 0 on (lo, hi); slo = sign of g at lo */
+static double theta_root(const Roche* R, const double P[3], double s, double c,
+                         double lo, double hi, int slo, double th, double* tw)
+{
+    if (!(th > lo && th < hi)) th = 0.5 * (lo + hi);
+    for (int it = 0; it < ROOT_MAXIT; ++it) {
+        double g, dg;
+        g_eval(R, P, s, c, th, tw, &g, &dg);
+        if ((g > 0.0) == (slo > 0)) lo = th; else hi = th;
+        double tn = (dg != 0.0) ? th - g / dg : 0.5 * (lo + hi);
+        if (!(tn > lo && tn < hi)) tn = 0.5 * (lo + hi);
+        double d = tn - th;
+        th = tn;
+        if (fabs(d) <= TH_TOL) break;
+    }
+    return th;
+}
+
+/* Eclipse interval of point P (MODEL_SPEC 4.3).  Returns 1 and the interval
+ * [*a, *b] in phase units if eclipsed; 0 (a = 1, b = -1) otherwise. */
+static int element_interval(const Roche* R, const double P[3], double s,
+                            double c, double Reff, double* a, double* b)
+{
+    *a = 1.0;
+    *b = -1.0;
+    double ux = 1.0 - P[0], uy = -P[1], uz = -P[2];
+    double uxy = sqrt(ux * ux + uy * uy);
+    double uu = ux * ux + uy * uy + uz * uz;
+    if (uu <= R->Rs2 || uxy <= 0.0 || s <= 0.0) return 0;
+    double thc = atan2(-uy, ux);
+    double cosD = (sqrt(uu - R->Rs2) - c * uz) / (s * uxy);
+    if (cosD >= 1.0) return 0;
+    double Dm = (cosD <= -1.0) ? PI : acos(cosD);
+    double lo = thc - Dm, hi = thc + Dm;
+
+    double tw = -1.0, g, dg;
+    int chord = g_eval(R, P, s, c, thc, &tw, &g, &dg);
+    if (!chord) return 0;
+    double thi = thc;
+    if (!(g < 0.0)) {
+        /* minimum search for an interior point (secant on dg, bisection
+         * safeguard); stops as soon as g < 0 is seen */
+        int found = 0, have = 0;
+        double th = thc, pth = 0.0, pdg = 0.0;
+        double mlo = lo, mhi = hi;
+        for (int it = 0; it < MIN_MAXIT; ++it) {
+            if (chord) {
+                if (g < 0.0) { found = 1; thi = th; break; }
+                if (dg > 0.0) mhi = th; else mlo = th;
+            } else {
+                if (th < thc) mlo = th; else mhi = th;
+            }
+            double tn;
+            if (chord && have && dg != pdg) tn = th - dg * (th - pth) / (dg - pdg);
+            else tn = 0.5 * (mlo + mhi);
+            if (!(tn > mlo && tn < mhi)) tn = 0.5 * (mlo + mhi);
+            if (fabs(tn - th) <= TH_TOL) break;
+            if (chord) { pth = th; pdg = dg; have = 1; }
+            th = tn;
+            chord = g_eval(R, P, s, c, th, &tw, &g, &dg);
+        }
+        if (!found) return 0;
+    }
+    /* initial guesses: tangency with a sphere of radius Reff about D */
+    double de;
+    double ce = (sqrt(fmax(uu - Reff * Reff, 0.0)) - c * uz) / (s * uxy);
+    if (ce > -1.0 && ce < 1.0) de = acos(ce); else de = 0.5 * Dm;
+    double twi = tw, two = tw;
+    double thin = theta_root(R, P, s, c, lo, thi, +1, thc - de, &twi);
+    double thout = theta_root(R, P, s, c, thi, hi, -1, thc + de, &two);
+    *a = thin / TWO_PI;
+    *b = thout / TWO_PI;
+    return 1;
+}
+
+/* -------------------------------------------------- findphi / findi (4.4) */
+static int findphi_R(const Roche* R, double inc_deg, double* dphi)
+{
+    double i = inc_deg * DEG;
+    double s = sin(i), c = cos(i);
+    double P[3] = {0.0, 0.0, 0.0};
+    double cosD = (sqrt(1.0 - R->Rs2)) / s;
+    if (!(s > 0.0) || cosD >= 1.0) { *dphi = 0.0; return LFO_BAD_DPHI; }
+    double Dm = acos(cosD);
+    double tw = -1.0, g, dg;
+    g_eval(R, P, s, c, 0.0, &tw, &g, &dg);
+    if (!(g < 0.0)) { *dphi = 0.0; return LFO_BAD_DPHI; }
+    double th = theta_root(R, P, s, c, 0.0, Dm, -1, 0.5 * Dm, &tw);
+    *dphi = th / PI;
+    return LFO_OK;
+}
+
+/* h(c) = g(theta_e) for the WD centre as a function of c = cos(i) */
+static int h_eval(const Roche* R, double cth, double sth, double c, double* tw,
+                  double* h, double* dh)
+{
+    double s = sqrt(1.0 - c * c);
+    double e[3] = {s * cth, -s * sth, c};
+    double P[3] = {0.0, 0.0, 0.0};
+    double fm;
+    if (!ray_min(R, P, e, tw, &fm)) { *h = 1.0; *dh = 0.0; return 0; }
+    double t = *tw, gr[3];
+    grad_pot(R, t * e[0], t * e[1], t * e[2], gr);
+    *h = fm - R->pl1;
+    double r = c / s;
+    *dh = t * (gr[0] * (-r * cth) + gr[1] * (r * sth) + gr[2]);
+    return 1;
+}
+
+static int findi_R(const Roche* R, double dphi, double* inc_deg)
+{
+    if (!(dphi > 0.0) || !(dphi < 0.5)) return LFO_BAD_DPHI;
+    double the = PI * dphi;
+    double cth = cos(the), sth = sin(the);
+    if (!(cth > 0.0)) return LFO_BAD_DPHI;
+    double smin = sqrt(1.0 - R->Rs2) / cth;
+    if (smin >= 1.0) return LFO_BAD_DPHI;
+    double cmax = sqrt(1.0 - smin * smin);
+    double tw = -1.0, h, dh;
+    h_eval(R, cth, sth, 0.0, &tw, &h, &dh);
+    if (!(h < 0.0)) return LFO_BAD_DPHI;
+    double lo = 0.0, hi = cmax, c = 0.5 * cmax;
+    for (int it = 0; it < ROOT_MAXIT; ++it) {
+        h_eval(R, cth, sth, c, &tw, &h, &dh);
+        if (h > 0.0) hi = c; else lo = c;
+        double cn = (dh != 0.0) ? c - h / dh : 0.5 * (lo + hi);
+        if (!(cn > lo && cn < hi)) cn = 0.5 * (lo + hi);
+        double d = cn - c;
+        c = cn;
+        if (fabs(d) <= TH_TOL) break;
+    }
+    *inc_deg = acos(c) / DEG;
+    return LFO_OK;
+}
+
+/* --------------------------------------------------------- bspot (4.5) */
+static void stream_deriv(const Roche* R, const double s[4], double d[4])
+{
+    double x = s[0], y = s[1];
+    double m1 = 1.0 / (1.0 + R->q), m2 = R->q / (1.0 + R->q);
+    double r1s = x * x + y * y, i1 = 1.0 / (r1s * sqrt(r1s));
+    double dx = x - 1.0, r2s = dx * dx + y * y, i2 = 1.0 / (r2s * sqrt(r2s));
+    double Ux = m1 * x * i1 + m2 * dx * i2 - (x - R->mu);
+    double Uy = m1 * y * i1 + m2 * y * i2 - y;
+    d[0] = s[2];
+    d[1] = s[3];
+    d[2] = -Ux + 2.0 * s[3];
+    d[3] = -Uy - 2.0 * s[2];
+}
+
+static void hermite(const double s0[4], const double s1[4], double dt,
+                    double tau, double out[4])
+{
+    double t2 = tau * tau, t3 = t2 * tau;
+    double h00 = 2.0 * t3 - 3.0 * t2 + 1.0, h10 = t3 - 2.0 * t2 + tau;
+    double h01 = -2.0 * t3 + 3.0 * t2, h11 = t3 - t2;
+    double d00 = 6.0 * t2 - 6.0 * tau, d10 = 3.0 * t2 - 4.0 * tau + 1.0;
+    double d01 = -6.0 * t2 + 6.0 * tau, d11 = 3.0 * t2 - 2.0 * tau;
+    for (int k = 0; k < 2; ++k) {
+        out[k] = h00 * s0[k] + h10 * dt * s0[k + 2] + h01 * s1[k] + h11 * dt * s1[k + 2];
+        out[k + 2] = (d00 * s0[k] + d01 * s1[k]) / dt + d10 * s0[k + 2] + d11 * s1[k + 2];
+    }
+}
+
+static int bspot_R(const Roche* R, double rad, double out[4])
+{
+    if (!(rad > 0.0) || !(rad < R->xl1)) return LFO_BAD_STREAM;
+    double q = R->q, x1 = R->xl1;
+    double K = 1.0 / ((1.0 + q) * x1 * x1 * x1) + q / ((1.0 + q) * R->Rs2 * R->Rs);
+    double L = 0.5 * ((K - 2.0) + sqrt((K - 2.0) * (K - 2.0) + 4.0 * (2.0 * K + 1.0) * (K - 1.0)));
+    double lam = sqrt(L);
+    double A = -1.0, B = (L - 2.0 * K - 1.0) / (2.0 * lam) * A;
+    double nrm = sqrt(A * A + B * B);
+    double s[4] = {x1 + STREAM_DELTA * A / nrm, STREAM_DELTA * B / nrm,
+                   STREAM_DELTA * lam * A / nrm, STREAM_DELTA * lam * B / nrm};
+    double r = sqrt(s[0] * s[0] + s[1] * s[1]);
+    for (int n = 0; n < STREAM_MAXSTEP; ++n) {
+        double dt = STREAM_KAPPA * r * sqrt(r);
+        if (dt > STREAM_DTMAX) dt = STREAM_DTMAX;
+        double k1[4], k2[4], k3[4], k4[4], tmp[4], sn[4];
+        stream_deriv(R, s, k1);
+        for (int j = 0; j < 4; ++j) tmp[j] = s[j] + 0.5 * dt * k1[j];
+        stream_deriv(R, tmp, k2);
+        for (int j = 0; j < 4; ++j) tmp[j] = s[j] + 0.5 * dt * k2[j];
+        stream_deriv(R, tmp, k3);
+        for (int j = 0; j < 4; ++j) tmp[j] = s[j] + dt * k3[j];
+        stream_deriv(R, tmp, k4);
+        for (int j = 0; j < 4; ++j)
+            sn[j] = s[j] + dt / 6.0 * (k1[j] + 2.0 * k2[j] + 2.0 * k3[j] + k4[j]);
+        double rn = sqrt(sn[0] * sn[0] + sn[1] * sn[1]);
+        if (rn < rad) {
+            double lo = 0.0, hi = 1.0, p[4];
+            for (int it = 0; it < 60; ++it) {
+                double m = 0.5 * (lo + hi);
+                hermite(s, sn, dt, m, p);
+                if (sqrt(p[0] * p[0] + p[1] * p[1]) > rad) lo = m; else hi = m;
+            }
+            hermite(s, sn, dt, 0.5 * (lo + hi), out);
+            return LFO_OK;
+        }
+        if (rn > r && n > 0) return LFO_BAD_STREAM; /* passed periastron */
+        memcpy(s, sn, sizeof(s));
+        r = rn;
+    }
+    return LFO_BAD_STREAM;
+}
+
+/* ------------------------------------------------------ public roche API */
+double lfo_xl1(double q)
+{
+    Roche R;
+    if (roche_init(&R, q) != LFO_OK) return NAN;
+    return R.xl1;
+}
+
+int lfo_findphi(double q, double inc_deg, double* dphi)
+{
+    Roche R;
+    int st = roche_init(&R, q);
+    if (st) return st;
+    return findphi_R(&R, inc_deg, dphi);
+}
+
+int lfo_findi(double q, double dphi, double* inc_deg)
+{
+    Roche R;
+    int st = roche_init(&R, q);
+    if (st) return st;
+    return findi_R(&R, dphi, inc_deg);
+}
+
+int lfo_bspot(double q, double rad, double out4[4])
+{
+    Roche R;
+    int st = roche_init(&R, q);
+    if (st) return st;
+    return bspot_R(&R, rad, out4);
+}
+
+int lfo_point_interval(double q, double inc_deg, const double P[3], double* a,
+                       double* b)
+{
+    Roche R;
+    int st = roche_init(&R, q);
+    if (st) return st;
+    double i = inc_deg * DEG;
+    return element_interval(&R, P, sin(i), cos(i), eggleton(q), a, b);
+}
+
+/* ------------------------------------------------------- the CV model (5) */
+typedef struct {
+    Roche R;
+    double wdFlux, dFlux, sFlux, rsFlux, dphi, rdisc, ulimb, rwd, scale, az,
+        fis, dexp, phi0, exp1, exp2, tilt, yaw;
+    double inc, s, c, rwd_a, rdisc_a, l, upk, umax, lnpk, Reff;
+    double bs[4];
+    double nb[3], bden;
+    /* element tables */
+    double a[LFO_NEL], b[LFO_NEL], wgt[LFO_NEL];
+    double wdtot, dtot, bstot;
+    double donor[LFO_NDONOR][3];
+    double dnorm;
+} Model;
+
+static int unpack(Model* M, const double* p, int np)
+{
+    if (np != 14 && np != 18) return LFO_BAD_ARGS;
+    for (int k = 0; k < np; ++k)
+        if (!isfinite(p[k])) return LFO_BAD_ARGS;
+    M->wdFlux = p[0]; M->dFlux = p[1]; M->sFlux = p[2]; M->rsFlux = p[3];
+    M->dphi = p[5]; M->rdisc = p[6]; M->ulimb = p[7]; M->rwd = p[8];
+    M->scale = p[9]; M->az = p[10]; M->fis = p[11]; M->dexp = p[12];
+    M->phi0 = p[13];
+    if (np == 18) {
+        M->exp1 = p[14]; M->exp2 = p[15]; M->tilt = p[16]; M->yaw = p[17];
+    } else { /* simple bright spot (MODEL_SPEC 5.3) */
+        M->exp1 = 2.0; M->exp2 = 1.0; M->tilt = 90.0; M->yaw = 0.0;
+    }
+    return roche_init(&M->R, p[4]);
+}
+
+static double bs_profile_root(double a, double b, double lnpk)
+{
+    /* F(u) = a ln u - u^b - lnpk + BS_TAIL, decreasing for u > upk */
+    double upk = pow(a / b, 1.0 / b);
+    double lo = upk, hi = 2.0 * upk + 1.0;
+    for (int k = 0; k < 200; ++k) {
+        double F = a * log(hi) - pow(hi, b) - lnpk + BS_TAIL;
+        if (F < 0.0) break;
+        lo = hi;
+        hi *= 2.0;
+    }
+    double u = 0.5 * (lo + hi);
+    for (int it = 0; it < ROOT_MAXIT; ++it) {
+        double ub = pow(u, b);
+        double F = a * log(u) - ub - lnpk + BS_TAIL;
+        double dF = a / u - b * ub / u;
+        if (F > 0.0) lo = u; else hi = u;
+        double un = (dF != 0.0) ? u - F / dF : 0.5 * (lo + hi);
+        if (!(un > lo && un < hi)) un = 0.5 * (lo + hi);
+        double d = un - u;
+        u = un;
+        if (fabs(d) <= 1e-14 * u) break;
+    }
+    return u;
+}
+
+static int setup(Model* M)
+{
+    Roche* R = &M->R;
+    int st = findi_R(R, M->dphi, &M->inc);
+    if (st) return st;
+    double i = M->inc * DEG;
+    M->s = sin(i);
+    M->c = cos(i);
+    M->rwd_a = M->rwd * R->xl1;
+    M->rdisc_a = M->rdisc * R->xl1;
+    if (!(M->rwd_a > 0.0) || !(M->rdisc_a > M->rwd_a) || !(M->rdisc_a < R->xl1))
+        return LFO_BAD_GEOMETRY;
+    if (!(M->scale > 0.0) || !(M->exp1 > 0.0) || !(M->exp2 > 0.0))
+        return LFO_BAD_GEOMETRY;
+    st = bspot_R(R, M->rdisc_a, M->bs);
+    if (st) return st;
+    M->l = M->scale * R->xl1;
+    double a = M->exp1, b = M->exp2;
+    M->upk = pow(a / b, 1.0 / b);
+    M->lnpk = a * log(M->upk) - pow(M->upk, b);
+    M->umax = bs_profile_root(a, b, M->lnpk);
+    double t = M->tilt * DEG, psi = (M->az - 90.0 + M->yaw) * DEG;
+    M->nb[0] = sin(t) * cos(psi);
+    M->nb[1] = sin(t) * sin(psi);
+    M->nb[2] = cos(t);
+    double nmax = fabs(sin(t)) * M->s + cos(t) * M->c;
+    M->bden = M->fis + (1.0 - M->fis) * fmax(nmax, 0.0);
+    M->Reff = eggleton(R->q);
+    return LFO_OK;
+}
+
+static void build_elements(Model* M)
+{
+    const Roche* R = &M->R;
+    double s = M->s, c = M->c;
+    int k = 0;
+    /* white dwarf: limb-darkened sphere, tiles of the projected disc (5.1) */
+    double u = M->ulimb;
+    M->wdtot = 0.0;
+    for (int ir = 0; ir < LFO_NWD_RINGS; ++ir) {
+        double r0 = (double)ir / LFO_NWD_RINGS, r1 = (double)(ir + 1) / LFO_NWD_RINGS;
+        int nk = 4 * (2 * ir + 1);
+        double F0 = (1.0 - u) * 0.5 * r0 * r0 - u * pow(1.0 - r0 * r0, 1.5) / 3.0;
+        double F1 = (1.0 - u) * 0.5 * r1 * r1 - u * pow(1.0 - r1 * r1, 1.5) / 3.0;
+        double wring = (TWO_PI / nk) * (F1 - F0);
+        double rc = sqrt(0.5 * (r0 * r0 + r1 * r1));
+        double mu0 = sqrt(1.0 - rc * rc);
+        for (int j = 0; j < nk; ++j, ++k) {
+            double psi = TWO_PI * (j + 0.5) / nk;
+            double cp = cos(psi), sp = sin(psi);
+            double P[3];
+            P[0] = M->rwd_a * (-rc * sp * c + mu0 * s);
+            P[1] = M->rwd_a * (rc * cp);
+            P[2] = M->rwd_a * (rc * sp * s + mu0 * c);
+            element_interval(R, P, s, c, M->Reff, &M->a[k], &M->b[k]);
+            M->wgt[k] = wring;
+            M->wdtot += wring;
+        }
+    }
+    /* disc: power-law surface brightness, r in [rwd_a, rdisc_a] (5.2) */
+    M->dtot = 0.0;
+    double dr = (M->rdisc_a - M->rwd_a) / LFO_NDISC_R;
+    double ex = 2.0 - M->dexp;
+    for (int ir = 0; ir < LFO_NDISC_R; ++ir) {
+        double r0 = M->rwd_a + ir * dr, r1 = M->rwd_a + (ir + 1) * dr;
+        double rc = 0.5 * (r0 + r1);
+        double I = (fabs(ex) < 1e-10) ? log(r1 / r0) : (pow(r1, ex) - pow(r0, ex)) / ex;
+        double wring = (TWO_PI / LFO_NDISC_AZ) * I;
+        for (int j = 0; j < LFO_NDISC_AZ; ++j, ++k) {
+            double al = TWO_PI * (j + 0.5) / LFO_NDISC_AZ;
+            double P[3] = {rc * cos(al), rc * sin(al), 0.0};
+            element_interval(R, P, s, c, M->Reff, &M->a[k], &M->b[k]);
+            M->wgt[k] = wring;
+            M->dtot += wring;
+        }
+    }
+    /* bright spot strip (5.3) */
+    M->bstot = 0.0;
+    double du = M->umax / LFO_NBS;
+    double ca = cos(M->az * DEG), sa = sin(M->az * DEG);
+    for (int j = 0; j < LFO_NBS; ++j, ++k) {
+        double uk = (j + 0.5) * du;
+        double wk = exp(M->exp1 * log(uk) - pow(uk, M->exp2) - M->lnpk);
+        double off = M->l * (uk - M->upk);
+        double P[3] = {M->bs[0] + off * ca, M->bs[1] + off * sa, 0.0};
+        element_interval(R, P, s, c, M->Reff, &M->a[k], &M->b[k]);
+        M->wgt[k] = wk;
+        M->bstot += wk;
+    }
+    /* donor: Roche-lobe tiles (5.4) */
+    for (int it = 0; it < LFO_NDONOR_T; ++it) {
+        double t0 = PI * it / LFO_NDONOR_T, t1 = PI * (it + 1) / LFO_NDONOR_T;
+        double tc = 0.5 * (t0 + t1);
+        double dOm = (cos(t0) - cos(t1)) * (TWO_PI / LFO_NDONOR_P);
+        for (int ip = 0; ip < LFO_NDONOR_P; ++ip) {
+            double ph = TWO_PI * (ip + 0.5) / LFO_NDONOR_P;
+            double d[3] = {-cos(tc), sin(tc) * cos(ph), sin(tc) * sin(ph)};
+            /* radius where Phi = Phi_L1 on (0, Rs] */
+            double lo = 0.0, hi = R->Rs, r = M->Reff;
+            if (!(r > lo && r < hi)) r = 0.5 * hi;
+            double g[3];
+            for (int itr = 0; itr < ROOT_MAXIT; ++itr) {
+                double X0 = 1.0 + r * d[0], X1 = r * d[1], X2 = r * d[2];
+                double f = pot(R, X0, X1, X2) - R->pl1;
+                grad_pot(R, X0, X1, X2, g);
+                double df = g[0] * d[0] + g[1] * d[1] + g[2] * d[2];
+                if (f > 0.0) hi = r; else lo = r;
+                double rn = (df > 0.0) ? r - f / df : 0.5 * (lo + hi);
+                if (!(rn > lo && rn < hi)) rn = 0.5 * (lo + hi);
+                double dd = rn - r;
+                r = rn;
+                if (fabs(dd) <= 1e-15) break;
+            }
+            grad_pot(R, 1.0 + r * d[0], r * d[1], r * d[2], g);
+            double gn = sqrt(g[0] * g[0] + g[1] * g[1] + g[2] * g[2]);
+            double nx = g[0] / gn, ny = g[1] / gn, nz = g[2] / gn;
+            double cosn = nx * d[0] + ny * d[1] + nz * d[2];
+            double dA = r * r * dOm / cosn;
+            int kk = it * LFO_NDONOR_P + ip;
+            M->donor[kk][0] = dA * nx;
+            M->donor[kk][1] = dA * ny;
+            M->donor[kk][2] = dA * nz;
+        }
+    }
+    M->dnorm = 0.0;
+    for (int j = 0; j < LFO_NDONOR; ++j) {
+        double v = M->donor[j][0] * 0.0 + M->donor[j][1] * (-s) + M->donor[j][2] * c;
+        if (v > 0.0) M->dnorm += v;
+    }
+}
+
+static double vis(double a, double b, double ph, double h)
+{
+    if (h > 0.0) {
+        double ov = fmin(b, ph + h) - fmax(a, ph - h);
+        return (ov > 0.0) ? 1.0 - ov / (2.0 * h) : 1.0;
+    }
+    return (ph > a && ph < b) ? 0.0 : 1.0;
+}
+
+static void model_flux(const Model* M, const double* x, const double* w, int n,
+                       int nsub, double* flux, double* ywd, double* yd,
+                       double* ys, double* yrs)
+{
+    const int kd = LFO_NWD, kb = LFO_NWD + LFO_NDISC;
+    for (int p = 0; p < n; ++p) {
+        double ph0 = x[p] - M->phi0;
+        double wp = w ? w[p] : 0.0;
+        double h = wp / nsub;
+        double swd = 0.0, sd = 0.0, sb = 0.0, sr = 0.0;
+        for (int j = 0; j < nsub; ++j) {
+            double ph = ph0 - wp + (2 * j + 1) * h;
+            ph -= floor(ph + 0.5);
+            double acc = 0.0;
+            for (int k = 0; k < kd; ++k) acc += M->wgt[k] * vis(M->a[k], M->b[k], ph, h);
+            swd += acc / M->wdtot;
+            acc = 0.0;
+            for (int k = kd; k < kb; ++k) acc += M->wgt[k] * vis(M->a[k], M->b[k], ph, h);
+            sd += acc / M->dtot;
+            acc = 0.0;
+            for (int k = kb; k < LFO_NEL; ++k) acc += M->wgt[k] * vis(M->a[k], M->b[k], ph, h);
+            double th = TWO_PI * ph;
+            double e0 = M->s * cos(th), e1 = -M->s * sin(th), e2 = M->c;
+            double beam = 0.0;
+            if (M->bden > 0.0) {
+                double ne = M->nb[0] * e0 + M->nb[1] * e1 + M->nb[2] * e2;
+                beam = (M->fis + (1.0 - M->fis) * fmax(ne, 0.0)) / M->bden;
+            }
+            sb += beam * acc / M->bstot;
+            double da = 0.0;
+            for (int k = 0; k < LFO_NDONOR; ++k) {
+                double v = M->donor[k][0] * e0 + M->donor[k][1] * e1 + M->donor[k][2] * e2;
+                if (v > 0.0) da += v;
+            }
+            sr += da / M->dnorm;
+        }
+        double fw = M->wdFlux * swd / nsub, fd = M->dFlux * sd / nsub;
+        double fb = M->sFlux * sb / nsub, fr = M->rsFlux * sr / nsub;
+        flux[p] = fw + fd + fb + fr;
+        if (ywd) ywd[p] = fw;
+        if (yd) yd[p] = fd;
+        if (ys) ys[p] = fb;
+        if (yrs) yrs[p] = fr;
+    }
+}
+
+static void fill_nan(double* v, int n)
+{
+    if (!v) return;
+    for (int k = 0; k < n; ++k) v[k] = NAN;
+}
+
+int lfo_flux(const double* pars, int npars, const double* x, const double* w,
+             int n, int nsub, double* flux, double* ywd, double* yd,
+             double* ys, double* yrs)
+{
+    if (nsub < 1 || n < 0) return LFO_BAD_ARGS;
+    Model* M = (Model*)malloc(sizeof(Model));
+    int st = unpack(M, pars, npars);
+    if (!st) st = setup(M);
+    if (!st) {
+        build_elements(M);
+        model_flux(M, x, w, n, nsub, flux, ywd, yd, ys, yrs);
+    } else {
+        fill_nan(flux, n); fill_nan(ywd, n); fill_nan(yd, n);
+        fill_nan(ys, n); fill_nan(yrs, n);
+    }
+    free(M);
+    return st;
+}
+
+int lfo_elements(const double* pars, int npars, double* a, double* b,
+                 double* wgt, double* donor, double* geo)
+{
+    Model* M = (Model*)malloc(sizeof(Model));
+    int st = unpack(M, pars, npars);
+    if (!st) st = setup(M);
+    if (!st) {
+        build_elements(M);
+        memcpy(a, M->a, sizeof(M->a));
+        memcpy(b, M->b, sizeof(M->b));
+        memcpy(wgt, M->wgt, sizeof(M->wgt));
+        memcpy(donor, M->donor, sizeof(M->donor));
+        double g[16] = {M->R.xl1, M->R.pl1, M->inc, M->rwd_a, M->rdisc_a,
+                        M->bs[0], M->bs[1], M->bs[2], M->bs[3], M->upk,
+                        M->umax, M->l, M->bden, M->dnorm, M->Reff, M->lnpk};
+        memcpy(geo, g, sizeof(g));
+    }
+    free(M);
+    return st;
+}
+
+/* ------------------------------------------------------------ priors (6) */
+double lfo_prior_lnprob(int type, double p1, double p2, double norm, double v)
+{
+    switch (type) {
+    case 0: /* gauss: log(scipy.stats.norm(loc=p1, scale=p2).pdf(v)) */
+    case 1: {
+        if (type == 1 && v <= 0.0) return -INFINITY;
+        double z = (v - p1) / p2;
+        double pdf = exp(-z * z / 2.0) / sqrt(2.0 * PI) / p2;
+        return (pdf > 0.0) ? log(pdf) : -INFINITY;
+    }
+    case 2:
+        return (v > p1 && v < p2) ? log(1.0 / fabs(p1 - p2)) : -INFINITY;
+    case 3:
+        return (v > p1 && v < p2) ? log(1.0 / norm / v) : -INFINITY;
+    case 4:
+        return (v > 0.0 && v < p2) ? log(1.0 / norm / (v + p1)) : -INFINITY;
+    }
+    return -INFINITY;
+}
+
+/* ------------------------------------------------- batched tree ln_prob */
+static double eclipse_roche_prior(const double* p)
+{
+    /* SimpleEclipse.ln_prior checks, CVModel.py:193-316 */
+    Roche R;
+    if (roche_init(&R, p[4]) != LFO_OK) return -INFINITY;
+    double rdisc_a = p[6] * R.xl1;
+    if (rdisc_a > DISC_MAX_A) return -INFINITY;
+    double rwd = p[8], scale = p[9];
+    if (scale > rwd * 3.0 || scale < rwd / 3.0) return -INFINITY;
+    double bs[4];
+    if (bspot_R(&R, rdisc_a, bs) != LFO_OK) return -INFINITY;
+    double alpha = atan2(bs[1], bs[0]) / DEG;
+    if (alpha < 0.0) alpha = 90.0 - alpha;
+    double tangent = alpha + 90.0;
+    double minaz = fmax(0.0, tangent - AZ_SLOPE), maxaz = fmin(178.0, tangent + AZ_SLOPE);
+    if (p[10] < minaz || p[10] > maxaz) return -INFINITY;
+    return 0.0;
+}
+
+int lfo_lnprob_batch(const double* walkers, int W, int ndim,
+                     int E, const int* gather, const int* npars,
+                     const double* consts,
+                     const int* off, const double* x, const double* y,
+                     const double* ye, const double* w, int nsub,
+                     const int* prior_type, const double* prior_p1,
+                     const double* prior_p2, const double* prior_norm,
+                     double* lnp, double* lnlike_e, int nthreads)
+{
+    int used = 1;
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel num_threads(nthreads)
+    {
+#pragma omp single
+        used = omp_get_num_threads();
+    }
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads)
+#endif
+    for (int iw = 0; iw < W; ++iw) {
+        const double* v = walkers + (size_t)iw * ndim;
+        double pars[18];
+        double lp = 0.0;
+        /* LCModel.ln_prior: dphi vs findphi(q, 90) (CVModel.py:452-473) */
+        {
+            int g4 = gather[4], g5 = gather[5];
+            double q = g4 >= 0 ? v[g4] : consts[-1 - g4];
+            double dphi = g5 >= 0 ? v[g5] : consts[-1 - g5];
+            double maxphi;
+            if (lfo_findphi(q, 90.0, &maxphi) != LFO_OK) lp = -INFINITY;
+            else if (dphi > maxphi - DPHI_TOL) lp = -INFINITY;
+        }
+        /* Node.ln_prior over the variable parameters (model.py:439-449) */
+        for (int d = 0; d < ndim && isfinite(lp); ++d)
+            lp += lfo_prior_lnprob(prior_type[d], prior_p1[d], prior_p2[d], prior_norm[d], v[d]);
+        for (int e = 0; e < E && isfinite(lp); ++e) {
+            for (int k = 0; k < npars[e]; ++k) {
+                int g = gather[e * 18 + k];
+                pars[k] = g >= 0 ? v[g] : consts[-1 - g];
+            }
+            lp += eclipse_roche_prior(pars);
+        }
+        double ll = 0.0;
+        for (int e = 0; e < E; ++e) {
+            double le = -INFINITY;
+            if (isfinite(lp)) {
+                for (int k = 0; k < npars[e]; ++k) {
+                    int g = gather[e * 18 + k];
+                    pars[k] = g >= 0 ? v[g] : consts[-1 - g];
+                }
+                int n = off[e + 1] - off[e];
+                double* f = (double*)malloc(sizeof(double) * (n > 0 ? n : 1));
+                int st = lfo_flux(pars, npars[e], x + off[e], w + off[e], n, nsub,
+                                  f, NULL, NULL, NULL, NULL);
+                double chi = 0.0;
+                if (st != LFO_OK) chi = INFINITY;
+                else {
+                    for (int p = 0; p < n; ++p) {
+                        if (isnan(f[p])) { chi = INFINITY; break; }
+                        double r = (y[off[e] + p] - f[p]) / ye[off[e] + p];
+                        chi += r * r;
+                    }
+                }
+                free(f);
+                le = -0.5 * chi;
+            }
+            if (lnlike_e) lnlike_e[(size_t)iw * E + e] = le;
+            ll += le;
+        }
+        lnp[iw] = isfinite(lp) ? lp + ll : -INFINITY;
+    }
+    return used;
+}
