@@ -1,0 +1,134 @@
+/*
+ * lfg.h -- C ABI of liblfg_hip.so, the MI355X-native CV eclipse light-curve
+ * evaluator.  Drop-in for the lfit.CV.calcFlux() hot path of
+ * wildjames/lfit_python (reference at /root/reference).
+ *
+ * Every entry point takes plain pointers and sizes (no torch types), is
+ * re-entrant, keeps no global mutable state, never allocates, and enqueues its
+ * kernels on the caller's HIP stream (`stream` = hipStream_t, NULL = default
+ * stream).  Pointers marked [dev] are device (HBM) pointers; scratch space is
+ * passed in as `ws` of at least lfg_workspace_size() bytes.  All arithmetic is
+ * FP64.  Return value: LFG_OK or an LFG_E_* code (launch/argument errors).
+ * Per-parameter-set model failures are NOT call errors: they are reported in
+ * `status` and turn into NaN flux / -inf ln_like, exactly as the reference
+ * turns an lfit exception into NaN (CVModel.py:137-144) and -inf
+ * (CVModel.py:163-171, model.py:485-493).
+ */
+#ifndef LFG_H
+#define LFG_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LFG_OK               0
+#define LFG_E_ARGS          -1
+#define LFG_E_WORKSPACE     -2
+#define LFG_E_LAUNCH        -3
+
+/* per-parameter-set status (same codes as oracle/lfg_oracle.h) */
+#define LFG_ST_OK            0
+#define LFG_ST_BAD_Q         1
+#define LFG_ST_BAD_DPHI      2
+#define LFG_ST_BAD_GEOMETRY  3
+#define LFG_ST_BAD_STREAM    4
+#define LFG_ST_BAD_ARGS      5
+
+/* element grid of MODEL_SPEC.md section 5 */
+#define LFG_NWD      400
+#define LFG_NDISC    1000
+#define LFG_NBS      100
+#define LFG_NDONOR   400
+#define LFG_NEL      (LFG_NWD + LFG_NDISC + LFG_NBS)
+#define LFG_NGEO     48
+
+/*
+ * Compiled model tree: the flat description of a model.py/CVModel.py tree
+ * (trunk -> bands -> eclipses) produced by lfit_python_amd.batch.  Replaces
+ * the per-walker Python recursion of Node.ln_prob (model.py:476-498).
+ *   gather[e*18+k] >= 0 : CV parameter k of eclipse e is walker[gather]
+ *   gather[e*18+k] <  0 : it is the constant consts[-1-gather] (isVar = 0)
+ * CV parameter order is lfit's (CVModel.py:384-388; README.md:24-43), so the
+ * tree's yaw/tilt storage order (CVModel.py:376-380) is swapped in `gather`.
+ */
+typedef struct lfg_tree {
+    int E;                    /* eclipses (leaves)                          */
+    int ndim;                 /* walker vector length                       */
+    int nsub;                 /* exposure sub-bins S >= 1 (1 = native)      */
+    int max_n;                /* max data points of any eclipse            */
+    const int* gather;        /* [dev] E*18                                 */
+    const int* npars;         /* [dev] E, 14 or 18                          */
+    const double* consts;     /* [dev] constant parameter values            */
+    const int* off;           /* [dev] E+1 offsets into x/y/ye/w            */
+    const double* x;          /* [dev] phases                               */
+    const double* y;          /* [dev] fluxes                               */
+    const double* ye;         /* [dev] flux errors                          */
+    const double* w;          /* [dev] exposure half-widths (lc.w)          */
+    const int* prior_type;    /* [dev] ndim; 0 gauss 1 gaussPos 2 uniform
+                                 3 log_uniform 4 mod_jeff; NULL = no priors */
+    const double* prior_p1;   /* [dev] ndim                                 */
+    const double* prior_p2;   /* [dev] ndim                                 */
+    const double* prior_norm; /* [dev] ndim: Prior.normalise                */
+    int roche_priors;         /* 1: LCModel + eclipse Roche priors
+                                 (CVModel.py:193-324, 440-491)             */
+} lfg_tree;
+
+/* scratch bytes needed for W parameter sets x E eclipses */
+size_t lfg_workspace_size(int W, int E);
+
+/*
+ * Batched lfit.CV.calcFlux (CVModel.py:132-147; lfit API README.md:21-48).
+ *   pars   [dev] W x P (P = 14 simple or 18 complex bright spot)
+ *   x, w   [dev] N phases and exposure half-widths shared by all W sets
+ *          (w = NULL: point evaluation)
+ *   flux   [dev] W x N
+ *   comps  [dev] nullable, 4 x W x N: white dwarf, disc, bright spot, donor
+ *          (lfit's cv.ywd, cv.yd, cv.ys, cv.yrs; CVModel.py:155)
+ *   status [dev] W (LFG_ST_*)
+ */
+int lfg_flux(const double* pars, int W, int P, const double* x,
+             const double* w, int N, int nsub, double* flux, double* comps,
+             int* status, void* ws, size_t ws_bytes, void* stream);
+
+/*
+ * Batched emcee log-probability of a whole walker ensemble through a compiled
+ * tree: mcmcfit.ln_prob (mcmcfit.py:37-41) -> Node.ln_prob (model.py:476-498)
+ * = ln_prior (model.py:426-474 + Roche priors) + sum_e -0.5 chi^2_e
+ * (CVModel.py:157-191), fused: no flux array is materialised.
+ *   walkers  [dev] W x ndim
+ *   lnp      [dev] W
+ *   lnlike_e [dev] nullable, W x E per-eclipse ln_like
+ */
+int lfg_lnprob(const double* walkers, int W, const lfg_tree* tree,
+               double* lnp, double* lnlike_e, void* ws, size_t ws_bytes,
+               void* stream);
+
+/*
+ * White-box access to the element tables of MODEL_SPEC.md section 5 for W
+ * parameter sets (tests): a, b, wgt [dev] W x LFG_NEL eclipse intervals
+ * (phase) and weights; donor [dev] W x LFG_NDONOR x 3; geo [dev] W x LFG_NGEO;
+ * status [dev] W.
+ */
+int lfg_elements(const double* pars, int W, int P, double* a, double* b,
+                 double* wgt, double* donor, double* geo, int* status,
+                 void* ws, size_t ws_bytes, void* stream);
+
+/*
+ * Batched trm.roche primitives (CVModel.py:222,288,460,561):
+ *   op 0 xl1(q = a[i])                     -> out[i]
+ *   op 1 findphi(q = a[i], inc = b[i])     -> out[i]
+ *   op 2 findi(q = a[i], dphi = b[i])      -> out[i]
+ *   op 3 bspot(q = a[i], rad = b[i])       -> out[4i .. 4i+3] = x, y, vx, vy
+ * a, b, out, status are [dev]; status[i] = LFG_ST_*.
+ */
+int lfg_roche(int op, const double* a, const double* b, int n, double* out,
+              int* status, void* stream);
+
+const char* lfg_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LFG_H */

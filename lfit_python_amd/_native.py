@@ -1,0 +1,136 @@
+"""Loader for liblfg_hip.so, the gfx950 HIP library behind include/lfg.h.
+
+The product path has no CPU fallback: every public entry point of this
+package goes through the HIP kernels, and fails loudly when the library or a
+GPU is missing.
+"""
+import ctypes
+import os
+import subprocess
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(_HERE)
+LIB_DIR = os.path.join(_HERE, "_lib")
+LIB_PATH = os.path.join(LIB_DIR, "liblfg_hip.so")
+SOURCES = [os.path.join(_HERE, "csrc", "lfg.hip")]
+HEADERS = [os.path.join(_HERE, "csrc", "lfg_device.hpp"),
+           os.path.join(REPO, "include", "lfg.h")]
+INCLUDE = os.path.join(REPO, "include")
+ARCH = "gfx950"
+
+# element grid (MODEL_SPEC.md section 5; mirrors include/lfg.h)
+NWD, NDISC, NBS, NDONOR = 400, 1000, 100, 400
+NEL = NWD + NDISC + NBS
+NGEO = 48
+
+STATUS_TEXT = {
+    0: "ok",
+    1: "invalid mass ratio q",
+    2: "dphi has no inclination solution (dphi >= findphi(q, 90) or <= 0)",
+    3: "invalid geometry (rwd, rdisc, scale or bright-spot exponents)",
+    4: "the gas stream does not reach the disc radius",
+    5: "non-finite or wrong-length parameter vector",
+}
+
+
+class LfgTree(ctypes.Structure):
+    """ctypes mirror of struct lfg_tree (include/lfg.h)."""
+    _fields_ = [
+        ("E", ctypes.c_int), ("ndim", ctypes.c_int), ("nsub", ctypes.c_int),
+        ("max_n", ctypes.c_int),
+        ("gather", ctypes.c_void_p), ("npars", ctypes.c_void_p),
+        ("consts", ctypes.c_void_p), ("off", ctypes.c_void_p),
+        ("x", ctypes.c_void_p), ("y", ctypes.c_void_p),
+        ("ye", ctypes.c_void_p), ("w", ctypes.c_void_p),
+        ("prior_type", ctypes.c_void_p), ("prior_p1", ctypes.c_void_p),
+        ("prior_p2", ctypes.c_void_p), ("prior_norm", ctypes.c_void_p),
+        ("roche_priors", ctypes.c_int),
+    ]
+
+
+EXPORTS = ("lfg_workspace_size", "lfg_flux", "lfg_lnprob", "lfg_elements",
+           "lfg_roche", "lfg_version")
+
+
+def build(force=False, verbose=False):
+    """Compile liblfg_hip.so in-tree for gfx950 (hipcc cross-compiles offline)."""
+    os.makedirs(LIB_DIR, exist_ok=True)
+    newest = max(os.path.getmtime(p) for p in SOURCES + HEADERS)
+    if not force and os.path.exists(LIB_PATH) and os.path.getmtime(LIB_PATH) >= newest:
+        return LIB_PATH
+    tmp = LIB_PATH + ".tmp"
+    cmd = ["hipcc", "--offload-arch=%s" % ARCH, "-O3", "-std=c++17", "-fPIC",
+           "-shared", "-I", INCLUDE, "-o", tmp] + SOURCES
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def lib():
+    """The loaded library; raises if it was never built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                "liblfg_hip.so is missing (%s): run __graft_entry__.build() or "
+                "lfit_python_amd._native.build(); there is no CPU fallback" % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        vp, ip, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+        L.lfg_workspace_size.restype = sz
+        L.lfg_workspace_size.argtypes = [ip, ip]
+        L.lfg_flux.restype = ip
+        L.lfg_flux.argtypes = [vp, ip, ip, vp, vp, ip, ip, vp, vp, vp, vp, sz, vp]
+        L.lfg_lnprob.restype = ip
+        L.lfg_lnprob.argtypes = [vp, ip, ctypes.POINTER(LfgTree), vp, vp, vp, sz, vp]
+        L.lfg_elements.restype = ip
+        L.lfg_elements.argtypes = [vp, ip, ip, vp, vp, vp, vp, vp, vp, vp, sz, vp]
+        L.lfg_roche.restype = ip
+        L.lfg_roche.argtypes = [ip, vp, vp, ip, vp, vp, vp]
+        L.lfg_version.restype = ctypes.c_char_p
+        L.lfg_version.argtypes = []
+        _lib = L
+        return L
+
+
+def check(rc, what):
+    if rc != 0:
+        raise RuntimeError("%s failed with code %d" % (what, rc))
+
+
+def require_gpu():
+    import torch
+    if not torch.cuda.is_available():
+        raise RuntimeError("lfit_python_amd needs a HIP GPU (MI355X): no device visible, "
+                           "and the product path has no CPU fallback")
+
+
+def stream_ptr(device=None):
+    import torch
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class Workspace:
+    """Grow-only scratch buffer for the lfg_* entry points (one per device)."""
+
+    _pool = {}
+
+    @classmethod
+    def get(cls, nbytes, device):
+        import torch
+        key = str(device)
+        buf = cls._pool.get(key)
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+            cls._pool[key] = buf
+        return buf

@@ -1,0 +1,155 @@
+"""Compile a model tree once; evaluate ln_prob for whole walker ensembles on
+the GPU in one batched launch sequence.
+
+compile_tree() flattens the tree's routing (Node.__set_parameter_vector__
+model.py:586-603 and ancestor_param_dict model.py:706-712) into an index map
+gather[E, 18]: CV parameter k of eclipse e (lfit order, CVModel.py:384-388)
+is walker[:, gather[e, k]] or, for isVar = 0 parameters, a constant.  The
+prior of every variable parameter becomes a row of a small table.  The
+result is plain numpy (no GPU needed to build or inspect it).
+
+LnProbEvaluator uploads that description once and then maps a device tensor
+walkers[W, ndim] to lnp[W] with lfg_lnprob (include/lfg.h): the batched
+replacement of mcmcfit.ln_prob (mcmcfit.py:37-41) for every walker at once.
+"""
+import ctypes
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _native
+from .cvmodel import LCModel, SimpleEclipse, ComplexEclipse, _GPLeaf
+
+
+@dataclass
+class CompiledTree:
+    E: int
+    ndim: int
+    names: list
+    gather: np.ndarray      # [E, 18] int32
+    npars: np.ndarray       # [E] int32
+    consts: np.ndarray      # [nconst] f64
+    offsets: np.ndarray     # [E + 1] int32
+    x: np.ndarray
+    y: np.ndarray
+    ye: np.ndarray
+    w: np.ndarray
+    prior_type: np.ndarray  # [ndim] int32
+    prior_p1: np.ndarray
+    prior_p2: np.ndarray
+    prior_norm: np.ndarray
+    nsub: int = 1
+    roche_priors: bool = True
+    fixed_invalid: bool = False
+    leaf_labels: list = field(default_factory=list)
+
+    @property
+    def max_n(self):
+        return int(np.max(np.diff(self.offsets))) if self.E else 0
+
+
+def compile_tree(model, nsub=1):
+    """Flatten `model` (an LCModel tree or a lone eclipse subtree)."""
+    params = [p for p, _ in model.descendant_params()]
+    var = [p for p in params if p.isVar]
+    index = {id(p): i for i, p in enumerate(var)}
+    leaves = [n for n in model.walk() if isinstance(n, SimpleEclipse)]
+    if not leaves:
+        raise ValueError("the tree has no eclipse leaves")
+    if any(isinstance(n, _GPLeaf) for n in leaves):
+        raise NotImplementedError("GP likelihood trees are out of scope this round (useGP = 0 only)")
+    consts, gather, npars = [], np.zeros((len(leaves), 18), np.int32), []
+    xs, ys, yes, ws, offs = [], [], [], [], [0]
+    for e, leaf in enumerate(leaves):
+        d = leaf.ancestor_param_dict
+        names = leaf.cv_parnames
+        npars.append(len(names))
+        for k, nm in enumerate(names):
+            p = d[nm]
+            if p.isVar:
+                gather[e, k] = index[id(p)]
+            else:
+                consts.append(float(p.currVal))
+                gather[e, k] = -len(consts)
+        for k in range(len(names), 18):
+            gather[e, k] = gather[e, 0]
+        xs.append(leaf.lc.x); ys.append(leaf.lc.y); yes.append(leaf.lc.ye); ws.append(leaf.lc.w)
+        offs.append(offs[-1] + leaf.lc.n_data)
+    fixed_invalid = any((not p.isVar) and (not p.isValid) for p in params)
+    cat = lambda a: np.ascontiguousarray(np.concatenate(a).astype(np.float64)) if a else np.zeros(0)
+    return CompiledTree(
+        E=len(leaves), ndim=len(var), names=model.dynasty_par_names,
+        gather=gather, npars=np.asarray(npars, np.int32),
+        consts=np.asarray(consts, np.float64), offsets=np.asarray(offs, np.int32),
+        x=cat(xs), y=cat(ys), ye=cat(yes), w=cat(ws),
+        prior_type=np.asarray([p.prior.code for p in var], np.int32),
+        prior_p1=np.asarray([p.prior.p1 for p in var], np.float64),
+        prior_p2=np.asarray([p.prior.p2 for p in var], np.float64),
+        prior_norm=np.asarray([p.prior.normalise for p in var], np.float64),
+        nsub=int(nsub), roche_priors=isinstance(model, LCModel),
+        fixed_invalid=fixed_invalid, leaf_labels=[l.label for l in leaves])
+
+
+class LnProbEvaluator:
+    """Device-resident ln_prob for a compiled tree (one per GPU / stream)."""
+
+    def __init__(self, tree, device=None, max_walkers=0):
+        import torch
+        _native.require_gpu()
+        self.L = _native.lib()
+        self.tree = tree
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        t = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=self.device)
+        f64, i32 = torch.float64, torch.int32
+        self._buf = dict(
+            gather=t(tree.gather.reshape(-1), i32), npars=t(tree.npars, i32),
+            consts=t(tree.consts if len(tree.consts) else np.zeros(1), f64),
+            off=t(tree.offsets, i32), x=t(tree.x, f64), y=t(tree.y, f64),
+            ye=t(tree.ye, f64), w=t(tree.w, f64),
+            prior_type=t(tree.prior_type, i32), prior_p1=t(tree.prior_p1, f64),
+            prior_p2=t(tree.prior_p2, f64), prior_norm=t(tree.prior_norm, f64))
+        b = self._buf
+        p = lambda k: ctypes.c_void_p(b[k].data_ptr())
+        self.ctree = _native.LfgTree(
+            tree.E, tree.ndim, tree.nsub, tree.max_n, p('gather'), p('npars'), p('consts'),
+            p('off'), p('x'), p('y'), p('ye'), p('w'), p('prior_type'), p('prior_p1'),
+            p('prior_p2'), p('prior_norm'), int(tree.roche_priors))
+        self._ws = None
+        self._ws_walkers = 0
+        if max_walkers:
+            self._ensure(max_walkers)
+
+    def _ensure(self, W):
+        import torch
+        if W > self._ws_walkers:
+            nbytes = self.L.lfg_workspace_size(W, self.tree.E)
+            self._ws = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+            self._ws_walkers = W
+
+    def __call__(self, walkers, out=None, lnlike_e=None):
+        """walkers: float64 device tensor [W, ndim] -> lnp [W] (same stream)."""
+        import torch
+        if walkers.dtype != torch.float64 or walkers.device != self.device or not walkers.is_contiguous():
+            walkers = walkers.to(device=self.device, dtype=torch.float64).contiguous()
+        W, nd = walkers.shape
+        if nd != self.tree.ndim:
+            raise ValueError("walker vectors have %d entries, the tree has %d" % (nd, self.tree.ndim))
+        self._ensure(W)
+        if out is None:
+            out = torch.empty(W, dtype=torch.float64, device=self.device)
+        rc = self.L.lfg_lnprob(ctypes.c_void_p(walkers.data_ptr()), W, ctypes.byref(self.ctree),
+                               ctypes.c_void_p(out.data_ptr()),
+                               ctypes.c_void_p(lnlike_e.data_ptr()) if lnlike_e is not None else None,
+                               ctypes.c_void_p(self._ws.data_ptr()), self._ws.numel(),
+                               _native.stream_ptr(self.device))
+        _native.check(rc, "lfg_lnprob")
+        if self.tree.fixed_invalid:
+            out.fill_(-np.inf)
+        return out
+
+
+def ln_prob_batch(model, walkers, nsub=1):
+    """Convenience: compile `model` and evaluate walkers [W, ndim] (numpy)."""
+    import torch
+    ev = LnProbEvaluator(compile_tree(model, nsub=nsub))
+    return ev(torch.as_tensor(np.asarray(walkers, dtype=np.float64))).cpu().numpy()

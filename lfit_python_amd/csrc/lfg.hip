@@ -1,0 +1,619 @@
+// lfg.hip -- MI355X (gfx950) kernels and the C ABI of liblfg_hip.so.
+//
+// Pipeline for one batch of walkers (one emcee half-step):
+//   k_setup     one lane per (walker, eclipse): parameter gather, L1, findi,
+//               bright-spot stream, strip/beam frame, eclipse Roche priors;
+//               extra lanes per walker: LCModel dphi prior + Prior.ln_prob sum
+//   k_elements  one lane per (walker, eclipse, element): eclipse interval of
+//               every WD / disc / bright-spot element, donor surface tiles
+//   k_lnlike    one workgroup per (walker, eclipse): element tables staged in
+//               LDS, lanes stride the phase axis (coalesced), exposure
+//               integration, fused chi^2 with a wavefront/LDS reduction
+//   k_combine   one lane per walker: ln_prob = ln_prior + sum_e ln_like_e
+// Replaces, per walker, mcmcfit.ln_prob (mcmcfit.py:37-41) -> Node.ln_prob
+// (model.py:476-498) -> lfit.CV.calcFlux (CVModel.py:138).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lfg.h"
+#include "lfg_device.hpp"
+
+using namespace lfg;
+
+namespace {
+
+constexpr int SETUP_BLOCK = 64;
+constexpr int ELEM_BLOCK = 256;
+constexpr int LIKE_BLOCK = 256;
+
+__device__ const int kIdentityGather[18] = {0, 1, 2, 3, 4, 5, 6, 7, 8,
+                                            9, 10, 11, 12, 13, 14, 15, 16, 17};
+
+struct Ws {
+    double* geo;
+    int* status;
+    double* a;
+    double* b;
+    double* wgt;
+    double* donor;
+    double* prior;
+    double* lle;
+    size_t total;
+};
+
+inline size_t align256(size_t v) { return (v + 255) & ~size_t(255); }
+
+Ws carve(void* base, int W, int E)
+{
+    const size_t pairs = size_t(W) * size_t(E);
+    Ws ws{};
+    char* p = static_cast<char*>(base);
+    size_t off = 0;
+    auto take = [&](size_t bytes) { char* r = p ? p + off : nullptr; off += align256(bytes); return r; };
+    ws.geo = reinterpret_cast<double*>(take(pairs * LFG_NGEO * sizeof(double)));
+    ws.status = reinterpret_cast<int*>(take(pairs * sizeof(int)));
+    ws.a = reinterpret_cast<double*>(take(pairs * NEL * sizeof(double)));
+    ws.b = reinterpret_cast<double*>(take(pairs * NEL * sizeof(double)));
+    ws.wgt = reinterpret_cast<double*>(take(pairs * NEL * sizeof(double)));
+    ws.donor = reinterpret_cast<double*>(take(pairs * NDONOR * 3 * sizeof(double)));
+    ws.prior = reinterpret_cast<double*>(take(size_t(W) * sizeof(double)));
+    ws.lle = reinterpret_cast<double*>(take(pairs * sizeof(double)));
+    ws.total = off;
+    return ws;
+}
+
+// ---------------------------------------------------------------- k_setup
+struct SetupArgs {
+    const double* walkers;
+    int W, ndim, E, P;
+    const int* gather;  // nullptr -> identity
+    const int* npars;   // nullptr -> P
+    const double* consts;
+    const int* prior_type;
+    const double* prior_p1;
+    const double* prior_p2;
+    const double* prior_norm;
+    int roche_priors;
+    double* geo;
+    int* status;
+    double* prior;
+};
+
+__device__ inline double gather_par(const SetupArgs& A, int w, int g)
+{
+    return g >= 0 ? A.walkers[size_t(w) * A.ndim + g] : A.consts[-1 - g];
+}
+
+__global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
+{
+    const int t = blockIdx.x * SETUP_BLOCK + threadIdx.x;
+    const int npairs = A.W * A.E;
+    if (t >= npairs + A.W) return;
+    const int* gat = A.gather ? A.gather : kIdentityGather;
+
+    if (t >= npairs) {
+        // per-walker lane: LCModel.ln_prior dphi check (CVModel.py:452-473)
+        // and Node.ln_prior over the variable parameters (model.py:439-449)
+        const int w = t - npairs;
+        double lp = 0.0;
+        if (A.roche_priors) {
+            const double q = gather_par(A, w, gat[4]);
+            const double dphi = gather_par(A, w, gat[5]);
+            Roche R;
+            double maxphi;
+            if (roche_init(R, q) != ST_OK || findphi(R, 90.0, maxphi) != ST_OK) lp = -INFINITY;
+            else if (dphi > maxphi - DPHI_TOL) lp = -INFINITY;
+        }
+        if (A.prior_type) {
+            const double* v = A.walkers + size_t(w) * A.ndim;
+            for (int d = 0; d < A.ndim && isfinite(lp); ++d)
+                lp += prior_lnprob(A.prior_type[d], A.prior_p1[d], A.prior_p2[d], A.prior_norm[d], v[d]);
+        }
+        A.prior[w] = lp;
+        return;
+    }
+
+    const int w = t / A.E, e = t - (t / A.E) * A.E;
+    const int np = A.npars ? A.npars[e] : A.P;
+    double p[18];
+    bool finite = (np == 14 || np == 18);
+    for (int k = 0; k < 18; ++k) {
+        p[k] = (k < np) ? gather_par(A, w, gat[e * 18 + k]) : 0.0;
+        finite = finite && isfinite(p[k]);
+    }
+    if (np == 14) { p[14] = 2.0; p[15] = 1.0; p[16] = 90.0; p[17] = 0.0; }  // MODEL_SPEC 5.3
+    double* G = A.geo + size_t(t) * LFG_NGEO;
+    int st = ST_OK;
+    double rprior = 0.0;
+    Roche R;
+    if (!finite) st = ST_BAD_ARGS;
+    else st = roche_init(R, p[4]);
+
+    double bs[4] = {0.0, 0.0, 0.0, 0.0};
+    int bst = ST_BAD_STREAM;
+    if (st == ST_OK) {
+        const double rdisc_a = p[6] * R.xl1;
+        bst = bspot(R, rdisc_a, bs);
+        // SimpleEclipse.ln_prior Roche checks (CVModel.py:215-316)
+        if (rdisc_a > DISC_MAX_A) rprior = -INFINITY;
+        const double rwd = p[8], scale = p[9];
+        if (scale > rwd * 3.0 || scale < rwd / 3.0) rprior = -INFINITY;
+        if (bst != ST_OK) rprior = -INFINITY;
+        else {
+            double alpha = atan2(bs[1], bs[0]) / DEG;
+            if (alpha < 0.0) alpha = 90.0 - alpha;
+            const double tangent = alpha + 90.0;
+            const double minaz = fmax(0.0, tangent - AZ_SLOPE), maxaz = fmin(178.0, tangent + AZ_SLOPE);
+            if (p[10] < minaz || p[10] > maxaz) rprior = -INFINITY;
+        }
+    } else {
+        rprior = -INFINITY;
+    }
+
+    double inc = 0.0;
+    if (st == ST_OK) st = findi(R, p[5], inc);
+    const double rwd_a = p[8] * R.xl1, rdisc_a = p[6] * R.xl1;
+    if (st == ST_OK && (!(rwd_a > 0.0) || !(rdisc_a > rwd_a) || !(rdisc_a < R.xl1))) st = ST_BAD_GEOMETRY;
+    if (st == ST_OK && (!(p[9] > 0.0) || !(p[14] > 0.0) || !(p[15] > 0.0))) st = ST_BAD_GEOMETRY;
+    if (st == ST_OK && bst != ST_OK) st = bst;
+
+    A.status[t] = st;
+    G[G_RPRIOR] = A.roche_priors ? rprior : 0.0;
+    if (st != ST_OK) return;
+
+    double s, c;
+    sincos(inc * DEG, &s, &c);
+    const double a1 = p[14], a2 = p[15];
+    const double upk = pow(a1 / a2, 1.0 / a2);
+    const double lnpk = a1 * log(upk) - pow(upk, a2);
+    const double tilt = p[16] * DEG, psi = (p[10] - 90.0 + p[17]) * DEG;
+    double st_, ct_, sp_, cp_;
+    sincos(tilt, &st_, &ct_);
+    sincos(psi, &sp_, &cp_);
+    const double nmax = fabs(st_) * s + ct_ * c;
+    double saz, caz;
+    sincos(p[10] * DEG, &saz, &caz);
+
+    G[G_Q] = R.q; G[G_CA] = R.cA; G[G_CB] = R.cB; G[G_MU] = R.mu;
+    G[G_XL1] = R.xl1; G[G_PL1] = R.pl1; G[G_RS] = R.Rs; G[G_RS2] = R.Rs2;
+    G[G_S] = s; G[G_C] = c; G[G_INC] = inc;
+    G[G_RWD] = rwd_a; G[G_RDISC] = rdisc_a; G[G_REFF] = eggleton(R.q);
+    G[G_ULIMB] = p[7]; G[G_DEXP] = p[12];
+    G[G_BSX] = bs[0]; G[G_BSY] = bs[1]; G[G_BSVX] = bs[2]; G[G_BSVY] = bs[3];
+    G[G_L] = p[9] * R.xl1; G[G_UPK] = upk; G[G_UMAX] = bs_umax(a1, a2, lnpk); G[G_LNPK] = lnpk;
+    G[G_EXP1] = a1; G[G_EXP2] = a2; G[G_CAZ] = caz; G[G_SAZ] = saz;
+    G[G_NB0] = st_ * cp_; G[G_NB1] = st_ * sp_; G[G_NB2] = ct_;
+    G[G_BDEN] = p[11] + (1.0 - p[11]) * fmax(nmax, 0.0);
+    G[G_FIS] = p[11]; G[G_PHI0] = p[13];
+    G[G_WDF] = p[0]; G[G_DF] = p[1]; G[G_SF] = p[2]; G[G_RSF] = p[3];
+}
+
+// ------------------------------------------------------------- k_elements
+__global__ __launch_bounds__(ELEM_BLOCK) void k_elements(const double* __restrict__ geo,
+                                                         const int* __restrict__ status, int npairs,
+                                                         double* __restrict__ A, double* __restrict__ B,
+                                                         double* __restrict__ WG, double* __restrict__ DON)
+{
+    const long t = long(blockIdx.x) * ELEM_BLOCK + threadIdx.x;
+    const int pair = int(t / NALL);
+    const int k = int(t - long(pair) * NALL);
+    if (pair >= npairs) return;
+    if (status[pair] != ST_OK) return;
+    const double* G = geo + size_t(pair) * LFG_NGEO;
+    Roche R{G[G_Q], G[G_CA], G[G_CB], G[G_MU], G[G_XL1], G[G_PL1], G[G_RS], G[G_RS2]};
+    const double s = G[G_S], c = G[G_C];
+
+    if (k >= NEL) {  // donor tile (MODEL_SPEC 5.4)
+        const int kk = k - NEL;
+        const int it = kk / NDONOR_P, ip = kk - it * NDONOR_P;
+        const double t0 = PI * it / NDONOR_T, t1 = PI * (it + 1) / NDONOR_T;
+        const double tc = 0.5 * (t0 + t1);
+        const double dOm = (cos(t0) - cos(t1)) * (TWO_PI / NDONOR_P);
+        double stc, ctc, sph, cph;
+        sincos(tc, &stc, &ctc);
+        sincos(TWO_PI * (ip + 0.5) / NDONOR_P, &sph, &cph);
+        const double dx = -ctc, dy = stc * cph, dz = stc * sph;
+        double lo = 0.0, hi = R.Rs, r = G[G_REFF];
+        if (!(r > lo && r < hi)) r = 0.5 * hi;
+        double gx, gy, gz;
+        for (int itr = 0; itr < ROOT_MAXIT; ++itr) {
+            const double X0 = fma(r, dx, 1.0), X1 = r * dy, X2 = r * dz;
+            const double f = rpot(R, X0, X1, X2) - R.pl1;
+            rgrad(R, X0, X1, X2, gx, gy, gz);
+            const double df = gx * dx + gy * dy + gz * dz;
+            if (f > 0.0) hi = r; else lo = r;
+            double rn = (df > 0.0) ? r - f / df : 0.5 * (lo + hi);
+            if (!(rn > lo && rn < hi)) rn = 0.5 * (lo + hi);
+            const double d = rn - r;
+            r = rn;
+            if (fabs(d) <= 1e-15) break;
+        }
+        rgrad(R, fma(r, dx, 1.0), r * dy, r * dz, gx, gy, gz);
+        const double ig = rsqrt(gx * gx + gy * gy + gz * gz);
+        const double nx = gx * ig, ny = gy * ig, nz = gz * ig;
+        const double dA = r * r * dOm / (nx * dx + ny * dy + nz * dz);
+        double* D = DON + (size_t(pair) * NDONOR + kk) * 3;
+        D[0] = dA * nx;
+        D[1] = dA * ny;
+        D[2] = dA * nz;
+        return;
+    }
+
+    double Px, Py, Pz, wk;
+    if (k < NWD) {  // white dwarf tile (MODEL_SPEC 5.1); ring ir starts at 4 ir^2
+        int ir = int(sqrt(k * 0.25));
+        if (4 * (ir + 1) * (ir + 1) <= k) ++ir;
+        if (4 * ir * ir > k) --ir;
+        const int nk = 4 * (2 * ir + 1), j = k - 4 * ir * ir;
+        const double u = G[G_ULIMB];
+        const double r0 = double(ir) / NWD_RINGS, r1 = double(ir + 1) / NWD_RINGS;
+        const double F0 = (1.0 - u) * 0.5 * r0 * r0 - u * pow(1.0 - r0 * r0, 1.5) / 3.0;
+        const double F1 = (1.0 - u) * 0.5 * r1 * r1 - u * pow(1.0 - r1 * r1, 1.5) / 3.0;
+        wk = (TWO_PI / nk) * (F1 - F0);
+        const double rc = sqrt(0.5 * (r0 * r0 + r1 * r1));
+        const double mu0 = sqrt(1.0 - rc * rc);
+        double sp, cp;
+        sincos(TWO_PI * (j + 0.5) / nk, &sp, &cp);
+        const double rw = G[G_RWD];
+        Px = rw * (-rc * sp * c + mu0 * s);
+        Py = rw * (rc * cp);
+        Pz = rw * (rc * sp * s + mu0 * c);
+    } else if (k < NWD + NDISC) {  // disc (MODEL_SPEC 5.2)
+        const int kk = k - NWD;
+        const int ir = kk / NDISC_AZ, j = kk - ir * NDISC_AZ;
+        const double rin = G[G_RWD];
+        const double dr = (G[G_RDISC] - rin) / NDISC_R;
+        const double r0 = rin + ir * dr, r1 = rin + (ir + 1) * dr;
+        const double rc = 0.5 * (r0 + r1);
+        const double ex = 2.0 - G[G_DEXP];
+        const double I = (fabs(ex) < 1e-10) ? log(r1 / r0) : (pow(r1, ex) - pow(r0, ex)) / ex;
+        wk = (TWO_PI / NDISC_AZ) * I;
+        double sa, ca;
+        sincos(TWO_PI * (j + 0.5) / NDISC_AZ, &sa, &ca);
+        Px = rc * ca;
+        Py = rc * sa;
+        Pz = 0.0;
+    } else {  // bright-spot strip (MODEL_SPEC 5.3)
+        const int j = k - NWD - NDISC;
+        const double uk = (j + 0.5) * (G[G_UMAX] / NBS);
+        wk = exp(G[G_EXP1] * log(uk) - pow(uk, G[G_EXP2]) - G[G_LNPK]);
+        const double off = G[G_L] * (uk - G[G_UPK]);
+        Px = fma(off, G[G_CAZ], G[G_BSX]);
+        Py = fma(off, G[G_SAZ], G[G_BSY]);
+        Pz = 0.0;
+    }
+    double a, b;
+    element_interval(R, Px, Py, Pz, s, c, G[G_REFF], a, b);
+    const size_t o = size_t(pair) * NEL + k;
+    A[o] = a;
+    B[o] = b;
+    WG[o] = wk;
+}
+
+// --------------------------------------------------------------- k_lnlike
+__device__ __forceinline__ double wave_sum(double v)
+{
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+__device__ __forceinline__ double wave_min(double v)
+{
+    for (int off = 32; off > 0; off >>= 1) v = fmin(v, __shfl_xor(v, off, 64));
+    return v;
+}
+__device__ __forceinline__ double wave_max(double v)
+{
+    for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
+    return v;
+}
+
+struct LikeArgs {
+    const double* geo;
+    const int* status;
+    const double* A;
+    const double* B;
+    const double* WG;
+    const double* DON;
+    int E;
+    const int* off;  // nullptr: every pair uses x[0..N)
+    int N;
+    const double* x;
+    const double* y;
+    const double* ye;
+    const double* w;
+    int nsub;
+    double* flux;   // nullable, [pairs][N]
+    double* comps;  // nullable, [4][pairs][N]
+    double* lle;    // nullable, [pairs]
+    int npairs;
+};
+
+template <bool CHI>
+__global__ __launch_bounds__(LIKE_BLOCK) void k_lnlike(LikeArgs L)
+{
+    __shared__ double sa[NEL], sb[NEL], sw[NEL];
+    __shared__ double sd[NDONOR * 3];
+    __shared__ double red[5][LIKE_BLOCK / 64];
+
+    const int pair = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int e = pair % L.E;
+    const int o0 = L.off ? L.off[e] : 0;
+    const int n = L.off ? L.off[e + 1] - o0 : L.N;
+    const int st = L.status[pair];
+    if (st != ST_OK) {
+        for (int p = tid; p < n; p += LIKE_BLOCK) {
+            if (L.flux) L.flux[size_t(pair) * n + p] = NAN;
+            if (L.comps)
+                for (int m = 0; m < 4; ++m) L.comps[(size_t(m) * L.npairs + pair) * n + p] = NAN;
+        }
+        if (CHI && tid == 0) L.lle[pair] = -INFINITY;
+        return;
+    }
+    const double* G = L.geo + size_t(pair) * LFG_NGEO;
+    const double s = G[G_S], c = G[G_C];
+
+    // stage element tables in LDS; per-component totals, eclipse window
+    double twd = 0.0, td = 0.0, tb = 0.0, amin = INFINITY, bmax = -INFINITY, dn = 0.0;
+    const double* Ap = L.A + size_t(pair) * NEL;
+    const double* Bp = L.B + size_t(pair) * NEL;
+    const double* Wp = L.WG + size_t(pair) * NEL;
+    for (int k = tid; k < NEL; k += LIKE_BLOCK) {
+        const double a = Ap[k], b = Bp[k], wg = Wp[k];
+        sa[k] = a;
+        sb[k] = b;
+        sw[k] = wg;
+        if (k < NWD) twd += wg; else if (k < NWD + NDISC) td += wg; else tb += wg;
+        if (a < b) { amin = fmin(amin, a); bmax = fmax(bmax, b); }
+    }
+    const double* Dp = L.DON + size_t(pair) * NDONOR * 3;
+    for (int k = tid; k < NDONOR; k += LIKE_BLOCK) {
+        const double vx = Dp[3 * k], vy = Dp[3 * k + 1], vz = Dp[3 * k + 2];
+        sd[k] = vx;
+        sd[NDONOR + k] = vy;
+        sd[2 * NDONOR + k] = vz;
+        dn += fmax(-s * vy + c * vz, 0.0);
+    }
+    twd = wave_sum(twd); td = wave_sum(td); tb = wave_sum(tb);
+    amin = wave_min(amin); bmax = wave_max(bmax); dn = wave_sum(dn);
+    if (lane == 0) { red[0][wv] = twd; red[1][wv] = td; red[2][wv] = tb; red[3][wv] = dn; }
+    __shared__ double rmin[LIKE_BLOCK / 64], rmax[LIKE_BLOCK / 64];
+    if (lane == 0) { rmin[wv] = amin; rmax[wv] = bmax; }
+    __syncthreads();
+    twd = td = tb = dn = 0.0;
+    amin = INFINITY;
+    bmax = -INFINITY;
+    for (int i = 0; i < LIKE_BLOCK / 64; ++i) {
+        twd += red[0][i]; td += red[1][i]; tb += red[2][i]; dn += red[3][i];
+        amin = fmin(amin, rmin[i]);
+        bmax = fmax(bmax, rmax[i]);
+    }
+
+    const double wdF = G[G_WDF], dF = G[G_DF], sF = G[G_SF], rsF = G[G_RSF];
+    const double phi0 = G[G_PHI0], fis = G[G_FIS], bden = G[G_BDEN];
+    const double nb0 = G[G_NB0], nb1 = G[G_NB1], nb2 = G[G_NB2];
+    const int S = L.nsub;
+    double chi = 0.0;
+    for (int p = tid; p < n; p += LIKE_BLOCK) {
+        const double xk = L.x[o0 + p];
+        const double wk = L.w ? L.w[o0 + p] : 0.0;
+        const double ph0 = xk - phi0;
+        const double phc = ph0 - floor(ph0 + 0.5);
+        const double lo = phc - wk, hi = phc + wk;
+        double ewd = 0.0, ed = 0.0;
+        const bool inwin = (hi >= amin) && (lo <= bmax);
+        if (inwin) {
+            if (wk > 0.0) {
+                for (int k = 0; k < NWD; ++k) ewd = fma(sw[k], fmax(fmin(sb[k], hi) - fmax(sa[k], lo), 0.0), ewd);
+                for (int k = NWD; k < NWD + NDISC; ++k) ed = fma(sw[k], fmax(fmin(sb[k], hi) - fmax(sa[k], lo), 0.0), ed);
+                ewd /= 2.0 * wk;
+                ed /= 2.0 * wk;
+            } else {
+                for (int k = 0; k < NWD; ++k) ewd += (phc > sa[k] && phc < sb[k]) ? sw[k] : 0.0;
+                for (int k = NWD; k < NWD + NDISC; ++k) ed += (phc > sa[k] && phc < sb[k]) ? sw[k] : 0.0;
+            }
+        }
+        const double fw = wdF * (1.0 - ewd / twd);
+        const double fd = dF * (1.0 - ed / td);
+        const double h = wk / S;
+        double sbs = 0.0, srs = 0.0;
+        for (int j = 0; j < S; ++j) {
+            double ph = ph0 - wk + (2 * j + 1) * h;
+            ph -= floor(ph + 0.5);
+            double sn, cs;
+            sincos(TWO_PI * ph, &sn, &cs);
+            const double e0 = s * cs, e1 = -s * sn, e2 = c;
+            double beam = 0.0;
+            if (bden > 0.0) beam = (fis + (1.0 - fis) * fmax(nb0 * e0 + nb1 * e1 + nb2 * e2, 0.0)) / bden;
+            double eb = 0.0;
+            const double l2 = ph - h, h2 = ph + h;
+            if (h2 >= amin && l2 <= bmax) {
+                if (h > 0.0) {
+                    for (int k = NWD + NDISC; k < NEL; ++k) eb = fma(sw[k], fmax(fmin(sb[k], h2) - fmax(sa[k], l2), 0.0), eb);
+                    eb /= 2.0 * h;
+                } else {
+                    for (int k = NWD + NDISC; k < NEL; ++k) eb += (ph > sa[k] && ph < sb[k]) ? sw[k] : 0.0;
+                }
+            }
+            sbs += beam * (1.0 - eb / tb);
+            double da = 0.0;
+            for (int k = 0; k < NDONOR; ++k)
+                da += fmax(sd[k] * e0 + sd[NDONOR + k] * e1 + sd[2 * NDONOR + k] * e2, 0.0);
+            srs += da / dn;
+        }
+        const double fb = sF * sbs / S, fr = rsF * srs / S;
+        const double f = fw + fd + fb + fr;
+        if (L.flux) L.flux[size_t(pair) * n + p] = f;
+        if (L.comps) {
+            L.comps[(size_t(0) * L.npairs + pair) * n + p] = fw;
+            L.comps[(size_t(1) * L.npairs + pair) * n + p] = fd;
+            L.comps[(size_t(2) * L.npairs + pair) * n + p] = fb;
+            L.comps[(size_t(3) * L.npairs + pair) * n + p] = fr;
+        }
+        if (CHI) {
+            const double r = (L.y[o0 + p] - f) / L.ye[o0 + p];
+            chi += isnan(f) ? INFINITY : r * r;
+        }
+    }
+    if (CHI) {
+        chi = wave_sum(chi);
+        __syncthreads();
+        if (lane == 0) red[4][wv] = chi;
+        __syncthreads();
+        if (tid == 0) {
+            double tot = 0.0;
+            for (int i = 0; i < LIKE_BLOCK / 64; ++i) tot += red[4][i];
+            L.lle[pair] = -0.5 * tot;
+        }
+    }
+}
+
+// -------------------------------------------------------------- k_combine
+__global__ void k_combine(int W, int E, const double* __restrict__ prior, const double* __restrict__ geo,
+                          double* __restrict__ lle, double* __restrict__ lnp)
+{
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= W) return;
+    double lp = prior[w];
+    for (int e = 0; e < E; ++e) lp += geo[(size_t(w) * E + e) * LFG_NGEO + G_RPRIOR];
+    if (!isfinite(lp)) {
+        for (int e = 0; e < E; ++e) lle[size_t(w) * E + e] = -INFINITY;
+        lnp[w] = -INFINITY;
+        return;
+    }
+    double ll = 0.0;
+    for (int e = 0; e < E; ++e) ll += lle[size_t(w) * E + e];
+    lnp[w] = lp + ll;
+}
+
+// ---------------------------------------------------------------- k_roche
+__global__ void k_roche(int op, const double* __restrict__ a, const double* __restrict__ b, int n,
+                        double* __restrict__ out, int* __restrict__ status)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Roche R;
+    int st = roche_init(R, a[i]);
+    if (op == 0) {
+        out[i] = (st == ST_OK) ? R.xl1 : NAN;
+    } else if (op == 1) {
+        double v = NAN;
+        if (st == ST_OK) st = findphi(R, b[i], v);
+        out[i] = (st == ST_OK) ? v : NAN;
+    } else if (op == 2) {
+        double v = NAN;
+        if (st == ST_OK) st = findi(R, b[i], v);
+        out[i] = (st == ST_OK) ? v : NAN;
+    } else {
+        double v[4] = {NAN, NAN, NAN, NAN};
+        if (st == ST_OK) st = bspot(R, b[i], v);
+        if (st != ST_OK) v[0] = v[1] = v[2] = v[3] = NAN;
+        for (int m = 0; m < 4; ++m) out[4 * size_t(i) + m] = v[m];
+    }
+    status[i] = st;
+}
+
+inline int launch_ok() { return hipGetLastError() == hipSuccess ? LFG_OK : LFG_E_LAUNCH; }
+
+int run_front(const SetupArgs& S, const Ws& ws, hipStream_t st)
+{
+    const int npairs = S.W * S.E;
+    const int nlanes = npairs + S.W;
+    hipLaunchKernelGGL(k_setup, dim3((nlanes + SETUP_BLOCK - 1) / SETUP_BLOCK), dim3(SETUP_BLOCK), 0, st, S);
+    if (launch_ok() != LFG_OK) return LFG_E_LAUNCH;
+    const long nthreads = long(npairs) * NALL;
+    hipLaunchKernelGGL(k_elements, dim3(unsigned((nthreads + ELEM_BLOCK - 1) / ELEM_BLOCK)), dim3(ELEM_BLOCK), 0,
+                       st, ws.geo, ws.status, npairs, ws.a, ws.b, ws.wgt, ws.donor);
+    return launch_ok();
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t lfg_workspace_size(int W, int E)
+{
+    if (W <= 0 || E <= 0) return 0;
+    return carve(nullptr, W, E).total;
+}
+
+int lfg_flux(const double* pars, int W, int P, const double* x, const double* w, int N, int nsub,
+             double* flux, double* comps, int* status, void* wsp, size_t ws_bytes, void* stream)
+{
+    if (W <= 0 || N < 0 || nsub < 1 || (P != 14 && P != 18) || !pars || (!x && N > 0)) return LFG_E_ARGS;
+    Ws ws = carve(wsp, W, 1);
+    if (!wsp || ws_bytes < ws.total) return LFG_E_WORKSPACE;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    SetupArgs S{pars, W, P, 1, P, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
+                ws.geo, ws.status, ws.prior};
+    int rc = run_front(S, ws, st);
+    if (rc) return rc;
+    if (N > 0) {
+        LikeArgs L{ws.geo, ws.status, ws.a, ws.b, ws.wgt, ws.donor, 1, nullptr, N, x, nullptr, nullptr, w,
+                   nsub, flux, comps, nullptr, W};
+        hipLaunchKernelGGL(k_lnlike<false>, dim3(W), dim3(LIKE_BLOCK), 0, st, L);
+        if ((rc = launch_ok())) return rc;
+    }
+    if (status && hipMemcpyAsync(status, ws.status, sizeof(int) * W, hipMemcpyDeviceToDevice, st) != hipSuccess)
+        return LFG_E_LAUNCH;
+    return LFG_OK;
+}
+
+int lfg_lnprob(const double* walkers, int W, const lfg_tree* T, double* lnp, double* lnlike_e, void* wsp,
+               size_t ws_bytes, void* stream)
+{
+    if (W <= 0 || !T || T->E <= 0 || T->ndim <= 0 || T->nsub < 1 || !walkers || !lnp) return LFG_E_ARGS;
+    Ws ws = carve(wsp, W, T->E);
+    if (!wsp || ws_bytes < ws.total) return LFG_E_WORKSPACE;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    SetupArgs S{walkers, W, T->ndim, T->E, 18, T->gather, T->npars, T->consts, T->prior_type, T->prior_p1,
+                T->prior_p2, T->prior_norm, T->roche_priors, ws.geo, ws.status, ws.prior};
+    int rc = run_front(S, ws, st);
+    if (rc) return rc;
+    double* lle = lnlike_e ? lnlike_e : ws.lle;
+    LikeArgs L{ws.geo, ws.status, ws.a, ws.b, ws.wgt, ws.donor, T->E, T->off, T->max_n, T->x, T->y, T->ye,
+               T->w, T->nsub, nullptr, nullptr, lle, W * T->E};
+    hipLaunchKernelGGL(k_lnlike<true>, dim3(W * T->E), dim3(LIKE_BLOCK), 0, st, L);
+    if ((rc = launch_ok())) return rc;
+    hipLaunchKernelGGL(k_combine, dim3((W + 255) / 256), dim3(256), 0, st, W, T->E, ws.prior, ws.geo, lle, lnp);
+    return launch_ok();
+}
+
+int lfg_elements(const double* pars, int W, int P, double* a, double* b, double* wgt, double* donor,
+                 double* geo, int* status, void* wsp, size_t ws_bytes, void* stream)
+{
+    if (W <= 0 || (P != 14 && P != 18) || !pars) return LFG_E_ARGS;
+    Ws ws = carve(wsp, W, 1);
+    if (!wsp || ws_bytes < ws.total) return LFG_E_WORKSPACE;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    SetupArgs S{pars, W, P, 1, P, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
+                ws.geo, ws.status, ws.prior};
+    int rc = run_front(S, ws, st);
+    if (rc) return rc;
+    const size_t ne = size_t(W) * NEL * sizeof(double);
+    bool ok = true;
+    if (a) ok &= hipMemcpyAsync(a, ws.a, ne, hipMemcpyDeviceToDevice, st) == hipSuccess;
+    if (b) ok &= hipMemcpyAsync(b, ws.b, ne, hipMemcpyDeviceToDevice, st) == hipSuccess;
+    if (wgt) ok &= hipMemcpyAsync(wgt, ws.wgt, ne, hipMemcpyDeviceToDevice, st) == hipSuccess;
+    if (donor)
+        ok &= hipMemcpyAsync(donor, ws.donor, size_t(W) * NDONOR * 3 * sizeof(double), hipMemcpyDeviceToDevice,
+                             st) == hipSuccess;
+    if (geo)
+        ok &= hipMemcpyAsync(geo, ws.geo, size_t(W) * LFG_NGEO * sizeof(double), hipMemcpyDeviceToDevice, st) ==
+              hipSuccess;
+    if (status) ok &= hipMemcpyAsync(status, ws.status, sizeof(int) * W, hipMemcpyDeviceToDevice, st) == hipSuccess;
+    return ok ? LFG_OK : LFG_E_LAUNCH;
+}
+
+int lfg_roche(int op, const double* a, const double* b, int n, double* out, int* status, void* stream)
+{
+    if (op < 0 || op > 3 || n < 0 || !a || !out || !status || (op > 0 && !b)) return LFG_E_ARGS;
+    if (n == 0) return LFG_OK;
+    hipLaunchKernelGGL(k_roche, dim3((n + 63) / 64), dim3(64), 0, static_cast<hipStream_t>(stream), op, a, b, n,
+                       out, status);
+    return launch_ok();
+}
+
+const char* lfg_version(void) { return "lfg 0.1.0 gfx950 fp64"; }
+
+}  // extern "C"

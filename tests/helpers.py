@@ -1,0 +1,45 @@
+"""Shared inputs for the tests (seeded, synthetic)."""
+import numpy as np
+
+# eclipse 0 / band g / core of the reference's test_data/mcmc_input.dat:48-86,
+# in lfit CV order (tilt before yaw, CVModel.py:384-388)
+TRUTH18 = [0.0528, 0.0707, 0.0613, 0.0131, 0.1037, 0.0392, 0.2953, 0.284, 0.0187,
+           0.043, 120.0, 0.048, 0.5, 0.001, 1.1342, 4.5971, 72.0006, 5.4]
+TRUTH14 = TRUTH18[:14]
+
+# a second, better-constrained eclipse (mcmc_input.dat eclipse 1)
+ECL1 = [0.0528, 0.1238, 0.1518, 0.0131, 0.1037, 0.0392, 0.5214, 0.284, 0.0187,
+        0.0497, 122.0724, 0.1684, 1.9539, -0.0013, 3.4876, 1.4429, 52.4720, 15.6635]
+
+
+def random_pars(n, complex_bs=True, seed=0, spread=1.0):
+    """n parameter sets scattered around the truth, inside the model domain."""
+    rng = np.random.default_rng(seed)
+    base = np.array(TRUTH18 if complex_bs else TRUTH14)
+    out = []
+    while len(out) < n:
+        p = base.copy()
+        p[0:4] *= 1 + 0.3 * spread * rng.standard_normal(4)
+        p[4] = rng.uniform(0.06, 0.4)                       # q
+        p[5] = rng.uniform(0.03, 0.06)                      # dphi
+        p[6] = rng.uniform(0.25, 0.6)                       # rdisc (xl1 units)
+        p[7] = rng.uniform(0.1, 0.5)                        # ulimb
+        p[8] = rng.uniform(0.01, 0.03)                      # rwd
+        p[9] = p[8] * rng.uniform(0.5, 2.5)                 # scale
+        p[10] = rng.uniform(80, 160)                        # az
+        p[11] = rng.uniform(0.01, 0.9)                      # fis
+        p[12] = rng.uniform(0.1, 1.9)                       # dexp
+        p[13] = rng.uniform(-0.005, 0.005)                  # phi0
+        if complex_bs:
+            p[14] = rng.uniform(0.3, 4.0)
+            p[15] = rng.uniform(0.6, 4.5)
+            p[16] = rng.uniform(20, 160)
+            p[17] = rng.uniform(-40, 40)
+        out.append(p)
+    return np.array(out)
+
+
+def phase_grid(n=300, lo=-0.3, hi=0.3):
+    x = np.linspace(lo, hi, n)
+    w = np.mean(np.diff(x)) * np.ones_like(x) / 2.0
+    return x, w

@@ -1,0 +1,137 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle.
+
+Bar (BASELINE.json north_star): flux within 1e-6 relative of the oracle on
+identical (pars, phase, width).  The kernels and the oracle solve the same
+converged root-finding problems, so the observed agreement is ~1e-12; the
+tolerances below are the contract, not the observation.
+"""
+import numpy as np
+import pytest
+
+from tests.helpers import TRUTH14, TRUTH18, ECL1, random_pars, phase_grid
+
+pytestmark = pytest.mark.gpu
+
+FLUX_RTOL = 1e-6      # north_star contract, relative to the flux scale
+PHASE_ATOL = 1e-9     # eclipse contact phases
+
+
+def _rel(a, b, scale):
+    return np.max(np.abs(np.asarray(a) - np.asarray(b))) / scale
+
+
+def test_roche_primitives(oracle):
+    from lfit_python_amd import roche
+    qs = np.array([0.05, 0.1037, 0.2, 0.5, 1.0, 2.0])
+    np.testing.assert_allclose(roche.xl1(qs), [oracle.xl1(q) for q in qs], rtol=1e-13)
+    assert abs(roche.xl1(1.0) - 0.5) < 1e-14
+    for q in qs:
+        for inc in (80.0, 86.9, 90.0):
+            assert abs(roche.findphi(q, inc) - oracle.findphi(q, inc)) < 1e-11
+        dphi = oracle.findphi(q, 85.0)
+        assert abs(roche.findi(q, dphi) - 85.0) < 1e-8
+        assert abs(roche.findi(q, dphi) - oracle.findi(q, dphi)) < 1e-9
+        x1 = oracle.xl1(q)
+        for rad in (0.25 * x1, 0.5 * x1):
+            np.testing.assert_allclose(roche.bspot(q, rad), oracle.bspot(q, rad), rtol=1e-9, atol=1e-11)
+
+
+def test_roche_errors():
+    from lfit_python_amd import roche
+    with pytest.raises(roche.RocheError):
+        roche.xl1(-1.0)
+    with pytest.raises(roche.RocheError):
+        roche.findi(0.1, 0.3)          # wider than any inclination allows
+    with pytest.raises(roche.RocheError):
+        roche.bspot(0.1, 0.01)         # inside the stream's periastron
+
+
+def _elements_gpu(pars):
+    import ctypes
+    import torch
+    from lfit_python_amd import _native
+    L = _native.lib()
+    P = torch.as_tensor(np.atleast_2d(pars), dtype=torch.float64, device="cuda").contiguous()
+    W, npar = P.shape
+    a = torch.empty((W, _native.NEL), dtype=torch.float64, device="cuda")
+    b, wg = torch.empty_like(a), torch.empty_like(a)
+    don = torch.empty((W, _native.NDONOR, 3), dtype=torch.float64, device="cuda")
+    geo = torch.empty((W, _native.NGEO), dtype=torch.float64, device="cuda")
+    st = torch.empty(W, dtype=torch.int32, device="cuda")
+    ws = torch.empty(L.lfg_workspace_size(W, 1), dtype=torch.uint8, device="cuda")
+    vp = lambda t: ctypes.c_void_p(t.data_ptr())
+    rc = L.lfg_elements(vp(P), W, npar, vp(a), vp(b), vp(wg), vp(don), vp(geo), vp(st),
+                        vp(ws), ws.numel(), _native.stream_ptr())
+    assert rc == 0
+    return [t.cpu().numpy() for t in (st, a, b, wg, don, geo)]
+
+
+@pytest.mark.parametrize("pars", [TRUTH18, ECL1, TRUTH14])
+def test_element_tables(oracle, pars):
+    st, a, b, wg, don, geo = _elements_gpu(pars)
+    ost, oa, ob, ow, odon, ogeo = oracle.elements(pars)
+    assert st[0] == ost == 0
+    ecl = oa < ob
+    assert np.array_equal(a[0] < b[0], ecl)
+    assert np.max(np.abs(a[0][ecl] - oa[ecl])) < PHASE_ATOL
+    assert np.max(np.abs(b[0][ecl] - ob[ecl])) < PHASE_ATOL
+    np.testing.assert_allclose(wg[0], ow, rtol=1e-12)
+    np.testing.assert_allclose(don[0], odon, rtol=1e-9, atol=1e-14)
+
+
+@pytest.mark.parametrize("complex_bs", [True, False])
+@pytest.mark.parametrize("nsub", [1, 5])
+def test_flux_matches_oracle(oracle, complex_bs, nsub):
+    from lfit_python_amd.lfit import flux_batch
+    pars = random_pars(24, complex_bs=complex_bs, seed=11 + nsub)
+    x, w = phase_grid(300)
+    flux, status, comps = flux_batch(pars, x, w, nsub=nsub, components=True)
+    flux, status, comps = flux.cpu().numpy(), status.cpu().numpy(), comps.cpu().numpy()
+    n_ok = 0
+    for i, p in enumerate(pars):
+        st, (f, ywd, yd, ys, yrs) = oracle.flux(p, x, w, nsub=nsub, components=True)
+        assert status[i] == st
+        if st != 0:
+            assert np.all(np.isnan(flux[i]))
+            continue
+        n_ok += 1
+        scale = np.max(np.abs(f))
+        assert _rel(flux[i], f, scale) < FLUX_RTOL
+        for k, ref in enumerate((ywd, yd, ys, yrs)):
+            assert _rel(comps[k, i], ref, scale) < FLUX_RTOL
+        np.testing.assert_allclose(comps[:, i].sum(0), flux[i], rtol=1e-12, atol=1e-15)
+    assert n_ok >= 18
+
+
+def test_cv_object_api(oracle):
+    """lfit.CV(pars).calcFlux(pars, x, w) and the ywd/yd/ys/yrs attributes."""
+    from lfit_python_amd.lfit import CV, LfitError
+    x, w = phase_grid(300)
+    cv = CV(TRUTH18)
+    f = cv.calcFlux(TRUTH18, x, w)
+    _, (of, ywd, yd, ys, yrs) = oracle.flux(TRUTH18, x, w, components=True)
+    assert _rel(f, of, of.max()) < FLUX_RTOL
+    for got, ref in ((cv.ywd, ywd), (cv.yd, yd), (cv.ys, ys), (cv.yrs, yrs)):
+        assert _rel(got, ref, of.max()) < FLUX_RTOL
+    # width inferred from the data when absent (README.md:63, CVModel.py:30)
+    np.testing.assert_allclose(cv(TRUTH18, x), f, rtol=0, atol=0)
+    bad = list(TRUTH18)
+    bad[5] = 0.4  # dphi impossible
+    with pytest.raises(LfitError):
+        cv.calcFlux(bad, x, w)
+
+
+def test_point_evaluation_and_edges(oracle):
+    from lfit_python_amd.lfit import flux_batch
+    x = np.linspace(-0.5, 0.5, 257)
+    f, st = flux_batch(np.array([TRUTH18]), x, np.zeros_like(x))
+    st0, of = oracle.flux(TRUTH18, x, np.zeros_like(x))
+    assert st[0].item() == st0 == 0
+    assert _rel(f.cpu().numpy()[0], of, of.max()) < FLUX_RTOL
+    # out of eclipse the components sum to their maximum-light fluxes
+    f, st, c = flux_batch(np.array([TRUTH18]), np.array([0.45]), np.array([0.0]), components=True)
+    c = c.cpu().numpy()[:, 0, 0]
+    assert abs(c[0] - TRUTH18[0]) < 1e-14 and abs(c[1] - TRUTH18[1]) < 1e-14
+    # empty phase array
+    f, st = flux_batch(np.array([TRUTH18]), np.zeros(0), np.zeros(0))
+    assert f.shape == (1, 0)
