@@ -101,7 +101,7 @@ __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
             const double dphi = gather_par(A, w, gat[5]);
             Roche R;
             double maxphi;
-            if (roche_init(R, q) != ST_OK || findphi(R, 90.0, maxphi) != ST_OK) lp = -INFINITY;
+            if (roche_init(R, q) != ST_OK || findphi_fast(R, 90.0, maxphi) != ST_OK) lp = -INFINITY;
             else if (dphi > maxphi - DPHI_TOL) lp = -INFINITY;
         }
         if (A.prior_type) {
@@ -151,7 +151,7 @@ __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
     }
 
     double inc = 0.0;
-    if (st == ST_OK) st = findi(R, p[5], inc);
+    if (st == ST_OK) st = findi_fast(R, p[5], inc);
     const double rwd_a = p[8] * R.xl1, rdisc_a = p[6] * R.xl1;
     if (st == ST_OK && (!(rwd_a > 0.0) || !(rdisc_a > rwd_a) || !(rdisc_a < R.xl1))) st = ST_BAD_GEOMETRY;
     if (st == ST_OK && (!(p[9] > 0.0) || !(p[14] > 0.0) || !(p[15] > 0.0))) st = ST_BAD_GEOMETRY;
@@ -186,26 +186,36 @@ __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
     G[G_BDEN] = p[11] + (1.0 - p[11]) * fmax(nmax, 0.0);
     G[G_FIS] = p[11]; G[G_PHI0] = p[13];
     G[G_WDF] = p[0]; G[G_DF] = p[1]; G[G_SF] = p[2]; G[G_RSF] = p[3];
+    const double sce = s * cos(PI * p[5]);
+    G[G_RCAL] = sqrt(1.0 - sce * sce);
 }
 
 // ------------------------------------------------------------- k_elements
+// One lane per symmetry-unique element.  The WD/disc grids are mirror
+// symmetric under y -> -y and the donor grid under y -> -y and z -> -z; the
+// Roche potential shares those symmetries, so a mirrored element's eclipse
+// interval is [-b, -a] and a mirrored tile's vector has y (and/or z) negated.
+// Unique items per (walker, eclipse): WD 200, disc 500, spot 100, donor 100.
+constexpr int U_WD = NWD / 2, U_DISC = NDISC / 2, U_BS = NBS, U_DON = NDONOR / 4;
+constexpr int NUNIQ = U_WD + U_DISC + U_BS + U_DON;
+
 __global__ __launch_bounds__(ELEM_BLOCK) void k_elements(const double* __restrict__ geo,
                                                          const int* __restrict__ status, int npairs,
                                                          double* __restrict__ A, double* __restrict__ B,
                                                          double* __restrict__ WG, double* __restrict__ DON)
 {
     const long t = long(blockIdx.x) * ELEM_BLOCK + threadIdx.x;
-    const int pair = int(t / NALL);
-    const int k = int(t - long(pair) * NALL);
+    const int pair = int(t / NUNIQ);
+    const int u = int(t - long(pair) * NUNIQ);
     if (pair >= npairs) return;
     if (status[pair] != ST_OK) return;
     const double* G = geo + size_t(pair) * LFG_NGEO;
-    Roche R{G[G_Q], G[G_CA], G[G_CB], G[G_MU], G[G_XL1], G[G_PL1], G[G_RS], G[G_RS2]};
+    const Roche R{G[G_Q], G[G_CA], G[G_CB], G[G_MU], G[G_XL1], G[G_PL1], G[G_RS], G[G_RS2]};
     const double s = G[G_S], c = G[G_C];
 
-    if (k >= NEL) {  // donor tile (MODEL_SPEC 5.4)
-        const int kk = k - NEL;
-        const int it = kk / NDONOR_P, ip = kk - it * NDONOR_P;
+    if (u >= U_WD + U_DISC + U_BS) {  // donor tile (MODEL_SPEC 5.4), phi' in (0, pi/2)
+        const int uu = u - (U_WD + U_DISC + U_BS);
+        const int it = uu / (NDONOR_P / 4), ip = uu - it * (NDONOR_P / 4);
         const double t0 = PI * it / NDONOR_T, t1 = PI * (it + 1) / NDONOR_T;
         const double tc = 0.5 * (t0 + t1);
         const double dOm = (cos(t0) - cos(t1)) * (TWO_PI / NDONOR_P);
@@ -232,23 +242,36 @@ __global__ __launch_bounds__(ELEM_BLOCK) void k_elements(const double* __restric
         const double ig = rsqrt(gx * gx + gy * gy + gz * gz);
         const double nx = gx * ig, ny = gy * ig, nz = gz * ig;
         const double dA = r * r * dOm / (nx * dx + ny * dy + nz * dz);
-        double* D = DON + (size_t(pair) * NDONOR + kk) * 3;
-        D[0] = dA * nx;
-        D[1] = dA * ny;
-        D[2] = dA * nz;
+        const double vx = dA * nx, vy = dA * ny, vz = dA * nz;
+        // mirrors of p: z -> -z is 19-p, y -> -y is 9-p, both is 10+p
+        const int base = it * NDONOR_P;
+        double* D = DON + size_t(pair) * NDONOR * 3;
+        const int ks[4] = {base + ip, base + NDONOR_P - 1 - ip, base + NDONOR_P / 2 - 1 - ip,
+                           base + NDONOR_P / 2 + ip};
+        const double sy[4] = {1.0, 1.0, -1.0, -1.0}, sz[4] = {1.0, -1.0, 1.0, -1.0};
+        for (int m = 0; m < 4; ++m) {
+            D[3 * ks[m]] = vx;
+            D[3 * ks[m] + 1] = sy[m] * vy;
+            D[3 * ks[m] + 2] = sz[m] * vz;
+        }
         return;
     }
 
     double Px, Py, Pz, wk;
-    if (k < NWD) {  // white dwarf tile (MODEL_SPEC 5.1); ring ir starts at 4 ir^2
-        int ir = int(sqrt(k * 0.25));
-        if (4 * (ir + 1) * (ir + 1) <= k) ++ir;
-        if (4 * ir * ir > k) --ir;
-        const int nk = 4 * (2 * ir + 1), j = k - 4 * ir * ir;
-        const double u = G[G_ULIMB];
+    int k, km;
+    if (u < U_WD) {  // white dwarf tile (MODEL_SPEC 5.1): ring ir holds 2(2ir+1) unique tiles
+        int ir = int(sqrt(u * 0.5));
+        if (2 * (ir + 1) * (ir + 1) <= u) ++ir;
+        if (2 * ir * ir > u) --ir;
+        const int nk = 4 * (2 * ir + 1), q4 = nk / 4, jj = u - 2 * ir * ir;
+        const int j = (jj < q4) ? jj : jj - q4 + 3 * q4;  // cos(psi) > 0 half
+        const int jm = (j < nk / 2) ? nk / 2 - 1 - j : 3 * nk / 2 - 1 - j;
+        k = 4 * ir * ir + j;
+        km = 4 * ir * ir + jm;
+        const double ul = G[G_ULIMB];
         const double r0 = double(ir) / NWD_RINGS, r1 = double(ir + 1) / NWD_RINGS;
-        const double F0 = (1.0 - u) * 0.5 * r0 * r0 - u * pow(1.0 - r0 * r0, 1.5) / 3.0;
-        const double F1 = (1.0 - u) * 0.5 * r1 * r1 - u * pow(1.0 - r1 * r1, 1.5) / 3.0;
+        const double F0 = (1.0 - ul) * 0.5 * r0 * r0 - ul * pow(1.0 - r0 * r0, 1.5) / 3.0;
+        const double F1 = (1.0 - ul) * 0.5 * r1 * r1 - ul * pow(1.0 - r1 * r1, 1.5) / 3.0;
         wk = (TWO_PI / nk) * (F1 - F0);
         const double rc = sqrt(0.5 * (r0 * r0 + r1 * r1));
         const double mu0 = sqrt(1.0 - rc * rc);
@@ -258,9 +281,11 @@ __global__ __launch_bounds__(ELEM_BLOCK) void k_elements(const double* __restric
         Px = rw * (-rc * sp * c + mu0 * s);
         Py = rw * (rc * cp);
         Pz = rw * (rc * sp * s + mu0 * c);
-    } else if (k < NWD + NDISC) {  // disc (MODEL_SPEC 5.2)
-        const int kk = k - NWD;
-        const int ir = kk / NDISC_AZ, j = kk - ir * NDISC_AZ;
+    } else if (u < U_WD + U_DISC) {  // disc (MODEL_SPEC 5.2), alpha in (0, pi)
+        const int uu = u - U_WD;
+        const int ir = uu / (NDISC_AZ / 2), j = uu - ir * (NDISC_AZ / 2);
+        k = NWD + ir * NDISC_AZ + j;
+        km = NWD + ir * NDISC_AZ + NDISC_AZ - 1 - j;
         const double rin = G[G_RWD];
         const double dr = (G[G_RDISC] - rin) / NDISC_R;
         const double r0 = rin + ir * dr, r1 = rin + (ir + 1) * dr;
@@ -273,8 +298,9 @@ __global__ __launch_bounds__(ELEM_BLOCK) void k_elements(const double* __restric
         Px = rc * ca;
         Py = rc * sa;
         Pz = 0.0;
-    } else {  // bright-spot strip (MODEL_SPEC 5.3)
-        const int j = k - NWD - NDISC;
+    } else {  // bright-spot strip (MODEL_SPEC 5.3): no mirror partner
+        const int j = u - U_WD - U_DISC;
+        k = km = NWD + NDISC + j;
         const double uk = (j + 0.5) * (G[G_UMAX] / NBS);
         wk = exp(G[G_EXP1] * log(uk) - pow(uk, G[G_EXP2]) - G[G_LNPK]);
         const double off = G[G_L] * (uk - G[G_UPK]);
@@ -283,11 +309,17 @@ __global__ __launch_bounds__(ELEM_BLOCK) void k_elements(const double* __restric
         Pz = 0.0;
     }
     double a, b;
-    element_interval(R, Px, Py, Pz, s, c, G[G_REFF], a, b);
-    const size_t o = size_t(pair) * NEL + k;
-    A[o] = a;
-    B[o] = b;
-    WG[o] = wk;
+    element_interval_fast(R, Px, Py, Pz, s, c, G[G_RCAL], G[G_REFF], a, b);
+    const size_t o = size_t(pair) * NEL;
+    A[o + k] = a;
+    B[o + k] = b;
+    WG[o + k] = wk;
+    if (km != k) {
+        const bool ecl = a < b;
+        A[o + km] = ecl ? -b : 1.0;
+        B[o + km] = ecl ? -a : -1.0;
+        WG[o + km] = wk;
+    }
 }
 
 // --------------------------------------------------------------- k_lnlike
@@ -521,7 +553,7 @@ int run_front(const SetupArgs& S, const Ws& ws, hipStream_t st)
     const int nlanes = npairs + S.W;
     hipLaunchKernelGGL(k_setup, dim3((nlanes + SETUP_BLOCK - 1) / SETUP_BLOCK), dim3(SETUP_BLOCK), 0, st, S);
     if (launch_ok() != LFG_OK) return LFG_E_LAUNCH;
-    const long nthreads = long(npairs) * NALL;
+    const long nthreads = long(npairs) * NUNIQ;
     hipLaunchKernelGGL(k_elements, dim3(unsigned((nthreads + ELEM_BLOCK - 1) / ELEM_BLOCK)), dim3(ELEM_BLOCK), 0,
                        st, ws.geo, ws.status, npairs, ws.a, ws.b, ws.wgt, ws.donor);
     return launch_ok();

@@ -51,7 +51,7 @@ enum Geo {
     G_S, G_C, G_INC, G_RWD, G_RDISC, G_REFF, G_ULIMB, G_DEXP,
     G_BSX, G_BSY, G_BSVX, G_BSVY, G_L, G_UPK, G_UMAX, G_LNPK,
     G_EXP1, G_EXP2, G_CAZ, G_SAZ, G_NB0, G_NB1, G_NB2, G_BDEN,
-    G_FIS, G_PHI0, G_WDF, G_DF, G_SF, G_RSF, G_RPRIOR,
+    G_FIS, G_PHI0, G_WDF, G_DF, G_SF, G_RSF, G_RPRIOR, G_RCAL,
     G_COUNT
 };
 static_assert(G_COUNT <= 48, "LFG_NGEO");
@@ -258,6 +258,144 @@ __device__ inline bool element_interval(const Roche& R, double Px, double Py, do
     return true;
 }
 
+// ---------------------------------------------------------------------------
+// Fast path for element_interval (same converged answer, ~10x less work).
+// The contact phases are the tangencies of the line of sight with the lobe
+// surface: F1 = Phi(X) - Phi_L1 = 0 and F2 = grad Phi(X).e = 0 at
+// X = P + t e(theta), solved by 2-D Newton in (theta, t).  With
+// e_theta = de/dtheta = (e_y, -e_x, 0) the Jacobian needs only scalars:
+//   J11 = t grad.e_th, J12 = F2, J21 = t e_th.H.e + grad.e_th, J22 = e.H.e
+// Existence is decided by Newton minimisation of Phi over the cone of lines
+// of sight (theta, t), which stops as soon as a point inside the lobe is seen.
+// Anything not cleanly converged falls back to the nested solver above.
+struct ConePt {
+    double phi, gth, F2, eHe, etHe, ethHeth, gtt, dX2;
+};
+
+__device__ __forceinline__ void cone_point(const Roche& R, double Px, double Py, double Pz, double s,
+                                           double c, double th, double t, ConePt& o)
+{
+    double sn, cs;
+    sincos(th, &sn, &cs);
+    const double ex = s * cs, ey = -s * sn;
+    const double x = fma(t, ex, Px), y = fma(t, ey, Py), z = fma(t, c, Pz);
+    const double r1s = x * x + y * y + z * z;
+    const double ir1 = rsqrt(r1s), ir1s = ir1 * ir1;
+    const double dx = x - 1.0;
+    const double r2s = dx * dx + y * y + z * z;
+    const double ir2 = rsqrt(r2s), ir2s = ir2 * ir2;
+    const double i1 = R.cA * ir1s * ir1, i2 = R.cB * ir2s * ir2, i12 = i1 + i2;
+    const double xm = x - R.mu;
+    o.phi = -R.cA * ir1 - R.cB * ir2 - xm * xm - y * y;
+    const double gx = i1 * x + i2 * dx - 2.0 * xm;
+    const double gy = (i12 - 2.0) * y;
+    const double gz = i12 * z;
+    const double p1 = x * ex + y * ey + z * c, p2 = p1 - ex;
+    const double q1 = x * ey - y * ex, q2 = q1 - ey;
+    const double k1 = 3.0 * i1 * ir1s, k2 = 3.0 * i2 * ir2s;
+    const double s2 = ex * ex + ey * ey;
+    o.F2 = gx * ex + gy * ey + gz * c;
+    o.gth = gx * ey - gy * ex;
+    o.eHe = i12 - k1 * p1 * p1 - k2 * p2 * p2 - 2.0 * s2;
+    o.etHe = -k1 * p1 * q1 - k2 * p2 * q2;
+    o.ethHeth = i12 * s2 - k1 * q1 * q1 - k2 * q2 * q2 - 2.0 * s2;
+    o.gtt = -(gx * ex + gy * ey);
+    o.dX2 = r2s;
+}
+
+// 2-D Newton for one contact phase; returns false unless cleanly converged
+// to a tangency of the right kind (ingress: g falling with theta).
+__device__ inline bool tangency(const Roche& R, double Px, double Py, double Pz, double s, double c,
+                                bool ingress, double& th, double& t)
+{
+    for (int it = 0; it < 16; ++it) {
+        ConePt o;
+        cone_point(R, Px, Py, Pz, s, c, th, t, o);
+        const double F1 = o.phi - R.pl1;
+        const double J11 = t * o.gth, J12 = o.F2;
+        const double J21 = t * o.etHe + o.gth, J22 = o.eHe;
+        const double det = J11 * J22 - J12 * J21;
+        if (!(det != 0.0)) return false;
+        const double idet = 1.0 / det;
+        double dth = -(F1 * J22 - o.F2 * J12) * idet;
+        const double dt = -(J11 * o.F2 - J21 * F1) * idet;
+        dth = fmin(fmax(dth, -0.05), 0.05);
+        th += dth;
+        t += dt;
+        if (fabs(dth) <= TH_TOL) {
+            return J22 > 0.0 && ((J11 < 0.0) == ingress) && t > 0.0 && o.dX2 < R.Rs2;
+        }
+    }
+    return false;
+}
+
+// 0: not eclipsed, 1: eclipsed, -1: undecided (use the nested solver)
+__device__ inline int cone_exists(const Roche& R, double Px, double Py, double Pz, double s, double c,
+                                  double th, double t)
+{
+    for (int it = 0; it < 16; ++it) {
+        ConePt o;
+        cone_point(R, Px, Py, Pz, s, c, th, t, o);
+        if (o.phi < R.pl1) return (o.dX2 < R.Rs2) ? 1 : -1;
+        const double Gth = t * o.gth, Gt = o.F2;
+        const double Htt = o.eHe, Hht = o.gth + t * o.etHe, Hhh = t * t * o.ethHeth + t * o.gtt;
+        const double det = Hhh * Htt - Hht * Hht;
+        if (!(Hhh > 0.0 && Htt > 0.0 && det > 0.0)) return -1;
+        const double idet = 1.0 / det;
+        double dth = -(Htt * Gth - Hht * Gt) * idet;
+        double dt = -(Hhh * Gt - Hht * Gth) * idet;
+        const double big = fmax(fabs(dth), fabs(dt));
+        if (big > 0.05) {  // trust region: shorten the step, keep its direction
+            dth *= 0.05 / big;
+            dt *= 0.05 / big;
+        }
+        th += dth;
+        t += dt;
+        if (fabs(dth) <= 1e-12 && fabs(dt) <= 1e-12) return 0;
+    }
+    return -1;
+}
+
+// element_interval with the fast path; Rcal = sphere radius reproducing the
+// WD-centre contact (initial guesses only)
+__device__ inline bool element_interval_fast(const Roche& R, double Px, double Py, double Pz, double s,
+                                             double c, double Rcal, double Reff, double& a, double& b)
+{
+    const double ux = 1.0 - Px, uy = -Py, uz = -Pz;
+    const double uxy2 = ux * ux + uy * uy;
+    const double uu = uxy2 + uz * uz;
+    if (uu > R.Rs2 && uxy2 > 0.0 && s > 0.0) {
+        const double uxy = sqrt(uxy2);
+        const double thc = atan2(-uy, ux);
+        const double cosD = (sqrt(uu - R.Rs2) - c * uz) / (s * uxy);
+        if (cosD >= 1.0) { a = 1.0; b = -1.0; return false; }
+        double sc, cc;
+        sincos(thc, &sc, &cc);
+        const double tc = ux * s * cc - uy * s * sc + uz * c;
+        const int ex = cone_exists(R, Px, Py, Pz, s, c, thc, tc);
+        if (ex == 0) { a = 1.0; b = -1.0; return false; }
+        if (ex == 1) {
+            const double Dm = (cosD <= -1.0) ? PI : acos(cosD);
+            const double ce = (sqrt(fmax(uu - Rcal * Rcal, 0.0)) - c * uz) / (s * uxy);
+            const double de = (ce > -1.0 && ce < 1.0) ? acos(ce) : 0.5 * Dm;
+            double thi = thc - de, tti, tho = thc + de, tto;
+            double si, ci, so, co;
+            sincos(thi, &si, &ci);
+            sincos(tho, &so, &co);
+            tti = ux * s * ci - uy * s * si + uz * c;
+            tto = ux * s * co - uy * s * so + uz * c;
+            const bool oki = tangency(R, Px, Py, Pz, s, c, true, thi, tti);
+            const bool oko = tangency(R, Px, Py, Pz, s, c, false, tho, tto);
+            if (oki && oko && thi < tho && thi > thc - Dm && tho < thc + Dm) {
+                a = thi * (1.0 / TWO_PI);
+                b = tho * (1.0 / TWO_PI);
+                return true;
+            }
+        }
+    }
+    return element_interval(R, Px, Py, Pz, s, c, Reff, a, b);
+}
+
 // MODEL_SPEC 4.4: full phase width of the WD-centre eclipse
 __device__ inline int findphi(const Roche& R, double inc_deg, double& dphi)
 {
@@ -317,6 +455,80 @@ __device__ inline int findi(const Roche& R, double dphi, double& inc_deg)
     }
     inc_deg = acos(c) / DEG;
     return ST_OK;
+}
+
+// findphi / findi with the same 2-D tangency Newton, nested solver fallback
+__device__ inline int findphi_fast(const Roche& R, double inc_deg, double& dphi)
+{
+    double s, c;
+    sincos(inc_deg * DEG, &s, &c);
+    const double cosD = sqrt(1.0 - R.Rs2) / s;
+    if (s > 0.0 && cosD < 1.0) {
+        const double Dm = acos(cosD);
+        const double R0 = eggleton(R.q);
+        const double c0 = sqrt(1.0 - R0 * R0) / s;
+        double th = (c0 < 1.0) ? acos(c0) : 0.5 * Dm;
+        double t = s * cos(th);
+        if (tangency(R, 0.0, 0.0, 0.0, s, c, false, th, t) && th > 0.0 && th < Dm) {
+            dphi = th / PI;
+            return ST_OK;
+        }
+    }
+    return findphi(R, inc_deg, dphi);
+}
+
+__device__ inline int findi_fast(const Roche& R, double dphi, double& inc_deg)
+{
+    if (dphi > 0.0 && dphi < 0.5) {
+        double sth, cth;
+        sincos(PI * dphi, &sth, &cth);
+        const double smin = sqrt(1.0 - R.Rs2) / cth;
+        if (cth > 0.0 && smin < 1.0) {
+            const double cmax = sqrt(1.0 - smin * smin);
+            const double R0 = eggleton(R.q);
+            double s0 = fmin(sqrt(1.0 - R0 * R0) / cth, 0.9999);
+            double c = sqrt(1.0 - s0 * s0), t = s0 * cth;
+            for (int it = 0; it < 20; ++it) {
+                const double s = sqrt(1.0 - c * c);
+                const double ex = s * cth, ey = -s * sth;
+                const double x = t * ex, y = t * ey, z = t * c;
+                const double r1s = x * x + y * y + z * z;
+                const double ir1 = rsqrt(r1s), ir1s = ir1 * ir1;
+                const double dx = x - 1.0;
+                const double r2s = dx * dx + y * y + z * z;
+                const double ir2 = rsqrt(r2s), ir2s = ir2 * ir2;
+                const double i1 = R.cA * ir1s * ir1, i2 = R.cB * ir2s * ir2, i12 = i1 + i2;
+                const double xm = x - R.mu;
+                const double phi = -R.cA * ir1 - R.cB * ir2 - xm * xm - y * y;
+                const double gx = i1 * x + i2 * dx - 2.0 * xm, gy = (i12 - 2.0) * y, gz = i12 * z;
+                const double p1 = t, p2 = t - ex;
+                const double k1 = 3.0 * i1 * ir1s, k2 = 3.0 * i2 * ir2s;
+                const double r = c / s;
+                const double ecx = -r * cth, ecy = r * sth;
+                const double F1 = phi - R.pl1, F2 = gx * ex + gy * ey + gz * c;
+                const double gec = gx * ecx + gy * ecy + gz;
+                const double J11 = t * gec, J12 = F2;
+                const double J21 = t * (k2 * p2 * ecx - 2.0 * (ecx * ex + ecy * ey)) + gec;
+                const double J22 = i12 - k1 * p1 * p1 - k2 * p2 * p2 - 2.0 * (ex * ex + ey * ey);
+                const double det = J11 * J22 - J12 * J21;
+                if (!(det != 0.0)) break;
+                double dc = -(F1 * J22 - F2 * J12) / det;
+                const double dt = -(J11 * F2 - J21 * F1) / det;
+                dc = fmin(fmax(dc, -0.05), 0.05);
+                c += dc;
+                t += dt;
+                if (fabs(dc) <= TH_TOL) {
+                    if (J22 > 0.0 && J11 > 0.0 && c >= 0.0 && c < cmax && t > 0.0 && r2s < R.Rs2) {
+                        inc_deg = acos(c) / DEG;
+                        return ST_OK;
+                    }
+                    break;
+                }
+                if (!(c > -0.5 && c < 0.99)) break;
+            }
+        }
+    }
+    return findi(R, dphi, inc_deg);
 }
 
 // MODEL_SPEC 4.5: ballistic stream from L1 to radius rad (trm.roche.bspot)

@@ -56,7 +56,7 @@ def flux_batch(pars, x, width=None, nsub=1, components=False, device=None):
     x_np = np.ascontiguousarray(np.asarray(x, dtype=np.float64).reshape(-1))
     if width is None:
         width = _default_width(x_np)
-    w_np = np.broadcast_to(np.asarray(width, dtype=np.float64), x_np.shape)
+    w_np = np.array(np.broadcast_to(np.asarray(width, dtype=np.float64), x_np.shape))
     x_t = torch.as_tensor(x_np, device=dev)
     w_t = torch.as_tensor(np.ascontiguousarray(w_np), device=dev)
     N = x_t.shape[0]

@@ -26,7 +26,7 @@ def _run(op, a, b=None):
     _native.require_gpu()
     L = _native.lib()
     a_np = np.atleast_1d(np.asarray(a, dtype=np.float64))
-    b_np = np.broadcast_to(np.asarray(b if b is not None else 0.0, dtype=np.float64), a_np.shape)
+    b_np = np.array(np.broadcast_to(np.asarray(b if b is not None else 0.0, dtype=np.float64), a_np.shape))
     dev = torch.device("cuda", torch.cuda.current_device())
     a_t = torch.as_tensor(np.ascontiguousarray(a_np.reshape(-1)), device=dev)
     b_t = torch.as_tensor(np.ascontiguousarray(b_np.reshape(-1)), device=dev)
