@@ -126,6 +126,41 @@ int lfg_elements(const double* pars, int W, int P, double* a, double* b,
 int lfg_roche(int op, const double* a, const double* b, int n, double* out,
               int* status, void* stream);
 
+/*
+ * Same as lfg_lnprob, recording caller-created hipEvent_t events on `stream`
+ * around each kernel: ev[0] before k_setup, ev[1] after k_setup, ev[2] after
+ * k_elements, ev[3] after k_lnlike, ev[4] after k_combine (bench timing).
+ */
+int lfg_lnprob_timed(const double* walkers, int W, const lfg_tree* tree,
+                     double* lnp, double* lnlike_e, void* ws, size_t ws_bytes,
+                     void* stream, void* const* ev);
+
+/*
+ * Device-resident affine-invariant stretch move (Goodman & Weare 2010), the
+ * move of emcee.EnsembleSampler that the reference drives (mcmcfit.py:283-288,
+ * mcmc_utils.py:114-183), with the emcee 2.x fixed red/blue halves:
+ * half h in {0, 1} updates walkers [h W/2, (h+1) W/2) against the other half.
+ * Random numbers come from Philox4x32-10 keyed by `seed` and counted by
+ * (walker, step, half), so every rank of a multi-GPU run draws identical
+ * proposals without communicating.
+ *   pos [dev] W x ndim (updated in place by accept), lnp [dev] W
+ *   q   [dev] W/2 x ndim proposals, zfac [dev] W/2 = (ndim-1) ln z
+ *   lnp_new [dev] W/2 ln_prob of q;  naccept [dev] W acceptance counters
+ */
+int lfg_stretch_propose(const double* pos, int W, int ndim, int half,
+                        double a, unsigned long long seed,
+                        unsigned long long step, double* q, double* zfac,
+                        void* stream);
+int lfg_stretch_accept(double* pos, double* lnp, int W, int ndim, int half,
+                       const double* q, const double* zfac,
+                       const double* lnp_new, unsigned long long seed,
+                       unsigned long long step, int* naccept, void* stream);
+
+/* hipEvent helpers for hosts without a HIP binding (ctypes) */
+int lfg_event_create(void** ev);
+int lfg_event_destroy(void* ev);
+int lfg_event_elapsed_ms(void* start, void* stop, float* ms);
+
 const char* lfg_version(void);
 
 #ifdef __cplusplus

@@ -49,8 +49,10 @@ class LfgTree(ctypes.Structure):
     ]
 
 
-EXPORTS = ("lfg_workspace_size", "lfg_flux", "lfg_lnprob", "lfg_elements",
-           "lfg_roche", "lfg_version")
+EXPORTS = ("lfg_workspace_size", "lfg_flux", "lfg_lnprob", "lfg_lnprob_timed",
+           "lfg_elements", "lfg_roche", "lfg_stretch_propose", "lfg_stretch_accept",
+           "lfg_event_create", "lfg_event_destroy", "lfg_event_elapsed_ms",
+           "lfg_version")
 
 
 def build(force=False, verbose=False):
@@ -97,6 +99,20 @@ def lib():
         L.lfg_elements.argtypes = [vp, ip, ip, vp, vp, vp, vp, vp, vp, vp, sz, vp]
         L.lfg_roche.restype = ip
         L.lfg_roche.argtypes = [ip, vp, vp, ip, vp, vp, vp]
+        L.lfg_lnprob_timed.restype = ip
+        L.lfg_lnprob_timed.argtypes = [vp, ip, ctypes.POINTER(LfgTree), vp, vp, vp, sz, vp,
+                                       ctypes.POINTER(vp)]
+        u64, f64 = ctypes.c_ulonglong, ctypes.c_double
+        L.lfg_stretch_propose.restype = ip
+        L.lfg_stretch_propose.argtypes = [vp, ip, ip, ip, f64, u64, u64, vp, vp, vp]
+        L.lfg_stretch_accept.restype = ip
+        L.lfg_stretch_accept.argtypes = [vp, vp, ip, ip, ip, vp, vp, vp, u64, u64, vp, vp]
+        L.lfg_event_create.restype = ip
+        L.lfg_event_create.argtypes = [ctypes.POINTER(vp)]
+        L.lfg_event_destroy.restype = ip
+        L.lfg_event_destroy.argtypes = [vp]
+        L.lfg_event_elapsed_ms.restype = ip
+        L.lfg_event_elapsed_ms.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_float)]
         L.lfg_version.restype = ctypes.c_char_p
         L.lfg_version.argtypes = []
         _lib = L

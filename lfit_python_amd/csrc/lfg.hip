@@ -518,6 +518,75 @@ __global__ void k_combine(int W, int E, const double* __restrict__ prior, const 
     lnp[w] = lp + ll;
 }
 
+// ------------------------------------------------------- stretch-move sampler
+// Philox4x32-10 (Salmon et al. 2011), counter = (walker, step lo, step hi,
+// half | purpose), key = seed.  Stateless: any rank reproduces any draw.
+__device__ inline uint4 philox(uint4 c, uint2 k)
+{
+    for (int r = 0; r < 10; ++r) {
+        const unsigned lo0 = c.x * 0xD2511F53u, hi0 = __umulhi(c.x, 0xD2511F53u);
+        const unsigned lo1 = c.z * 0xCD9E8D57u, hi1 = __umulhi(c.z, 0xCD9E8D57u);
+        c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+        k.x += 0x9E3779B9u;
+        k.y += 0xBB67AE85u;
+    }
+    return c;
+}
+
+__device__ inline double u53(unsigned a, unsigned b)  // uniform on [0, 1)
+{
+    return double((static_cast<unsigned long long>(a >> 5) << 26) | (b >> 6)) * (1.0 / 9007199254740992.0);
+}
+
+__device__ inline uint4 draw(unsigned long long seed, unsigned long long step, int half, int purpose, int i)
+{
+    return philox(make_uint4(unsigned(i), unsigned(step), unsigned(step >> 32), unsigned(half * 2 + purpose)),
+                  make_uint2(unsigned(seed), unsigned(seed >> 32)));
+}
+
+// emcee StretchMove.get_proposal: z = ((a-1) u + 1)^2 / a,
+// q = c_j - (c_j - s) z = c_j + z (s - c_j), factor = (ndim - 1) ln z
+__global__ void k_propose(const double* __restrict__ pos, int W, int ndim, int half, double a,
+                          unsigned long long seed, unsigned long long step, double* __restrict__ q,
+                          double* __restrict__ zfac)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int ns = W / 2;
+    if (i >= ns) return;
+    const uint4 r = draw(seed, step, half, 0, i);
+    const double u = u53(r.x, r.y);
+    const double zr = (a - 1.0) * u + 1.0;
+    const double z = zr * zr / a;
+    const int j = int(__umulhi(r.z, unsigned(ns)));  // partner in the other half
+    const double* s = pos + size_t(half * ns + i) * ndim;
+    const double* cj = pos + size_t((1 - half) * ns + j) * ndim;
+    double* out = q + size_t(i) * ndim;
+    for (int d = 0; d < ndim; ++d) out[d] = cj[d] - (cj[d] - s[d]) * z;
+    zfac[i] = (ndim - 1.0) * log(z);
+}
+
+// Metropolis acceptance: accept if ln u < factor + lnp_new - lnp_old
+__global__ void k_accept(double* __restrict__ pos, double* __restrict__ lnp, int W, int ndim, int half,
+                         const double* __restrict__ q, const double* __restrict__ zfac,
+                         const double* __restrict__ lnp_new, unsigned long long seed, unsigned long long step,
+                         int* __restrict__ naccept)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int ns = W / 2;
+    if (i >= ns) return;
+    const int w = half * ns + i;
+    const uint4 r = draw(seed, step, half, 1, i);
+    const double lu = log(u53(r.x, r.y));
+    const double diff = zfac[i] + lnp_new[i] - lnp[w];
+    if (lu < diff) {
+        double* p = pos + size_t(w) * ndim;
+        const double* qi = q + size_t(i) * ndim;
+        for (int d = 0; d < ndim; ++d) p[d] = qi[d];
+        lnp[w] = lnp_new[i];
+        if (naccept) naccept[w] += 1;
+    }
+}
+
 // ---------------------------------------------------------------- k_roche
 __global__ void k_roche(int op, const double* __restrict__ a, const double* __restrict__ b, int n,
                         double* __restrict__ out, int* __restrict__ status)
@@ -591,24 +660,97 @@ int lfg_flux(const double* pars, int W, int P, const double* x, const double* w,
     return LFG_OK;
 }
 
-int lfg_lnprob(const double* walkers, int W, const lfg_tree* T, double* lnp, double* lnlike_e, void* wsp,
-               size_t ws_bytes, void* stream)
+static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* lnp, double* lnlike_e, void* wsp,
+                       size_t ws_bytes, void* stream, void* const* ev)
 {
     if (W <= 0 || !T || T->E <= 0 || T->ndim <= 0 || T->nsub < 1 || !walkers || !lnp) return LFG_E_ARGS;
     Ws ws = carve(wsp, W, T->E);
     if (!wsp || ws_bytes < ws.total) return LFG_E_WORKSPACE;
     hipStream_t st = static_cast<hipStream_t>(stream);
+    auto mark = [&](int i) {
+        if (ev && ev[i]) (void)hipEventRecord(static_cast<hipEvent_t>(ev[i]), st);
+    };
     SetupArgs S{walkers, W, T->ndim, T->E, 18, T->gather, T->npars, T->consts, T->prior_type, T->prior_p1,
                 T->prior_p2, T->prior_norm, T->roche_priors, ws.geo, ws.status, ws.prior};
-    int rc = run_front(S, ws, st);
+    const int npairs = W * T->E;
+    const int nlanes = npairs + W;
+    mark(0);
+    hipLaunchKernelGGL(k_setup, dim3((nlanes + SETUP_BLOCK - 1) / SETUP_BLOCK), dim3(SETUP_BLOCK), 0, st, S);
+    int rc = launch_ok();
     if (rc) return rc;
+    mark(1);
+    const long nthreads = long(npairs) * NUNIQ;
+    hipLaunchKernelGGL(k_elements, dim3(unsigned((nthreads + ELEM_BLOCK - 1) / ELEM_BLOCK)), dim3(ELEM_BLOCK), 0,
+                       st, ws.geo, ws.status, npairs, ws.a, ws.b, ws.wgt, ws.donor);
+    if ((rc = launch_ok())) return rc;
+    mark(2);
     double* lle = lnlike_e ? lnlike_e : ws.lle;
     LikeArgs L{ws.geo, ws.status, ws.a, ws.b, ws.wgt, ws.donor, T->E, T->off, T->max_n, T->x, T->y, T->ye,
-               T->w, T->nsub, nullptr, nullptr, lle, W * T->E};
-    hipLaunchKernelGGL(k_lnlike<true>, dim3(W * T->E), dim3(LIKE_BLOCK), 0, st, L);
+               T->w, T->nsub, nullptr, nullptr, lle, npairs};
+    hipLaunchKernelGGL(k_lnlike<true>, dim3(npairs), dim3(LIKE_BLOCK), 0, st, L);
     if ((rc = launch_ok())) return rc;
+    mark(3);
     hipLaunchKernelGGL(k_combine, dim3((W + 255) / 256), dim3(256), 0, st, W, T->E, ws.prior, ws.geo, lle, lnp);
+    rc = launch_ok();
+    mark(4);
+    return rc;
+}
+
+int lfg_lnprob(const double* walkers, int W, const lfg_tree* T, double* lnp, double* lnlike_e, void* wsp,
+               size_t ws_bytes, void* stream)
+{
+    return lnprob_impl(walkers, W, T, lnp, lnlike_e, wsp, ws_bytes, stream, nullptr);
+}
+
+int lfg_lnprob_timed(const double* walkers, int W, const lfg_tree* T, double* lnp, double* lnlike_e, void* wsp,
+                     size_t ws_bytes, void* stream, void* const* ev)
+{
+    return lnprob_impl(walkers, W, T, lnp, lnlike_e, wsp, ws_bytes, stream, ev);
+}
+
+int lfg_stretch_propose(const double* pos, int W, int ndim, int half, double a, unsigned long long seed,
+                        unsigned long long step, double* q, double* zfac, void* stream)
+{
+    if (W < 4 || (W & 1) || ndim <= 0 || (half != 0 && half != 1) || !(a > 1.0) || !pos || !q || !zfac)
+        return LFG_E_ARGS;
+    const int ns = W / 2;
+    hipLaunchKernelGGL(k_propose, dim3((ns + 63) / 64), dim3(64), 0, static_cast<hipStream_t>(stream), pos, W,
+                       ndim, half, a, seed, step, q, zfac);
     return launch_ok();
+}
+
+int lfg_stretch_accept(double* pos, double* lnp, int W, int ndim, int half, const double* q, const double* zfac,
+                       const double* lnp_new, unsigned long long seed, unsigned long long step, int* naccept,
+                       void* stream)
+{
+    if (W < 4 || (W & 1) || ndim <= 0 || (half != 0 && half != 1) || !pos || !lnp || !q || !zfac || !lnp_new)
+        return LFG_E_ARGS;
+    const int ns = W / 2;
+    hipLaunchKernelGGL(k_accept, dim3((ns + 63) / 64), dim3(64), 0, static_cast<hipStream_t>(stream), pos, lnp,
+                       W, ndim, half, q, zfac, lnp_new, seed, step, naccept);
+    return launch_ok();
+}
+
+int lfg_event_create(void** ev)
+{
+    if (!ev) return LFG_E_ARGS;
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return LFG_E_LAUNCH;
+    *ev = static_cast<void*>(e);
+    return LFG_OK;
+}
+
+int lfg_event_destroy(void* ev)
+{
+    return hipEventDestroy(static_cast<hipEvent_t>(ev)) == hipSuccess ? LFG_OK : LFG_E_LAUNCH;
+}
+
+int lfg_event_elapsed_ms(void* start, void* stop, float* ms)
+{
+    if (!ms) return LFG_E_ARGS;
+    return hipEventElapsedTime(ms, static_cast<hipEvent_t>(start), static_cast<hipEvent_t>(stop)) == hipSuccess
+               ? LFG_OK
+               : LFG_E_LAUNCH;
 }
 
 int lfg_elements(const double* pars, int W, int P, double* a, double* b, double* wgt, double* donor,

@@ -1,0 +1,194 @@
+"""Device-resident affine-invariant ensemble sampler.
+
+Stands in for emcee.EnsembleSampler(nwalkers, ndim, ln_prob, args=(model,),
+pool=pool) as the reference drives it (mcmcfit.py:272-343,
+mcmc_utils.py:46-183): the walker ensemble lives in HBM, each emcee step is
+two half-steps (red/blue halves, emcee 2.x fixed split) of
+  propose (HIP, Philox) -> ln_prob of the proposals (one batched lfg_lnprob
+  on this rank's shard) -> all_gather of the new ln_prob -> accept (HIP)
+and nothing crosses PCIe inside the loop.  With torch.distributed
+initialised, every rank holds the full ensemble and draws identical random
+numbers (counter-based Philox keyed by the seed), evaluates only its shard of
+each half and exchanges W/2 doubles per half-step; the accept step is then
+identical on every rank, so positions never travel.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _native
+
+# comp_scat scatter factors (mcmcfit.py:208-232)
+SCATTER_FACTORS = {
+    'ln_ampin_gp': 5.0, 'ln_ampout_gp': 5.0, 'ln_tau_gp': 5.0,
+    'q': 1, 'rwd': 1, 'dphi': 0.2, 'dFlux': 1, 'sFlux': 1, 'wdFlux': 1, 'rsFlux': 1,
+    'rdisc': 1, 'ulimb': 1e-6, 'scale': 1, 'fis': 1, 'dexp': 1, 'phi0': 1, 'az': 1,
+    'exp1': 1, 'exp2': 1, 'yaw': 1, 'tilt': 1,
+}
+
+
+def comp_scatter(names, scatter):
+    """Per-parameter scatter vector of mcmcfit.py:204-246."""
+    from .tree import extract_par_and_key
+    out = np.full(len(names), float(scatter))
+    for i, n in enumerate(names):
+        key, _ = extract_par_and_key(n)
+        if key.startswith('ln'):
+            continue
+        out[i] *= SCATTER_FACTORS[key]
+    return out
+
+
+class EnsembleSampler:
+    def __init__(self, nwalkers, ndim, evaluator, a=2.0, seed=0, group=None):
+        import torch
+        if nwalkers % 2 or nwalkers < 4:
+            raise ValueError("nwalkers must be even and >= 4")
+        self.W, self.ndim, self.a = int(nwalkers), int(ndim), float(a)
+        self.ev = evaluator
+        self.dev = evaluator.device
+        self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        self.L = _native.lib()
+        self.group = group
+        dist = torch.distributed
+        self.world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
+        self.rank = dist.get_rank(group) if self.world > 1 else 0
+        ns = self.W // 2
+        if ns % self.world:
+            raise ValueError("W/2 = %d walkers per half must divide over %d ranks" % (ns, self.world))
+        self.shard = ns // self.world
+        f64 = dict(dtype=torch.float64, device=self.dev)
+        self.pos = torch.empty((self.W, self.ndim), **f64)
+        self.lnp = torch.empty(self.W, **f64)
+        self.q = torch.empty((ns, self.ndim), **f64)
+        self.zfac = torch.empty(ns, **f64)
+        self.lnp_new = torch.empty(ns, **f64)
+        self.naccept = torch.zeros(self.W, dtype=torch.int32, device=self.dev)
+        self.iteration = 0
+        self.chain = None
+        self.lnprob_chain = None
+        self.timer = None  # optional callable(walkers) -> lnp used instead of self.ev
+
+    def _vp(self, t):
+        return ctypes.c_void_p(t.data_ptr())
+
+    def _eval(self, x, out):
+        return (self.timer or self.ev)(x, out=out)
+
+    def set_state(self, p0, lnp0=None):
+        import torch
+        self.pos.copy_(torch.as_tensor(np.asarray(p0), dtype=torch.float64))
+        if lnp0 is None:
+            self.lnp.copy_(self.ln_prob(self.pos))
+        else:
+            self.lnp.copy_(torch.as_tensor(np.asarray(lnp0), dtype=torch.float64))
+        self.naccept.zero_()
+
+    def ln_prob(self, x):
+        """ln_prob of walkers x [n, ndim], sharded over ranks when n divides."""
+        import torch
+        n = x.shape[0]
+        if self.world == 1 or n % self.world:
+            return self.ev(x)
+        k = n // self.world
+        mine = self.ev(x[self.rank * k:(self.rank + 1) * k].contiguous())
+        out = torch.empty(n, dtype=torch.float64, device=self.dev)
+        torch.distributed.all_gather_into_tensor(out, mine, group=self.group)
+        return out
+
+    def step(self):
+        """One emcee iteration: both halves, in place."""
+        import torch
+        stream = _native.stream_ptr(self.dev)
+        for half in (0, 1):
+            rc = self.L.lfg_stretch_propose(self._vp(self.pos), self.W, self.ndim, half, self.a,
+                                            self.seed, self.iteration, self._vp(self.q),
+                                            self._vp(self.zfac), stream)
+            _native.check(rc, "lfg_stretch_propose")
+            if self.world == 1:
+                self._eval(self.q, self.lnp_new)
+            else:
+                lo = self.rank * self.shard
+                mine = self._eval(self.q[lo:lo + self.shard], None)
+                torch.distributed.all_gather_into_tensor(self.lnp_new, mine, group=self.group)
+            rc = self.L.lfg_stretch_accept(self._vp(self.pos), self._vp(self.lnp), self.W, self.ndim,
+                                           half, self._vp(self.q), self._vp(self.zfac),
+                                           self._vp(self.lnp_new), self.seed, self.iteration,
+                                           self._vp(self.naccept), stream)
+            _native.check(rc, "lfg_stretch_accept")
+        self.iteration += 1
+
+    def run_mcmc(self, p0, nsteps, store=True, lnp0=None):
+        """emcee-style run; returns (pos, lnp) as numpy.  With store=True the
+        chain [nsteps, W, ndim] and ln_prob [nsteps, W] stay on the device."""
+        import torch
+        if p0 is not None:
+            self.set_state(p0, lnp0)
+        if store:
+            self.chain = torch.empty((nsteps, self.W, self.ndim), dtype=torch.float64, device=self.dev)
+            self.lnprob_chain = torch.empty((nsteps, self.W), dtype=torch.float64, device=self.dev)
+        for i in range(nsteps):
+            self.step()
+            if store:
+                self.chain[i].copy_(self.pos)
+                self.lnprob_chain[i].copy_(self.lnp)
+        return self.pos.cpu().numpy(), self.lnp.cpu().numpy()
+
+    @property
+    def acceptance_fraction(self):
+        return (self.naccept.double() / max(self.iteration, 1)).cpu().numpy()
+
+    def reset(self):
+        self.iteration = 0
+        self.naccept.zero_()
+        self.chain = self.lnprob_chain = None
+
+
+def initialise_walkers(p, scatter, nwalkers, ln_prob_fn, seed=0, max_rounds=1000):
+    """mcmc_utils.initialise_walkers (mcmc_utils.py:46-72): a Gaussian ball
+    (emcee.utils.sample_ball) resampled until every walker has a finite
+    ln_prior.  ln_prob_fn maps [n, ndim] numpy -> [n] numpy; -inf means invalid."""
+    rng = np.random.default_rng(seed)
+    p = np.asarray(p, dtype=np.float64)
+    std = scatter * p
+    p0 = p + std * rng.standard_normal((nwalkers, len(p)))
+    for _ in range(max_rounds):
+        ok = np.isfinite(ln_prob_fn(p0))
+        nbad = int((~ok).sum())
+        if nbad == 0:
+            return p0
+        good = p0[ok]
+        if len(good) == 0:
+            raise RuntimeError("no valid walker in the initial ball")
+        rep = good[rng.integers(len(good), size=nbad)]
+        rep = rep + 0.5 * rep * scatter * rng.standard_normal(rep.shape)
+        p0[~ok] = rep
+    raise RuntimeError("could not initialise walkers")
+
+
+def write_chain(fname, names, chain, lnprob, mode="w"):
+    """chain_prod.txt in the reference's format (mcmcfit.py:317,
+    mcmc_utils.py:157-164): header `walker_no <names> ln_prob`, then one row
+    per walker per step: '{k:4d} {repr(x) ...} {lnp:f}'."""
+    chain = np.asarray(chain)
+    lnprob = np.asarray(lnprob)
+    with open(fname, mode) as fh:
+        if mode == "w":
+            fh.write("walker_no " + " ".join(names) + " ln_prob\n")
+        for s in range(chain.shape[0]):
+            rows = ["{0:4d} {1:s} {2:f}\n".format(k, " ".join(map(repr, map(float, chain[s, k]))),
+                                                 float(lnprob[s, k]))
+                    for k in range(chain.shape[1])]
+            fh.write("".join(rows))
+
+
+def read_chain(fname):
+    """Inverse of write_chain -> chain [nwalkers, nsteps, npars + 1] like
+    mcmc_utils.readchain (mcmc_utils.py:252-272); last column is ln_prob."""
+    data = np.loadtxt(fname, skiprows=1)
+    nw = int(data[:, 0].max()) + 1
+    ns = data.shape[0] // nw
+    chain = np.full((nw, ns, data.shape[1] - 1), np.nan)
+    for i in range(nw):
+        chain[i] = data[data[:, 0] == i, 1:]
+    return chain
