@@ -13,6 +13,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(_HERE)
 LIB_DIR = os.path.join(_HERE, "_lib")
 LIB_PATH = os.path.join(LIB_DIR, "liblfg_hip.so")
+# diagnostic builds (e.g. -DLFG_PROFILE_SETUP) are loaded through LFG_LIB
+LOAD_PATH = os.environ.get("LFG_LIB", LIB_PATH)
 SOURCES = [os.path.join(_HERE, "csrc", "lfg.hip")]
 HEADERS = [os.path.join(_HERE, "csrc", "lfg_device.hpp"),
            os.path.join(REPO, "include", "lfg.h")]
@@ -83,11 +85,11 @@ def lib():
     with _lock:
         if _lib is not None:
             return _lib
-        if not os.path.exists(LIB_PATH):
+        if not os.path.exists(LOAD_PATH):
             raise RuntimeError(
                 "liblfg_hip.so is missing (%s): run __graft_entry__.build() or "
-                "lfit_python_amd._native.build(); there is no CPU fallback" % LIB_PATH)
-        L = ctypes.CDLL(LIB_PATH)
+                "lfit_python_amd._native.build(); there is no CPU fallback" % LOAD_PATH)
+        L = ctypes.CDLL(LOAD_PATH)
         vp, ip, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
         L.lfg_workspace_size.restype = sz
         L.lfg_workspace_size.argtypes = [ip, ip]

@@ -129,11 +129,20 @@ __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
     if (!finite) st = ST_BAD_ARGS;
     else st = roche_init(R, p[4]);
 
+#ifdef LFG_PROFILE_SETUP
+    // diagnostic build only: phase cycle counts into spare geo slots
+    unsigned long long tp0 = __builtin_amdgcn_s_memtime(), tp1 = tp0, tp2 = tp0, tp3 = tp0;
+#define LFG_STAMP(v) (v) = __builtin_amdgcn_s_memtime()
+#else
+#define LFG_STAMP(v)
+#endif
     double bs[4] = {0.0, 0.0, 0.0, 0.0};
     int bst = ST_BAD_STREAM;
+    LFG_STAMP(tp1);
     if (st == ST_OK) {
         const double rdisc_a = p[6] * R.xl1;
         bst = bspot(R, rdisc_a, bs);
+        LFG_STAMP(tp2);
         // SimpleEclipse.ln_prior Roche checks (CVModel.py:215-316)
         if (rdisc_a > DISC_MAX_A) rprior = -INFINITY;
         const double rwd = p[8], scale = p[9];
@@ -152,6 +161,22 @@ __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
 
     double inc = 0.0;
     if (st == ST_OK) st = findi_fast(R, p[5], inc);
+    LFG_STAMP(tp3);
+#ifdef LFG_PROFILE_SETUP
+    {
+        double mp;
+        const unsigned long long ta = __builtin_amdgcn_s_memtime();
+        findphi_fast(R, 90.0, mp);
+        const unsigned long long tb = __builtin_amdgcn_s_memtime();
+        const double um = bs_umax(p[14], p[15], p[14] * log(pow(p[14] / p[15], 1.0 / p[15])) - p[14] / p[15]);
+        const unsigned long long tc2 = __builtin_amdgcn_s_memtime();
+        G[42] = double(tp1 - tp0);
+        G[43] = double(tp2 - tp1);
+        G[44] = double(tp3 - tp2);
+        G[45] = double(tb - ta);
+        G[46] = double(tc2 - tb) + 0.0 * um;
+    }
+#endif
     const double rwd_a = p[8] * R.xl1, rdisc_a = p[6] * R.xl1;
     if (st == ST_OK && (!(rwd_a > 0.0) || !(rdisc_a > rwd_a) || !(rdisc_a < R.xl1))) st = ST_BAD_GEOMETRY;
     if (st == ST_OK && (!(p[9] > 0.0) || !(p[14] > 0.0) || !(p[15] > 0.0))) st = ST_BAD_GEOMETRY;

@@ -22,9 +22,9 @@ constexpr double TH_TOL = 1e-13;
 constexpr int ROOT_MAXIT = 100;
 constexpr int MIN_MAXIT = 100;
 constexpr double BS_TAIL = 16.0;
-constexpr double STREAM_DELTA = 1e-5;
-constexpr double STREAM_KAPPA = 0.1;
-constexpr double STREAM_DTMAX = 0.1;
+constexpr double STREAM_DELTA = 1e-2;
+constexpr double STREAM_KAPPA = 0.15;
+constexpr double STREAM_DTMAX = 0.15;
 constexpr int STREAM_MAXSTEP = 4000;
 constexpr double DISC_MAX_A = 0.46;  // CVModel.py:217
 constexpr double AZ_SLOPE = 80.0;    // CVModel.py:282
@@ -566,17 +566,36 @@ __device__ inline void hermite(const StreamState& s0, const StreamState& s1, dou
     out[3] = (d00 * s0.y + d01 * s1.y) / dt + d10 * s0.vy + d11 * s1.vy;
 }
 
+// second-order point of the L1 unstable manifold (MODEL_SPEC 4.5)
+__device__ inline StreamState stream_start(const Roche& R)
+{
+    const double x1 = R.xl1;
+    const double m1 = 0.5 * R.cA, m2 = 0.5 * R.cB;
+    const double ix1 = 1.0 / x1, irs = 1.0 / R.Rs;
+    const double K = m1 * ix1 * ix1 * ix1 + m2 * irs * irs * irs;
+    const double Uxx = -2.0 * K - 1.0, Uyy = K - 1.0;
+    const double L = 0.5 * ((K - 2.0) + sqrt((K - 2.0) * (K - 2.0) + 4.0 * (2.0 * K + 1.0) * (K - 1.0)));
+    const double lam = sqrt(L);
+    const double B = -(L - 2.0 * K - 1.0) / (2.0 * lam);
+    const double inrm = rsqrt(1.0 + B * B);
+    const double v0 = -inrm, v1 = B * inrm;
+    const double Uxxx = 6.0 * m1 * ix1 * ix1 * ix1 * ix1 - 6.0 * m2 * irs * irs * irs * irs;
+    const double Uxyy = -0.5 * Uxxx;
+    const double N2x = -0.5 * (Uxxx * v0 * v0 + Uxyy * v1 * v1);
+    const double N2y = -Uxyy * v0 * v1;
+    const double a11 = Uxx + 4.0 * L, a22 = Uyy + 4.0 * L;
+    const double idet = 1.0 / (a11 * a22 + 16.0 * L);
+    const double w0 = (N2x * a22 + 4.0 * lam * N2y) * idet;
+    const double w1 = (a11 * N2y - 4.0 * lam * N2x) * idet;
+    const double d = STREAM_DELTA, d2 = d * d;
+    return StreamState{x1 + d * v0 + d2 * w0, d * v1 + d2 * w1, d * lam * v0 + d2 * 2.0 * lam * w0,
+                       d * lam * v1 + d2 * 2.0 * lam * w1};
+}
+
 __device__ inline int bspot(const Roche& R, double rad, double out[4])
 {
     if (!(rad > 0.0) || !(rad < R.xl1)) return ST_BAD_STREAM;
-    const double q = R.q, x1 = R.xl1;
-    const double K = 1.0 / ((1.0 + q) * x1 * x1 * x1) + q / ((1.0 + q) * R.Rs2 * R.Rs);
-    const double L = 0.5 * ((K - 2.0) + sqrt((K - 2.0) * (K - 2.0) + 4.0 * (2.0 * K + 1.0) * (K - 1.0)));
-    const double lam = sqrt(L);
-    const double A = -1.0, B = (L - 2.0 * K - 1.0) / (2.0 * lam) * A;
-    const double nrm = sqrt(A * A + B * B);
-    StreamState s{x1 + STREAM_DELTA * A / nrm, STREAM_DELTA * B / nrm,
-                  STREAM_DELTA * lam * A / nrm, STREAM_DELTA * lam * B / nrm};
+    StreamState s = stream_start(R);
     double r = sqrt(s.x * s.x + s.y * s.y);
     for (int n = 0; n < STREAM_MAXSTEP; ++n) {
         const double dt = fmin(STREAM_KAPPA * r * sqrt(r), STREAM_DTMAX);
@@ -590,14 +609,22 @@ __device__ inline int bspot(const Roche& R, double rad, double out[4])
                        s.vx + h6 * (k1.vx + 2.0 * k2.vx + 2.0 * k3.vx + k4.vx),
                        s.vy + h6 * (k1.vy + 2.0 * k2.vy + 2.0 * k3.vy + k4.vy)};
         const double rn = sqrt(sn.x * sn.x + sn.y * sn.y);
-        if (rn < rad) {
-            double lo = 0.0, hi = 1.0, p[4];
-            for (int it = 0; it < 60; ++it) {
-                const double m = 0.5 * (lo + hi);
-                hermite(s, sn, dt, m, p);
-                if (sqrt(p[0] * p[0] + p[1] * p[1]) > rad) lo = m; else hi = m;
+        if (rn < rad) {  // Hermite crossing, safeguarded Newton on |H|^2 - rad^2
+            const double r2 = rad * rad;
+            const double f0 = r * r - r2, f1 = rn * rn - r2;
+            double lo = 0.0, hi = 1.0, tau = f0 / (f0 - f1), p[4];
+            for (int it = 0; it < 100; ++it) {
+                hermite(s, sn, dt, tau, p);
+                const double f = p[0] * p[0] + p[1] * p[1] - r2;
+                const double df = 2.0 * dt * (p[0] * p[2] + p[1] * p[3]);
+                if (f > 0.0) lo = tau; else hi = tau;
+                double tn = (df != 0.0) ? tau - f / df : 0.5 * (lo + hi);
+                if (!(tn > lo && tn < hi)) tn = 0.5 * (lo + hi);
+                const double dd = tn - tau;
+                tau = tn;
+                if (fabs(dd) <= 1e-15) break;
             }
-            hermite(s, sn, dt, 0.5 * (lo + hi), out);
+            hermite(s, sn, dt, tau, out);
             return ST_OK;
         }
         if (rn > r && n > 0) return ST_BAD_STREAM;
@@ -608,28 +635,20 @@ __device__ inline int bspot(const Roche& R, double rad, double out[4])
 }
 
 // MODEL_SPEC 5.3: end of the bright-spot strip, F(u) = BS_TAIL below the peak
+// (in v = u^b: G(v) = v - (a/b) ln v - C is convex increasing past its
+// minimum, so Newton from the right converges monotonically; one log per step)
 __device__ inline double bs_umax(double a, double b, double lnpk)
 {
-    const double upk = pow(a / b, 1.0 / b);
-    double lo = upk, hi = 2.0 * upk + 1.0;
-    for (int k = 0; k < 200; ++k) {
-        if (a * log(hi) - pow(hi, b) - lnpk + BS_TAIL < 0.0) break;
-        lo = hi;
-        hi *= 2.0;
-    }
-    double u = 0.5 * (lo + hi);
+    const double k = a / b, C = BS_TAIL - lnpk;
+    double v = fmax(2.0 * k, C + k * log(C + 2.0 * k) + 1.0);
+    for (int it = 0; it < 200 && v - k * log(v) - C <= 0.0; ++it) v *= 2.0;
     for (int it = 0; it < ROOT_MAXIT; ++it) {
-        const double ub = pow(u, b);
-        const double F = a * log(u) - ub - lnpk + BS_TAIL;
-        const double dF = (a - b * ub) / u;
-        if (F > 0.0) lo = u; else hi = u;
-        double un = (dF != 0.0) ? u - F / dF : 0.5 * (lo + hi);
-        if (!(un > lo && un < hi)) un = 0.5 * (lo + hi);
-        const double d = un - u;
-        u = un;
-        if (fabs(d) <= 1e-14 * u) break;
+        const double G = v - k * log(v) - C;
+        const double dv = G / (1.0 - k / v);
+        v -= dv;
+        if (fabs(dv) <= 1e-15 * v) break;
     }
-    return u;
+    return exp(log(v) / b);
 }
 
 // Prior.ln_prob, model.py:83-113 (gauss through log(pdf), as scipy does)

@@ -34,9 +34,9 @@
 #define ROOT_MAXIT     100
 #define MIN_MAXIT      100
 #define BS_TAIL        16.0
-#define STREAM_DELTA   1e-5
-#define STREAM_KAPPA   0.1
-#define STREAM_DTMAX   0.1
+#define STREAM_DELTA   1e-2
+#define STREAM_KAPPA   0.15
+#define STREAM_DTMAX   0.15
 #define STREAM_MAXSTEP 4000
 #define DISC_MAX_A     0.46   /* CVModel.py:217 */
 #define AZ_SLOPE       80.0   /* CVModel.py:282 */
@@ -336,17 +336,41 @@ static void hermite(const double s0[4], const double s1[4], double dt,
     }
 }
 
-static int bspot_R(const Roche* R, double rad, double out[4])
+/* MODEL_SPEC 4.5: start on the unstable manifold of L1 to second order,
+ * x = L1 + d v + d^2 w, with (2 lam I - A) w = N2(v) from the third
+ * derivatives of the potential at L1. */
+static void stream_start(const Roche* R, double s[4])
 {
-    if (!(rad > 0.0) || !(rad < R->xl1)) return LFO_BAD_STREAM;
     double q = R->q, x1 = R->xl1;
-    double K = 1.0 / ((1.0 + q) * x1 * x1 * x1) + q / ((1.0 + q) * R->Rs2 * R->Rs);
+    double m1 = 1.0 / (1.0 + q), m2 = q / (1.0 + q);
+    double K = m1 / (x1 * x1 * x1) + m2 / (R->Rs2 * R->Rs);
+    double Uxx = -2.0 * K - 1.0, Uyy = K - 1.0;
     double L = 0.5 * ((K - 2.0) + sqrt((K - 2.0) * (K - 2.0) + 4.0 * (2.0 * K + 1.0) * (K - 1.0)));
     double lam = sqrt(L);
     double A = -1.0, B = (L - 2.0 * K - 1.0) / (2.0 * lam) * A;
     double nrm = sqrt(A * A + B * B);
-    double s[4] = {x1 + STREAM_DELTA * A / nrm, STREAM_DELTA * B / nrm,
-                   STREAM_DELTA * lam * A / nrm, STREAM_DELTA * lam * B / nrm};
+    double v[4] = {A / nrm, B / nrm, lam * A / nrm, lam * B / nrm};
+    double Uxxx = 6.0 * m1 / (x1 * x1 * x1 * x1) - 6.0 * m2 / (R->Rs2 * R->Rs2);
+    double Uxyy = -0.5 * Uxxx;
+    double N2x = -0.5 * (Uxxx * v[0] * v[0] + Uxyy * v[1] * v[1]);
+    double N2y = -Uxyy * v[0] * v[1];
+    double a11 = Uxx + 4.0 * L, a22 = Uyy + 4.0 * L;
+    double det = a11 * a22 + 16.0 * L;
+    double w0 = (N2x * a22 + 4.0 * lam * N2y) / det;
+    double w1 = (a11 * N2y - 4.0 * lam * N2x) / det;
+    double w[4] = {w0, w1, 2.0 * lam * w0, 2.0 * lam * w1};
+    double d = STREAM_DELTA, d2 = d * d;
+    s[0] = x1 + d * v[0] + d2 * w[0];
+    s[1] = d * v[1] + d2 * w[1];
+    s[2] = d * v[2] + d2 * w[2];
+    s[3] = d * v[3] + d2 * w[3];
+}
+
+static int bspot_R(const Roche* R, double rad, double out[4])
+{
+    if (!(rad > 0.0) || !(rad < R->xl1)) return LFO_BAD_STREAM;
+    double s[4];
+    stream_start(R, s);
     double r = sqrt(s[0] * s[0] + s[1] * s[1]);
     for (int n = 0; n < STREAM_MAXSTEP; ++n) {
         double dt = STREAM_KAPPA * r * sqrt(r);
@@ -363,13 +387,23 @@ static int bspot_R(const Roche* R, double rad, double out[4])
             sn[j] = s[j] + dt / 6.0 * (k1[j] + 2.0 * k2[j] + 2.0 * k3[j] + k4[j]);
         double rn = sqrt(sn[0] * sn[0] + sn[1] * sn[1]);
         if (rn < rad) {
-            double lo = 0.0, hi = 1.0, p[4];
-            for (int it = 0; it < 60; ++it) {
-                double m = 0.5 * (lo + hi);
-                hermite(s, sn, dt, m, p);
-                if (sqrt(p[0] * p[0] + p[1] * p[1]) > rad) lo = m; else hi = m;
+            /* crossing of the cubic Hermite interpolant: safeguarded Newton
+             * on rho(tau) = |H(tau)|^2 - rad^2, rho(0) > 0 > rho(1) */
+            double r2 = rad * rad;
+            double f0 = r * r - r2, f1 = rn * rn - r2;
+            double lo = 0.0, hi = 1.0, tau = f0 / (f0 - f1), p[4];
+            for (int it = 0; it < 100; ++it) {
+                hermite(s, sn, dt, tau, p);
+                double f = p[0] * p[0] + p[1] * p[1] - r2;
+                double df = 2.0 * dt * (p[0] * p[2] + p[1] * p[3]);
+                if (f > 0.0) lo = tau; else hi = tau;
+                double tn = (df != 0.0) ? tau - f / df : 0.5 * (lo + hi);
+                if (!(tn > lo && tn < hi)) tn = 0.5 * (lo + hi);
+                double dd = tn - tau;
+                tau = tn;
+                if (fabs(dd) <= 1e-15) break;
             }
-            hermite(s, sn, dt, 0.5 * (lo + hi), out);
+            hermite(s, sn, dt, tau, out);
             return LFO_OK;
         }
         if (rn > r && n > 0) return LFO_BAD_STREAM; /* passed periastron */
@@ -455,28 +489,20 @@ static int unpack(Model* M, const double* p, int np)
 
 static double bs_profile_root(double a, double b, double lnpk)
 {
-    /* F(u) = a ln u - u^b - lnpk + BS_TAIL, decreasing for u > upk */
-    double upk = pow(a / b, 1.0 / b);
-    double lo = upk, hi = 2.0 * upk + 1.0;
-    for (int k = 0; k < 200; ++k) {
-        double F = a * log(hi) - pow(hi, b) - lnpk + BS_TAIL;
-        if (F < 0.0) break;
-        lo = hi;
-        hi *= 2.0;
-    }
-    double u = 0.5 * (lo + hi);
+    /* end of the strip (MODEL_SPEC 5.3): a ln u - u^b = lnpk - BS_TAIL on
+     * u > upk.  With v = u^b and k = a/b: G(v) = v - k ln v - C = 0,
+     * C = BS_TAIL - lnpk, G convex and increasing for v > k, so Newton from
+     * any v with G(v) > 0 decreases monotonically onto the root. */
+    double k = a / b, C = BS_TAIL - lnpk;
+    double v = fmax(2.0 * k, C + k * log(C + 2.0 * k) + 1.0);
+    for (int it = 0; it < 200 && v - k * log(v) - C <= 0.0; ++it) v *= 2.0;
     for (int it = 0; it < ROOT_MAXIT; ++it) {
-        double ub = pow(u, b);
-        double F = a * log(u) - ub - lnpk + BS_TAIL;
-        double dF = a / u - b * ub / u;
-        if (F > 0.0) lo = u; else hi = u;
-        double un = (dF != 0.0) ? u - F / dF : 0.5 * (lo + hi);
-        if (!(un > lo && un < hi)) un = 0.5 * (lo + hi);
-        double d = un - u;
-        u = un;
-        if (fabs(d) <= 1e-14 * u) break;
+        double G = v - k * log(v) - C;
+        double dv = G / (1.0 - k / v);
+        v -= dv;
+        if (fabs(dv) <= 1e-15 * v) break;
     }
-    return u;
+    return exp(log(v) / b);
 }
 
 static int setup(Model* M)
