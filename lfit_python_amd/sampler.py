@@ -39,8 +39,37 @@ def comp_scatter(names, scatter):
     return out
 
 
+class HipStretchOps:
+    """The stretch move's two device kernels (include/lfg.h)."""
+
+    def __init__(self, device):
+        self.L = _native.lib()
+        self.device = device
+
+    @staticmethod
+    def _vp(t):
+        return ctypes.c_void_p(t.data_ptr())
+
+    def propose(self, pos, half, a, seed, step, q, zfac):
+        W, ndim = pos.shape
+        rc = self.L.lfg_stretch_propose(self._vp(pos), W, ndim, half, a, seed, step, self._vp(q),
+                                        self._vp(zfac), _native.stream_ptr(self.device))
+        _native.check(rc, "lfg_stretch_propose")
+
+    def accept(self, pos, lnp, half, q, zfac, lnp_new, seed, step, naccept):
+        W, ndim = pos.shape
+        rc = self.L.lfg_stretch_accept(self._vp(pos), self._vp(lnp), W, ndim, half, self._vp(q),
+                                       self._vp(zfac), self._vp(lnp_new), seed, step,
+                                       self._vp(naccept), _native.stream_ptr(self.device))
+        _native.check(rc, "lfg_stretch_accept")
+
+
 class EnsembleSampler:
-    def __init__(self, nwalkers, ndim, evaluator, a=2.0, seed=0, group=None):
+    """evaluator(x [n, ndim] tensor, out=None) -> ln_prob [n] on evaluator.device.
+    ops: the propose/accept implementation (HipStretchOps by default; the
+    CPU tests inject a host double to exercise the sharding logic)."""
+
+    def __init__(self, nwalkers, ndim, evaluator, a=2.0, seed=0, group=None, ops=None):
         import torch
         if nwalkers % 2 or nwalkers < 4:
             raise ValueError("nwalkers must be even and >= 4")
@@ -48,7 +77,7 @@ class EnsembleSampler:
         self.ev = evaluator
         self.dev = evaluator.device
         self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
-        self.L = _native.lib()
+        self.ops = ops if ops is not None else HipStretchOps(self.dev)
         self.group = group
         dist = torch.distributed
         self.world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
@@ -69,8 +98,12 @@ class EnsembleSampler:
         self.lnprob_chain = None
         self.timer = None  # optional callable(walkers) -> lnp used instead of self.ev
 
-    def _vp(self, t):
-        return ctypes.c_void_p(t.data_ptr())
+    def _gather(self, out, mine):
+        import torch.distributed as dist
+        if dist.get_backend(self.group) == "nccl":
+            dist.all_gather_into_tensor(out, mine, group=self.group)
+        else:
+            dist.all_gather(list(out.chunk(self.world)), mine, group=self.group)
 
     def _eval(self, x, out):
         return (self.timer or self.ev)(x, out=out)
@@ -93,29 +126,21 @@ class EnsembleSampler:
         k = n // self.world
         mine = self.ev(x[self.rank * k:(self.rank + 1) * k].contiguous())
         out = torch.empty(n, dtype=torch.float64, device=self.dev)
-        torch.distributed.all_gather_into_tensor(out, mine, group=self.group)
+        self._gather(out, mine)
         return out
 
     def step(self):
         """One emcee iteration: both halves, in place."""
-        import torch
-        stream = _native.stream_ptr(self.dev)
         for half in (0, 1):
-            rc = self.L.lfg_stretch_propose(self._vp(self.pos), self.W, self.ndim, half, self.a,
-                                            self.seed, self.iteration, self._vp(self.q),
-                                            self._vp(self.zfac), stream)
-            _native.check(rc, "lfg_stretch_propose")
+            self.ops.propose(self.pos, half, self.a, self.seed, self.iteration, self.q, self.zfac)
             if self.world == 1:
                 self._eval(self.q, self.lnp_new)
             else:
                 lo = self.rank * self.shard
                 mine = self._eval(self.q[lo:lo + self.shard], None)
-                torch.distributed.all_gather_into_tensor(self.lnp_new, mine, group=self.group)
-            rc = self.L.lfg_stretch_accept(self._vp(self.pos), self._vp(self.lnp), self.W, self.ndim,
-                                           half, self._vp(self.q), self._vp(self.zfac),
-                                           self._vp(self.lnp_new), self.seed, self.iteration,
-                                           self._vp(self.naccept), stream)
-            _native.check(rc, "lfg_stretch_accept")
+                self._gather(self.lnp_new, mine)
+            self.ops.accept(self.pos, self.lnp, half, self.q, self.zfac, self.lnp_new, self.seed,
+                            self.iteration, self.naccept)
         self.iteration += 1
 
     def run_mcmc(self, p0, nsteps, store=True, lnp0=None):

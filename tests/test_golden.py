@@ -1,0 +1,153 @@
+"""Host logic against fixtures captured from the reference's own Python
+(tests/golden/README.md): priors, parameter routing, light-curve loading,
+the compiled gather map, and the oracle's batched ln_prob against the
+reference tree's ln_prob."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from lfit_python_amd import batch, cvmodel
+from lfit_python_amd.tree import Prior, extract_par_and_key
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+INPUT = os.path.join(GOLD, "ref_test_data", "mcmc_input.dat")
+
+
+def _same(a, b, rtol=1e-13):
+    a, b = np.asarray(a, float), np.asarray(b, float)
+    assert np.array_equal(np.isfinite(a), np.isfinite(b)), (a, b)
+    assert np.array_equal(a[np.isinf(a)], b[np.isinf(b)])
+    f = np.isfinite(a)
+    np.testing.assert_allclose(a[f], b[f], rtol=rtol, atol=1e-13 if rtol else 0.0)
+
+
+def test_priors_match_reference(oracle):
+    g = json.load(open(os.path.join(GOLD, "priors.json")))
+    for case in g["cases"]:
+        pr = Prior(case["type"], case["p1"], case["p2"])
+        if case["normalise"] is not None:
+            assert abs(pr.normalise - case["normalise"]) <= 1e-12 * abs(case["normalise"])
+        assert pr.p1 == case["p1_used"]
+        _same([pr.ln_prob(v) for v in case["vals"]], case["ln_prob"], rtol=1e-12)
+        # the oracle / device formula of the same prior
+        code = pr.code
+        _same([oracle.prior_lnprob(code, pr.p1, pr.p2, pr.normalise, v) for v in case["vals"]],
+              case["ln_prob"], rtol=1e-12)
+
+
+def test_prior_quirks():
+    # log_uniform normaliser integrates the log-density (model.py:77-79)
+    assert abs(Prior('log_uniform', 0.001, 0.2).normalise - 0.5139798) < 1e-7
+    assert abs(Prior('log_uniform', 0.001, 0.2).ln_prob(0.043) - 3.8121264) < 1e-7
+    assert abs(Prior('gauss', 0.284, 0.001).ln_prob(0.284) - 5.9888167) < 1e-7
+    assert Prior('gauss', 0.284, 0.001).ln_prob(0.284 + 40 * 0.001) == -np.inf
+    assert Prior('uniform', 0.03, 0.5).ln_prob(0.5) == -np.inf          # open interval
+    with pytest.raises(AssertionError):
+        Prior('beta', 0, 1)
+
+
+def test_extract_par_and_key():
+    assert extract_par_and_key("wdFlux_long_complex_key_label") == ("wdFlux", "long_complex_key_label")
+    assert extract_par_and_key("ln_tau_gp_core") == ("ln_tau_gp", "core")
+    assert extract_par_and_key("q_core") == ("q", "core")
+
+
+def test_routing_matches_reference():
+    g = json.load(open(os.path.join(GOLD, "routing.json")))
+    m = cvmodel.construct_model(INPUT)
+    assert type(m).__name__ == g["root"] == "GPLCModel"
+    assert m.dynasty_par_names == g["names"]
+    assert len(g["names"]) == 87
+    _same(m.dynasty_par_vals, g["start"], rtol=0)
+    m.dynasty_par_vals = g["vector"]
+    leaves = m.leaves()
+    assert [l.label for l in leaves] == [e["label"] for e in g["eclipses"]]
+    lcs = np.load(os.path.join(GOLD, "lightcurves.npz"))
+    for leaf, e in zip(leaves, g["eclipses"]):
+        assert leaf.parent.label == e["band"]
+        assert leaf.cv_parnames == e["cv_parnames"]
+        _same(leaf.cv_parlist, e["cv_parlist"], rtol=0)
+        assert leaf.lc.n_data == e["n"]
+        for k in ("x", "y", "ye", "w"):
+            _same(getattr(leaf.lc, k), lcs["%s_%s" % (k, leaf.label)], rtol=0)
+    # yaw/tilt swap: the tree stores yaw before tilt, lfit takes tilt before yaw
+    names = leaves[0].node_par_names
+    assert names.index('yaw') < names.index('tilt')
+    assert leaves[0].cv_parnames.index('tilt') < leaves[0].cv_parnames.index('yaw')
+
+
+def test_gp_tree_routes_but_gp_likelihood_is_out_of_scope():
+    m = cvmodel.construct_model(INPUT)
+    with pytest.raises(NotImplementedError):
+        batch.compile_tree(m)
+
+
+def _tree_from_golden(tag):
+    d = np.load(os.path.join(GOLD, "lnprob_%s.npz" % tag))
+    path = os.path.join(GOLD, "ref_test_data", "mcmc_input_%s.dat" % tag)
+    if not os.path.exists(path):
+        with open(path, "w") as fh:
+            fh.write(str(d["input"]))
+    return d, cvmodel.construct_model(path)
+
+
+@pytest.mark.parametrize("tag", ["tree", "simple"])
+def test_compiled_gather_reproduces_cv_parlists(tag):
+    d, m = _tree_from_golden(tag)
+    assert m.dynasty_par_names == list(d["names"])
+    t = batch.compile_tree(m)
+    assert t.ndim == len(d["names"])
+    assert t.E == (6 if tag == "tree" else 1)
+    for v in d["walkers"][:5]:
+        m.dynasty_par_vals = list(v)
+        for e, leaf in enumerate(m.leaves()):
+            g = t.gather[e, :t.npars[e]]
+            got = np.where(g >= 0, v[np.maximum(g, 0)], t.consts[np.maximum(-1 - g, 0)] if len(t.consts) else 0)
+            _same(got, leaf.cv_parlist, rtol=0)
+    # prior table rows follow the dynasty order
+    for k, name in enumerate(t.names):
+        par = m[name]
+        assert t.prior_type[k] == par.prior.code
+        assert t.prior_p1[k] == par.prior.p1 and t.prior_p2[k] == par.prior.p2
+
+
+def test_fixed_parameters_become_constants():
+    d, m = _tree_from_golden("tree")
+    m['ulimb_g'].isVar = False
+    m['tilt_3'].isVar = False
+    t = batch.compile_tree(m)
+    assert t.ndim == len(d["names"]) - 2
+    assert len(t.consts) == 2 + 1  # ulimb_g feeds both g eclipses, tilt_3 one
+    assert 'ulimb_g' not in t.names and 'tilt_3' not in t.names
+
+
+@pytest.mark.parametrize("tag", ["tree", "simple"])
+def test_oracle_lnprob_matches_reference_tree(oracle, tag):
+    """The oracle's batched ln_prob (the composition the HIP kernels
+    implement) against the reference's own Node.ln_prob on the same walkers
+    (reference flux = oracle flux, so this pins priors, Roche priors,
+    routing and chi^2 composition)."""
+    d, m = _tree_from_golden(tag)
+    t = batch.compile_tree(m)
+    lnp, lle, _ = oracle.lnprob_batch(d["walkers"], t)
+    _same(lnp, d["ln_prob"], rtol=1e-10)
+    fin = np.isfinite(d["ln_prior"])
+    _same(lle.sum(1)[fin], d["ln_like"][fin], rtol=1e-10)
+
+
+def test_chain_file_format(tmp_path):
+    from lfit_python_amd.sampler import read_chain, write_chain
+    rng = np.random.default_rng(1)
+    chain = rng.standard_normal((3, 4, 5))
+    lnp = rng.standard_normal((3, 4))
+    f = tmp_path / "chain_prod.txt"
+    names = ["a_core", "b_g", "c_0", "d_0", "e_0"]
+    write_chain(str(f), names, chain, lnp)
+    lines = f.read_text().splitlines()
+    assert lines[0] == "walker_no a_core b_g c_0 d_0 e_0 ln_prob"
+    assert lines[1].startswith("   0 ")
+    assert len(lines) == 1 + 12
+    back = read_chain(str(f))
+    np.testing.assert_array_equal(back[:, :, :5], np.transpose(chain, (1, 0, 2)))

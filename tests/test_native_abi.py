@@ -1,0 +1,88 @@
+"""The C ABI library without a GPU: it loads, exports every entry point that
+include/lfg.h declares, its struct layout matches the ctypes mirror, and
+argument errors come back as codes.  No kernel is launched here."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from lfit_python_amd import _native
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "lfg.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(lfg_[a-z_]+)\s*\(", text)))
+
+
+def test_header_declares_and_library_exports_everything():
+    names = declared_functions()
+    assert "lfg_flux" in names and "lfg_lnprob" in names and len(names) >= 10
+    L = _native.lib()
+    for n in names:
+        assert hasattr(L, n), n
+    assert set(names) == set(_native.EXPORTS)
+    nm = subprocess.run(["nm", "-D", "--defined-only", _native.LOAD_PATH], capture_output=True,
+                        text=True, check=True).stdout
+    exported = set(re.findall(r" T (lfg_[a-z_]+)", nm))
+    assert set(names) <= exported
+
+
+def test_tree_struct_layout_matches_ctypes(tmp_path):
+    prog = tmp_path / "layout.c"
+    prog.write_text(r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "lfg.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu\n", sizeof(lfg_tree), offsetof(lfg_tree, gather),
+         offsetof(lfg_tree, x), offsetof(lfg_tree, prior_norm), offsetof(lfg_tree, roche_priors));
+  return 0;
+}''')
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(prog)], check=True)
+    got = list(map(int, subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()))
+    T = _native.LfgTree
+    assert got == [ctypes.sizeof(T), T.gather.offset, T.x.offset, T.prior_norm.offset, T.roche_priors.offset]
+
+
+def test_constants_agree_with_header():
+    text = open(HEADER).read()
+    for name, val in (("LFG_NWD", _native.NWD), ("LFG_NDISC", _native.NDISC), ("LFG_NBS", _native.NBS),
+                      ("LFG_NDONOR", _native.NDONOR), ("LFG_NGEO", _native.NGEO)):
+        assert re.search(r"#define %s\s+%d\b" % (name, val), text), name
+
+
+def test_argument_errors_without_gpu():
+    L = _native.lib()
+    assert L.lfg_workspace_size(0, 1) == 0
+    ws1 = L.lfg_workspace_size(1024, 1)
+    assert ws1 > 1024 * (3 * 1500 + 3 * 400) * 8
+    assert L.lfg_workspace_size(2048, 1) > ws1
+    assert L.lfg_flux(None, 0, 18, None, None, 10, 1, None, None, None, None, 0, None) == -1
+    assert L.lfg_flux(ctypes.c_void_p(8), 4, 15, None, None, 10, 1, None, None, None, None, 0, None) == -1
+    # a valid call with too little workspace is refused before any launch
+    assert L.lfg_flux(ctypes.c_void_p(8), 4, 18, ctypes.c_void_p(8), None, 10, 1, ctypes.c_void_p(8),
+                      None, None, ctypes.c_void_p(8), 16, None) == -2
+    assert L.lfg_lnprob(None, 4, None, None, None, None, 0, None) == -1
+    assert L.lfg_stretch_propose(None, 15, 4, 0, 2.0, 1, 0, None, None, None) == -1
+    assert L.lfg_roche(7, None, None, 1, None, None, None) == -1
+    assert L.lfg_version().startswith(b"lfg")
+
+
+def test_product_path_fails_loudly_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from lfit_python_amd import lfit, roche
+    from tests.helpers import TRUTH18
+    with pytest.raises(RuntimeError, match="GPU"):
+        lfit.CV(TRUTH18).calcFlux(TRUTH18, np.linspace(-0.1, 0.1, 11))
+    with pytest.raises(RuntimeError, match="GPU"):
+        roche.xl1(0.1)
