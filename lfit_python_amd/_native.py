@@ -17,6 +17,7 @@ LIB_PATH = os.path.join(LIB_DIR, "liblfg_hip.so")
 LOAD_PATH = os.environ.get("LFG_LIB", LIB_PATH)
 SOURCES = [os.path.join(_HERE, "csrc", "lfg.hip")]
 HEADERS = [os.path.join(_HERE, "csrc", "lfg_device.hpp"),
+           os.path.join(_HERE, "csrc", "lfg_tables.hpp"),
            os.path.join(REPO, "include", "lfg.h")]
 INCLUDE = os.path.join(REPO, "include")
 ARCH = "gfx950"

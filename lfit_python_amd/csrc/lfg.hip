@@ -17,6 +17,7 @@
 
 #include "lfg.h"
 #include "lfg_device.hpp"
+#include "lfg_tables.hpp"
 
 using namespace lfg;
 
@@ -24,7 +25,6 @@ namespace {
 
 constexpr int SETUP_BLOCK = 64;
 constexpr int ELEM_BLOCK = 256;
-constexpr int LIKE_BLOCK = 256;
 
 __device__ const int kIdentityGather[18] = {0, 1, 2, 3, 4, 5, 6, 7, 8,
                                             9, 10, 11, 12, 13, 14, 15, 16, 17};
@@ -32,10 +32,8 @@ __device__ const int kIdentityGather[18] = {0, 1, 2, 3, 4, 5, 6, 7, 8,
 struct Ws {
     double* geo;
     int* status;
-    double* a;
-    double* b;
-    double* wgt;
-    double* donor;
+    double2* ab;    // [pairs][NEL] eclipse intervals (a, b)
+    double* donor;  // [pairs][NDONOR/4][3] symmetry-unique donor tiles
     double* prior;
     double* lle;
     size_t total;
@@ -52,10 +50,8 @@ Ws carve(void* base, int W, int E)
     auto take = [&](size_t bytes) { char* r = p ? p + off : nullptr; off += align256(bytes); return r; };
     ws.geo = reinterpret_cast<double*>(take(pairs * LFG_NGEO * sizeof(double)));
     ws.status = reinterpret_cast<int*>(take(pairs * sizeof(int)));
-    ws.a = reinterpret_cast<double*>(take(pairs * NEL * sizeof(double)));
-    ws.b = reinterpret_cast<double*>(take(pairs * NEL * sizeof(double)));
-    ws.wgt = reinterpret_cast<double*>(take(pairs * NEL * sizeof(double)));
-    ws.donor = reinterpret_cast<double*>(take(pairs * NDONOR * 3 * sizeof(double)));
+    ws.ab = reinterpret_cast<double2*>(take(pairs * NEL * sizeof(double2)));
+    ws.donor = reinterpret_cast<double*>(take(pairs * (NDONOR / 4) * 3 * sizeof(double)));
     ws.prior = reinterpret_cast<double*>(take(size_t(W) * sizeof(double)));
     ws.lle = reinterpret_cast<double*>(take(pairs * sizeof(double)));
     ws.total = off;
@@ -221,13 +217,22 @@ __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
 // Roche potential shares those symmetries, so a mirrored element's eclipse
 // interval is [-b, -a] and a mirrored tile's vector has y (and/or z) negated.
 // Unique items per (walker, eclipse): WD 200, disc 500, spot 100, donor 100.
+// Output: eclipse intervals as (a, b) pairs and the 100 unique donor tile
+// vectors; weights depend on ring only and are formed in k_lnlike.
 constexpr int U_WD = NWD / 2, U_DISC = NDISC / 2, U_BS = NBS, U_DON = NDONOR / 4;
 constexpr int NUNIQ = U_WD + U_DISC + U_BS + U_DON;
 
+__device__ __forceinline__ int wd_ring_of(int u)  // ring of unique WD tile u (ring ir starts at 2 ir^2)
+{
+    int ir = int(sqrt(u * 0.5));
+    if (2 * (ir + 1) * (ir + 1) <= u) ++ir;
+    if (2 * ir * ir > u) --ir;
+    return ir;
+}
+
 __global__ __launch_bounds__(ELEM_BLOCK) void k_elements(const double* __restrict__ geo,
                                                          const int* __restrict__ status, int npairs,
-                                                         double* __restrict__ A, double* __restrict__ B,
-                                                         double* __restrict__ WG, double* __restrict__ DON)
+                                                         double2* __restrict__ AB, double* __restrict__ DON)
 {
     const long t = long(blockIdx.x) * ELEM_BLOCK + threadIdx.x;
     const int pair = int(t / NUNIQ);
@@ -241,13 +246,8 @@ __global__ __launch_bounds__(ELEM_BLOCK) void k_elements(const double* __restric
     if (u >= U_WD + U_DISC + U_BS) {  // donor tile (MODEL_SPEC 5.4), phi' in (0, pi/2)
         const int uu = u - (U_WD + U_DISC + U_BS);
         const int it = uu / (NDONOR_P / 4), ip = uu - it * (NDONOR_P / 4);
-        const double t0 = PI * it / NDONOR_T, t1 = PI * (it + 1) / NDONOR_T;
-        const double tc = 0.5 * (t0 + t1);
-        const double dOm = (cos(t0) - cos(t1)) * (TWO_PI / NDONOR_P);
-        double stc, ctc, sph, cph;
-        sincos(tc, &stc, &ctc);
-        sincos(TWO_PI * (ip + 0.5) / NDONOR_P, &sph, &cph);
-        const double dx = -ctc, dy = stc * cph, dz = stc * sph;
+        const double stc = kDonSt[it], ctc = kDonCt[it];
+        const double dx = -ctc, dy = stc * kDonCp[ip], dz = stc * kDonSp[ip];
         double lo = 0.0, hi = R.Rs, r = G[G_REFF];
         if (!(r > lo && r < hi)) r = 0.5 * hi;
         double gx, gy, gz;
@@ -266,42 +266,25 @@ __global__ __launch_bounds__(ELEM_BLOCK) void k_elements(const double* __restric
         rgrad(R, fma(r, dx, 1.0), r * dy, r * dz, gx, gy, gz);
         const double ig = rsqrt(gx * gx + gy * gy + gz * gz);
         const double nx = gx * ig, ny = gy * ig, nz = gz * ig;
-        const double dA = r * r * dOm / (nx * dx + ny * dy + nz * dz);
-        const double vx = dA * nx, vy = dA * ny, vz = dA * nz;
-        // mirrors of p: z -> -z is 19-p, y -> -y is 9-p, both is 10+p
-        const int base = it * NDONOR_P;
-        double* D = DON + size_t(pair) * NDONOR * 3;
-        const int ks[4] = {base + ip, base + NDONOR_P - 1 - ip, base + NDONOR_P / 2 - 1 - ip,
-                           base + NDONOR_P / 2 + ip};
-        const double sy[4] = {1.0, 1.0, -1.0, -1.0}, sz[4] = {1.0, -1.0, 1.0, -1.0};
-        for (int m = 0; m < 4; ++m) {
-            D[3 * ks[m]] = vx;
-            D[3 * ks[m] + 1] = sy[m] * vy;
-            D[3 * ks[m] + 2] = sz[m] * vz;
-        }
+        const double dA = r * r * kDonOmega[it] / (nx * dx + ny * dy + nz * dz);
+        double* D = DON + (size_t(pair) * U_DON + uu) * 3;
+        D[0] = dA * nx;
+        D[1] = dA * ny;
+        D[2] = dA * nz;
         return;
     }
 
-    double Px, Py, Pz, wk;
+    double Px, Py, Pz;
     int k, km;
-    if (u < U_WD) {  // white dwarf tile (MODEL_SPEC 5.1): ring ir holds 2(2ir+1) unique tiles
-        int ir = int(sqrt(u * 0.5));
-        if (2 * (ir + 1) * (ir + 1) <= u) ++ir;
-        if (2 * ir * ir > u) --ir;
+    if (u < U_WD) {  // white dwarf tile (MODEL_SPEC 5.1), cos(psi) > 0 half
+        const int ir = wd_ring_of(u);
         const int nk = 4 * (2 * ir + 1), q4 = nk / 4, jj = u - 2 * ir * ir;
-        const int j = (jj < q4) ? jj : jj - q4 + 3 * q4;  // cos(psi) > 0 half
+        const int j = (jj < q4) ? jj : jj - q4 + 3 * q4;
         const int jm = (j < nk / 2) ? nk / 2 - 1 - j : 3 * nk / 2 - 1 - j;
         k = 4 * ir * ir + j;
         km = 4 * ir * ir + jm;
-        const double ul = G[G_ULIMB];
-        const double r0 = double(ir) / NWD_RINGS, r1 = double(ir + 1) / NWD_RINGS;
-        const double F0 = (1.0 - ul) * 0.5 * r0 * r0 - ul * pow(1.0 - r0 * r0, 1.5) / 3.0;
-        const double F1 = (1.0 - ul) * 0.5 * r1 * r1 - ul * pow(1.0 - r1 * r1, 1.5) / 3.0;
-        wk = (TWO_PI / nk) * (F1 - F0);
-        const double rc = sqrt(0.5 * (r0 * r0 + r1 * r1));
-        const double mu0 = sqrt(1.0 - rc * rc);
-        double sp, cp;
-        sincos(TWO_PI * (j + 0.5) / nk, &sp, &cp);
+        const double rc = kWdRc[ir], mu0 = kWdMu0[ir];
+        const double cp = kWdCos[u], sp = kWdSin[u];
         const double rw = G[G_RWD];
         Px = rw * (-rc * sp * c + mu0 * s);
         Py = rw * (rc * cp);
@@ -312,38 +295,96 @@ __global__ __launch_bounds__(ELEM_BLOCK) void k_elements(const double* __restric
         k = NWD + ir * NDISC_AZ + j;
         km = NWD + ir * NDISC_AZ + NDISC_AZ - 1 - j;
         const double rin = G[G_RWD];
-        const double dr = (G[G_RDISC] - rin) / NDISC_R;
-        const double r0 = rin + ir * dr, r1 = rin + (ir + 1) * dr;
-        const double rc = 0.5 * (r0 + r1);
-        const double ex = 2.0 - G[G_DEXP];
-        const double I = (fabs(ex) < 1e-10) ? log(r1 / r0) : (pow(r1, ex) - pow(r0, ex)) / ex;
-        wk = (TWO_PI / NDISC_AZ) * I;
-        double sa, ca;
-        sincos(TWO_PI * (j + 0.5) / NDISC_AZ, &sa, &ca);
-        Px = rc * ca;
-        Py = rc * sa;
+        const double rc = rin + (ir + 0.5) * ((G[G_RDISC] - rin) / NDISC_R);
+        Px = rc * kDiscCos[j];
+        Py = rc * kDiscSin[j];
         Pz = 0.0;
     } else {  // bright-spot strip (MODEL_SPEC 5.3): no mirror partner
         const int j = u - U_WD - U_DISC;
         k = km = NWD + NDISC + j;
         const double uk = (j + 0.5) * (G[G_UMAX] / NBS);
-        wk = exp(G[G_EXP1] * log(uk) - pow(uk, G[G_EXP2]) - G[G_LNPK]);
         const double off = G[G_L] * (uk - G[G_UPK]);
         Px = fma(off, G[G_CAZ], G[G_BSX]);
         Py = fma(off, G[G_SAZ], G[G_BSY]);
         Pz = 0.0;
     }
     double a, b;
+#ifdef LFG_MARK_FALLBACK
+    bool fb = false;  // diagnostic build: NaN-tagged b marks a slow-path element
+    element_interval_fast(R, Px, Py, Pz, s, c, G[G_RCAL], G[G_REFF], a, b, &fb);
+    if (fb) a = -a - 10.0;
+#else
     element_interval_fast(R, Px, Py, Pz, s, c, G[G_RCAL], G[G_REFF], a, b);
+#endif
     const size_t o = size_t(pair) * NEL;
-    A[o + k] = a;
-    B[o + k] = b;
-    WG[o + k] = wk;
+    AB[o + k] = make_double2(a, b);
     if (km != k) {
         const bool ecl = a < b;
-        A[o + km] = ecl ? -b : 1.0;
-        B[o + km] = ecl ? -a : -1.0;
-        WG[o + km] = wk;
+        AB[o + km] = ecl ? make_double2(-b, -a) : make_double2(1.0, -1.0);
+    }
+}
+
+// element weights (MODEL_SPEC 5.1-5.3): per WD ring, per disc ring, per spot element
+__device__ inline double wd_ring_weight(int ir, double ul) { return fma(kWdA[ir], 1.0 - ul, kWdB[ir] * ul); }
+
+// radial integral of r^(1 - dexp) dr over the disc annuli (MODEL_SPEC 5.2):
+// the boundary term P(r) = r^ex / ex, or ln r when ex = 2 - dexp vanishes
+__device__ inline double disc_boundary(int i, const double* G)
+{
+    const double rin = G[G_RWD];
+    const double r = rin + i * ((G[G_RDISC] - rin) / NDISC_R);
+    const double ex = 2.0 - G[G_DEXP];
+    return (fabs(ex) < 1e-10) ? log(r) : pow(r, ex) / ex;
+}
+
+__device__ inline double disc_ring_weight(int ir, const double* G)
+{
+    return (TWO_PI / NDISC_AZ) * (disc_boundary(ir + 1, G) - disc_boundary(ir, G));
+}
+
+__device__ inline double bs_weight(int j, const double* G)
+{
+    const double uk = (j + 0.5) * (G[G_UMAX] / NBS);
+    return exp(G[G_EXP1] * log(uk) - pow(uk, G[G_EXP2]) - G[G_LNPK]);
+}
+
+// test/inspection only: per-element weights and the full 400-tile donor
+__global__ void k_expand(const double* __restrict__ geo, const int* __restrict__ status, int npairs,
+                         const double2* __restrict__ AB, const double* __restrict__ DON, double* __restrict__ A,
+                         double* __restrict__ B, double* __restrict__ WG, double* __restrict__ DFULL)
+{
+    const long t = long(blockIdx.x) * blockDim.x + threadIdx.x;
+    const int pair = int(t / NEL), k = int(t - long(pair) * NEL);
+    if (pair >= npairs || status[pair] != ST_OK) return;
+    const double* G = geo + size_t(pair) * LFG_NGEO;
+    const double2 ab = AB[size_t(pair) * NEL + k];
+    if (A) A[size_t(pair) * NEL + k] = ab.x;
+    if (B) B[size_t(pair) * NEL + k] = ab.y;
+    double w;
+    if (k < NWD) {
+        int ir = int(sqrt(k * 0.25));
+        if (4 * (ir + 1) * (ir + 1) <= k) ++ir;
+        if (4 * ir * ir > k) --ir;
+        w = wd_ring_weight(ir, G[G_ULIMB]);
+    } else if (k < NWD + NDISC) {
+        w = disc_ring_weight((k - NWD) / NDISC_AZ, G);
+    } else {
+        w = bs_weight(k - NWD - NDISC, G);
+    }
+    if (WG) WG[size_t(pair) * NEL + k] = w;
+    if (DFULL && k < U_DON) {
+        const int it = k / (NDONOR_P / 4), ip = k - it * (NDONOR_P / 4);
+        const double* v = DON + (size_t(pair) * U_DON + k) * 3;
+        const int base = it * NDONOR_P;
+        const int ks[4] = {base + ip, base + NDONOR_P - 1 - ip, base + NDONOR_P / 2 - 1 - ip,
+                           base + NDONOR_P / 2 + ip};
+        const double sy[4] = {1.0, 1.0, -1.0, -1.0}, sz[4] = {1.0, -1.0, 1.0, -1.0};
+        double* D = DFULL + size_t(pair) * NDONOR * 3;
+        for (int m = 0; m < 4; ++m) {
+            D[3 * ks[m]] = v[0];
+            D[3 * ks[m] + 1] = sy[m] * v[1];
+            D[3 * ks[m] + 2] = sz[m] * v[2];
+        }
     }
 }
 
@@ -353,23 +394,11 @@ __device__ __forceinline__ double wave_sum(double v)
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
     return v;
 }
-__device__ __forceinline__ double wave_min(double v)
-{
-    for (int off = 32; off > 0; off >>= 1) v = fmin(v, __shfl_xor(v, off, 64));
-    return v;
-}
-__device__ __forceinline__ double wave_max(double v)
-{
-    for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
-    return v;
-}
 
 struct LikeArgs {
     const double* geo;
     const int* status;
-    const double* A;
-    const double* B;
-    const double* WG;
+    const double2* AB;
     const double* DON;
     int E;
     const int* off;  // nullptr: every pair uses x[0..N)
@@ -385,13 +414,145 @@ struct LikeArgs {
     int npairs;
 };
 
-template <bool CHI>
-__global__ __launch_bounds__(LIKE_BLOCK) void k_lnlike(LikeArgs L)
-{
-    __shared__ double sa[NEL], sb[NEL], sw[NEL];
-    __shared__ double sd[NDONOR * 3];
-    __shared__ double red[5][LIKE_BLOCK / 64];
+// element groups with their own [min a, max b] window: 10 WD rings, 20 disc
+// rings, 5 spot blocks of 20 -- a point only scans the groups it overlaps
+constexpr int NG_WD = NWD_RINGS, NG_DISC = NDISC_R, NG_BS = 5, NGROUP = NG_WD + NG_DISC + NG_BS;
 
+__device__ __forceinline__ int group_start(int g)
+{
+    return g < NG_WD ? 4 * g * g : (g < NG_WD + NG_DISC ? NWD + (g - NG_WD) * NDISC_AZ
+                                                       : NWD + NDISC + (g - NG_WD - NG_DISC) * (NBS / NG_BS));
+}
+
+__device__ __forceinline__ double ov1(double2 e, double lo, double hi)
+{
+    return fmax(fmin(e.y, hi) - fmax(e.x, lo), 0.0);
+}
+
+// sum over k in [k0, k1) of |[a_k, b_k] n [lo, hi]|; four independent chains
+// keep four 128-bit LDS reads in flight
+__device__ __forceinline__ double overlap_sum(const double2* __restrict__ ab, int k0, int k1, double lo,
+                                              double hi)
+{
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    int k = k0;
+#pragma unroll 1
+    for (; k + 3 < k1; k += 4) {
+        const double2 e0 = ab[k], e1 = ab[k + 1], e2 = ab[k + 2], e3 = ab[k + 3];
+        s0 += ov1(e0, lo, hi);
+        s1 += ov1(e1, lo, hi);
+        s2 += ov1(e2, lo, hi);
+        s3 += ov1(e3, lo, hi);
+    }
+#pragma unroll 1
+    for (; k < k1; ++k) s0 += ov1(ab[k], lo, hi);
+    return (s0 + s1) + (s2 + s3);
+}
+
+// weighted variant for the spot strip (per-element weights wt[k - k0])
+__device__ __forceinline__ double overlap_wsum(const double2* __restrict__ ab, const double* __restrict__ wt,
+                                               int k0, int k1, double lo, double hi)
+{
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    int k = k0;
+#pragma unroll 1
+    for (; k + 3 < k1; k += 4) {
+        const double2 e0 = ab[k], e1 = ab[k + 1], e2 = ab[k + 2], e3 = ab[k + 3];
+        const int i = k - k0;
+        s0 = fma(wt[i], ov1(e0, lo, hi), s0);
+        s1 = fma(wt[i + 1], ov1(e1, lo, hi), s1);
+        s2 = fma(wt[i + 2], ov1(e2, lo, hi), s2);
+        s3 = fma(wt[i + 3], ov1(e3, lo, hi), s3);
+    }
+#pragma unroll 1
+    for (; k < k1; ++k) s0 = fma(wt[k - k0], ov1(ab[k], lo, hi), s0);
+    return (s0 + s1) + (s2 + s3);
+}
+
+// bit g set when group g's eclipse window meets [lo, hi]
+__device__ __forceinline__ unsigned long long group_mask(const double2* __restrict__ gb, int g0, int g1, double lo,
+                                                         double hi)
+{
+    unsigned long long m = 0;
+#pragma unroll 5
+    for (int g = g0; g < g1; ++g) {
+        const double2 b = gb[g];
+        m |= (hi >= b.x && lo <= b.y) ? (1ull << g) : 0ull;
+    }
+    return m;
+}
+
+__device__ __forceinline__ double inside_count(const double2* __restrict__ ab, const double* wt, int k0, int k1,
+                                               double ph)
+{
+    double s = 0.0;
+    for (int k = k0; k < k1; ++k) s += (ph > ab[k].x && ph < ab[k].y) ? (wt ? wt[k - k0] : 1.0) : 0.0;
+    return s;
+}
+
+// ---- sweep over a phase-sorted tile of points (MODEL_SPEC 6.1 restated) ----
+// With lo_p = phase_p - w_p and hi_p = phase_p + w_p both non-decreasing in p,
+// the points an element [a, b] overlaps form the contiguous range [P1, P4),
+// and those it covers whole form [P2, P3):
+//   P1 = #{hi <= a}, P2 = #{lo < a}, P3 = #{hi <= b}, P4 = #{lo < b}.
+// Covered points gain the element's normalised weight through a difference
+// array; the (few) partly covered points gain w |[a,b] n [lo,hi]| / (hi - lo)
+// directly.  Contributions are 2^-61 fixed point in int64 so that LDS atomics
+// sum them exactly and the result is independent of summation order.
+constexpr int LIKE_THREADS = 256;
+constexpr int LIKE_TILE = 2 * LIKE_THREADS;  // points per sweep tile
+constexpr double FX_SCALE = 2305843009213693952.0;  // 2^61
+constexpr double FX_INV = 1.0 / FX_SCALE;
+
+__device__ __forceinline__ void count4(const double* __restrict__ lo, const double* __restrict__ hi, int m,
+                                       double a, double b, int& P1, int& P2, int& P3, int& P4)
+{
+    // branch-free lower bounds; the trip count depends on m only (wave-uniform)
+    int b1 = 0, b2 = 0, b3 = 0, b4 = 0, len = m;
+    while (len > 1) {
+        const int half = len >> 1;
+        b1 += (hi[b1 + half - 1] <= a) ? half : 0;
+        b2 += (lo[b2 + half - 1] < a) ? half : 0;
+        b3 += (hi[b3 + half - 1] <= b) ? half : 0;
+        b4 += (lo[b4 + half - 1] < b) ? half : 0;
+        len -= half;
+    }
+    P1 = b1 + (hi[b1] <= a);
+    P2 = b2 + (lo[b2] < a);
+    P3 = b3 + (hi[b3] <= b);
+    P4 = b4 + (lo[b4] < b);
+}
+
+__device__ __forceinline__ void fx_add(unsigned long long* acc, int p, long long q)
+{
+    atomicAdd(acc + p, static_cast<unsigned long long>(q));
+}
+
+__device__ __forceinline__ long long wave_scan_incl(long long v, int lane)
+{
+    for (int off = 1; off < 64; off <<= 1) {
+        const long long u = __shfl_up(v, off, 64);
+        if (lane >= off) v += u;
+    }
+    return v;
+}
+
+template <bool CHI>
+__global__ __launch_bounds__(LIKE_THREADS) void k_lnlike(LikeArgs L)
+{
+    __shared__ double2 sab[NEL];
+    __shared__ double sbw[NBS];
+    __shared__ double swr[NG_WD + NG_DISC];
+    __shared__ double sdb[NDISC_R + 1];
+    __shared__ double2 sgb[NGROUP];
+    __shared__ double2 sdxy[U_DON];
+    __shared__ double sdz[U_DON];
+    __shared__ double slo[LIKE_TILE], shi[LIKE_TILE];
+    __shared__ unsigned long long sacc[2][LIKE_TILE + 1];
+    __shared__ long long sscan[2][LIKE_THREADS / 64];
+    __shared__ double red[4][LIKE_THREADS / 64];
+
+    constexpr int nt = LIKE_THREADS, nw = LIKE_THREADS / 64;
     const int pair = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int e = pair % L.E;
@@ -399,7 +560,7 @@ __global__ __launch_bounds__(LIKE_BLOCK) void k_lnlike(LikeArgs L)
     const int n = L.off ? L.off[e + 1] - o0 : L.N;
     const int st = L.status[pair];
     if (st != ST_OK) {
-        for (int p = tid; p < n; p += LIKE_BLOCK) {
+        for (int p = tid; p < n; p += nt) {
             if (L.flux) L.flux[size_t(pair) * n + p] = NAN;
             if (L.comps)
                 for (int m = 0; m < 4; ++m) L.comps[(size_t(m) * L.npairs + pair) * n + p] = NAN;
@@ -410,116 +571,227 @@ __global__ __launch_bounds__(LIKE_BLOCK) void k_lnlike(LikeArgs L)
     const double* G = L.geo + size_t(pair) * LFG_NGEO;
     const double s = G[G_S], c = G[G_C];
 
-    // stage element tables in LDS; per-component totals, eclipse window
-    double twd = 0.0, td = 0.0, tb = 0.0, amin = INFINITY, bmax = -INFINITY, dn = 0.0;
-    const double* Ap = L.A + size_t(pair) * NEL;
-    const double* Bp = L.B + size_t(pair) * NEL;
-    const double* Wp = L.WG + size_t(pair) * NEL;
-    for (int k = tid; k < NEL; k += LIKE_BLOCK) {
-        const double a = Ap[k], b = Bp[k], wg = Wp[k];
-        sa[k] = a;
-        sb[k] = b;
-        sw[k] = wg;
-        if (k < NWD) twd += wg; else if (k < NWD + NDISC) td += wg; else tb += wg;
-        if (a < b) { amin = fmin(amin, a); bmax = fmax(bmax, b); }
+    // stage: intervals, spot weights, disc annulus boundaries, donor quads
+    const double2* ABp = L.AB + size_t(pair) * NEL;
+    for (int k = tid; k < NEL; k += nt) sab[k] = ABp[k];
+    double tb = 0.0, dn = 0.0;
+    for (int i = tid; i < NBS + NDISC_R + 1 + NG_WD; i += nt) {
+        if (i < NBS) {
+            const double w = bs_weight(i, G);
+            sbw[i] = w;
+            tb += w;
+        } else if (i < NBS + NDISC_R + 1) {
+            sdb[i - NBS] = disc_boundary(i - NBS, G);
+        } else {
+            swr[i - NBS - NDISC_R - 1] = wd_ring_weight(i - NBS - NDISC_R - 1, G[G_ULIMB]);
+        }
     }
-    const double* Dp = L.DON + size_t(pair) * NDONOR * 3;
-    for (int k = tid; k < NDONOR; k += LIKE_BLOCK) {
-        const double vx = Dp[3 * k], vy = Dp[3 * k + 1], vz = Dp[3 * k + 2];
-        sd[k] = vx;
-        sd[NDONOR + k] = vy;
-        sd[2 * NDONOR + k] = vz;
-        dn += fmax(-s * vy + c * vz, 0.0);
+    const double* Dp = L.DON + size_t(pair) * U_DON * 3;
+    for (int q = tid; q < U_DON; q += nt) {
+        const double vx = Dp[3 * q], vy = Dp[3 * q + 1], vz = Dp[3 * q + 2];
+        sdxy[q] = make_double2(vx, vy);
+        const double zc = vz * c;
+        sdz[q] = zc;
+        // donor normalisation at quadrature (theta = pi/2): X = +-vz c, Y = vy s
+        const double ay = fabs(vy * s);
+        dn += fmax(zc + ay, 0.0) + fmax(zc - ay, 0.0) + fmax(-zc + ay, 0.0) + fmax(-zc - ay, 0.0);
     }
-    twd = wave_sum(twd); td = wave_sum(td); tb = wave_sum(tb);
-    amin = wave_min(amin); bmax = wave_max(bmax); dn = wave_sum(dn);
-    if (lane == 0) { red[0][wv] = twd; red[1][wv] = td; red[2][wv] = tb; red[3][wv] = dn; }
-    __shared__ double rmin[LIKE_BLOCK / 64], rmax[LIKE_BLOCK / 64];
-    if (lane == 0) { rmin[wv] = amin; rmax[wv] = bmax; }
+    tb = wave_sum(tb);
+    dn = wave_sum(dn);
+    if (lane == 0) { red[0][wv] = tb; red[1][wv] = dn; }
     __syncthreads();
-    twd = td = tb = dn = 0.0;
-    amin = INFINITY;
-    bmax = -INFINITY;
-    for (int i = 0; i < LIKE_BLOCK / 64; ++i) {
-        twd += red[0][i]; td += red[1][i]; tb += red[2][i]; dn += red[3][i];
-        amin = fmin(amin, rmin[i]);
-        bmax = fmax(bmax, rmax[i]);
+    if (tid < NDISC_R) swr[NG_WD + tid] = (TWO_PI / NDISC_AZ) * (sdb[tid + 1] - sdb[tid]);
+    for (int g = wv; g < NGROUP; g += nw) {  // eclipse window of each group, one wave per group
+        const int k0 = group_start(g), k1 = group_start(g + 1);
+        double lo = INFINITY, hi = -INFINITY;
+        for (int k = k0 + lane; k < k1; k += 64) {
+            const double2 ab = sab[k];
+            if (ab.x < ab.y) { lo = fmin(lo, ab.x); hi = fmax(hi, ab.y); }
+        }
+        for (int sh = 32; sh > 0; sh >>= 1) {
+            lo = fmin(lo, __shfl_xor(lo, sh, 64));
+            hi = fmax(hi, __shfl_xor(hi, sh, 64));
+        }
+        if (lane == 0) sgb[g] = make_double2(lo, hi);
     }
+    // totals telescope: WD 2 pi [F(1) - F(0)], disc 2 pi [P(rdisc) - P(rin)]
+    const double ul = G[G_ULIMB];
+    const double twd = TWO_PI * ((1.0 - ul) * 0.5 + ul / 3.0);
+    const double td = TWO_PI * (sdb[NDISC_R] - sdb[0]);
+    tb = dn = 0.0;
+    for (int i = 0; i < nw; ++i) { tb += red[0][i]; dn += red[1][i]; }
+    __syncthreads();
+    const double iwd = 1.0 / twd, id = 1.0 / td;
 
     const double wdF = G[G_WDF], dF = G[G_DF], sF = G[G_SF], rsF = G[G_RSF];
     const double phi0 = G[G_PHI0], fis = G[G_FIS], bden = G[G_BDEN];
     const double nb0 = G[G_NB0], nb1 = G[G_NB1], nb2 = G[G_NB2];
     const int S = L.nsub;
     double chi = 0.0;
-    for (int p = tid; p < n; p += LIKE_BLOCK) {
-        const double xk = L.x[o0 + p];
-        const double wk = L.w ? L.w[o0 + p] : 0.0;
-        const double ph0 = xk - phi0;
-        const double phc = ph0 - floor(ph0 + 0.5);
-        const double lo = phc - wk, hi = phc + wk;
-        double ewd = 0.0, ed = 0.0;
-        const bool inwin = (hi >= amin) && (lo <= bmax);
-        if (inwin) {
-            if (wk > 0.0) {
-                for (int k = 0; k < NWD; ++k) ewd = fma(sw[k], fmax(fmin(sb[k], hi) - fmax(sa[k], lo), 0.0), ewd);
-                for (int k = NWD; k < NWD + NDISC; ++k) ed = fma(sw[k], fmax(fmin(sb[k], hi) - fmax(sa[k], lo), 0.0), ed);
-                ewd /= 2.0 * wk;
-                ed /= 2.0 * wk;
-            } else {
-                for (int k = 0; k < NWD; ++k) ewd += (phc > sa[k] && phc < sb[k]) ? sw[k] : 0.0;
-                for (int k = NWD; k < NWD + NDISC; ++k) ed += (phc > sa[k] && phc < sb[k]) ? sw[k] : 0.0;
-            }
+    for (int t0 = 0; t0 < n; t0 += LIKE_TILE) {
+        const int m = min(LIKE_TILE, n - t0);
+        // tile phases; the sweep needs lo, hi non-decreasing and widths > 0
+        int bad = 0;
+        for (int i = tid; i < m; i += nt) {
+            const int p = o0 + t0 + i;
+            const double wk = L.w ? L.w[p] : 0.0;
+            const double ph0 = L.x[p] - phi0;
+            const double phc = ph0 - floor(ph0 + 0.5);
+            slo[i] = phc - wk;
+            shi[i] = phc + wk;
+            bad |= !(wk > 0.0);
+            sacc[0][i] = 0ull;
+            sacc[1][i] = 0ull;
         }
-        const double fw = wdF * (1.0 - ewd / twd);
-        const double fd = dF * (1.0 - ed / td);
-        const double h = wk / S;
-        double sbs = 0.0, srs = 0.0;
-        for (int j = 0; j < S; ++j) {
-            double ph = ph0 - wk + (2 * j + 1) * h;
-            ph -= floor(ph + 0.5);
-            double sn, cs;
-            sincos(TWO_PI * ph, &sn, &cs);
-            const double e0 = s * cs, e1 = -s * sn, e2 = c;
-            double beam = 0.0;
-            if (bden > 0.0) beam = (fis + (1.0 - fis) * fmax(nb0 * e0 + nb1 * e1 + nb2 * e2, 0.0)) / bden;
-            double eb = 0.0;
-            const double l2 = ph - h, h2 = ph + h;
-            if (h2 >= amin && l2 <= bmax) {
-                if (h > 0.0) {
-                    for (int k = NWD + NDISC; k < NEL; ++k) eb = fma(sw[k], fmax(fmin(sb[k], h2) - fmax(sa[k], l2), 0.0), eb);
-                    eb /= 2.0 * h;
+        __syncthreads();
+        for (int i = tid + 1; i < m; i += nt) bad |= (slo[i] < slo[i - 1]) || (shi[i] < shi[i - 1]);
+        const bool sweep = !__syncthreads_or(bad);
+        if (sweep) {
+            const double tlo = slo[0], thi = shi[m - 1];
+            for (int k = tid; k < NWD + NDISC; k += nt) {
+                const double2 ab = sab[k];
+                if (!(ab.x < ab.y) || ab.y <= tlo || ab.x >= thi) continue;
+                int comp, ring;
+                if (k < NWD) {
+                    ring = int(sqrt(k * 0.25));
+                    if (4 * (ring + 1) * (ring + 1) <= k) ++ring;
+                    if (4 * ring * ring > k) --ring;
+                    comp = 0;
                 } else {
-                    for (int k = NWD + NDISC; k < NEL; ++k) eb += (ph > sa[k] && ph < sb[k]) ? sw[k] : 0.0;
+                    ring = NG_WD + (k - NWD) / NDISC_AZ;
+                    comp = 1;
+                }
+                const double wn = swr[ring] * (comp ? id : iwd);
+                int P1, P2, P3, P4;
+                count4(slo, shi, m, ab.x, ab.y, P1, P2, P3, P4);
+                unsigned long long* acc = sacc[comp];
+                int e0 = P4, s1 = P4;  // partial ranges [P1, e0) and [s1, P4)
+                if (P2 < P3) {
+                    const long long q = llrint(wn * FX_SCALE);
+                    fx_add(acc, P2, q);
+                    fx_add(acc, P3, -q);
+                    e0 = P2;
+                    s1 = P3;
+                }
+                for (int r = 0; r < 2; ++r) {
+                    const int pe = r ? P4 : e0;
+                    for (int p = r ? s1 : P1; p < pe; ++p) {
+                        const double lo = slo[p], hi = shi[p];
+                        const double ov = fmin(ab.y, hi) - fmax(ab.x, lo);
+                        if (ov > 0.0) {
+                            const long long q = llrint(wn * (ov / (hi - lo)) * FX_SCALE);
+                            fx_add(acc, p, q);
+                            fx_add(acc, p + 1, -q);
+                        }
+                    }
                 }
             }
-            sbs += beam * (1.0 - eb / tb);
-            double da = 0.0;
-            for (int k = 0; k < NDONOR; ++k)
-                da += fmax(sd[k] * e0 + sd[NDONOR + k] * e1 + sd[2 * NDONOR + k] * e2, 0.0);
-            srs += da / dn;
+            __syncthreads();
+            // inclusive scan of both difference arrays (2 entries per thread)
+            long long v0[2], v1[2];
+            for (int j = 0; j < 2; ++j) {
+                const int i = 2 * tid + j;
+                v0[j] = (i < m) ? static_cast<long long>(sacc[0][i]) : 0;
+                v1[j] = (i < m) ? static_cast<long long>(sacc[1][i]) : 0;
+            }
+            v0[1] += v0[0];
+            v1[1] += v1[0];
+            const long long w0 = wave_scan_incl(v0[1], lane), w1 = wave_scan_incl(v1[1], lane);
+            if (lane == 63) { sscan[0][wv] = w0; sscan[1][wv] = w1; }
+            __syncthreads();
+            long long b0 = w0 - v0[1], b1 = w1 - v1[1];
+            for (int i = 0; i < wv; ++i) { b0 += sscan[0][i]; b1 += sscan[1][i]; }
+            if (2 * tid < m) { sacc[0][2 * tid] = b0 + v0[0]; sacc[1][2 * tid] = b1 + v1[0]; }
+            if (2 * tid + 1 < m) { sacc[0][2 * tid + 1] = b0 + v0[1]; sacc[1][2 * tid + 1] = b1 + v1[1]; }
+            __syncthreads();
         }
-        const double fb = sF * sbs / S, fr = rsF * srs / S;
-        const double f = fw + fd + fb + fr;
-        if (L.flux) L.flux[size_t(pair) * n + p] = f;
-        if (L.comps) {
-            L.comps[(size_t(0) * L.npairs + pair) * n + p] = fw;
-            L.comps[(size_t(1) * L.npairs + pair) * n + p] = fd;
-            L.comps[(size_t(2) * L.npairs + pair) * n + p] = fb;
-            L.comps[(size_t(3) * L.npairs + pair) * n + p] = fr;
+        for (int i = tid; i < m; i += nt) {
+            const int p = o0 + t0 + i;
+            const double lo = slo[i], hi = shi[i];
+            const double wk = L.w ? L.w[p] : 0.0;
+            const double phc = 0.5 * (lo + hi);
+            double fwd, fdd;  // eclipsed fractions of WD and disc
+            if (sweep) {
+                fwd = double(static_cast<long long>(sacc[0][i])) * FX_INV;
+                fdd = double(static_cast<long long>(sacc[1][i])) * FX_INV;
+            } else {  // unsorted points or zero widths: scan the overlapping rings
+                double ewd = 0.0, ed = 0.0;
+                for (unsigned long long msk = group_mask(sgb, 0, NG_WD + NG_DISC, lo, hi); msk; msk &= msk - 1) {
+                    const int g = __builtin_ctzll(msk);
+                    const int k0 = group_start(g), k1 = group_start(g + 1);
+                    const double ov = (wk > 0.0) ? overlap_sum(sab, k0, k1, lo, hi)
+                                                 : inside_count(sab, nullptr, k0, k1, phc);
+                    if (g < NG_WD) ewd = fma(swr[g], ov, ewd); else ed = fma(swr[g], ov, ed);
+                }
+                if (wk > 0.0) {
+                    ewd /= 2.0 * wk;
+                    ed /= 2.0 * wk;
+                }
+                fwd = ewd * iwd;
+                fdd = ed * id;
+            }
+            const double fw = wdF * (1.0 - fwd);
+            const double fd = dF * (1.0 - fdd);
+            const double ph0 = L.x[p] - phi0;
+            const double h = wk / S;
+            double sbs = 0.0, srs = 0.0;
+#pragma unroll 1
+            for (int j = 0; j < S; ++j) {
+                double ph = ph0 - wk + (2 * j + 1) * h;
+                ph -= floor(ph + 0.5);
+                double sn, cs;
+                sincospi(2.0 * ph, &sn, &cs);  // |2 ph| <= 1: cheap exact reduction
+                const double e0 = s * cs, e1 = -s * sn;
+                double beam = 0.0;
+                if (bden > 0.0) beam = (fis + (1.0 - fis) * fmax(nb0 * e0 + nb1 * e1 + nb2 * c, 0.0)) / bden;
+                double eb = 0.0;
+                const double l2 = ph - h, h2 = ph + h;
+                for (unsigned long long msk = group_mask(sgb, NG_WD + NG_DISC, NGROUP, l2, h2); msk;
+                     msk &= msk - 1) {
+                    const int g = __builtin_ctzll(msk);
+                    const int k0 = group_start(g), k1 = group_start(g + 1);
+                    const double* wt = sbw + (k0 - NWD - NDISC);
+                    eb += (h > 0.0) ? overlap_wsum(sab, wt, k0, k1, l2, h2) : inside_count(sab, wt, k0, k1, ph);
+                }
+                if (h > 0.0) eb /= 2.0 * h;
+                sbs += beam * (1.0 - eb / tb);
+                // donor: 100 quads of mirror tiles (vx, +-vy, +-vz); for A = vx e0 +- vz c and
+                // Y = |vy e1|: max(A + Y, 0) + max(A - Y, 0) = max(A + max(Y, A), 0)
+                double d0 = 0.0, d1 = 0.0;
+#pragma unroll 4
+                for (int q = 0; q < U_DON; ++q) {
+                    const double2 v = sdxy[q];
+                    const double z = sdz[q];
+                    const double y = fabs(v.y * e1);
+                    const double A1 = fma(v.x, e0, z), A2 = fma(v.x, e0, -z);
+                    d0 += fmax(A1 + fmax(y, A1), 0.0);
+                    d1 += fmax(A2 + fmax(y, A2), 0.0);
+                }
+                srs += (d0 + d1) / dn;
+            }
+            const double fb = sF * sbs / S, fr = rsF * srs / S;
+            const double f = fw + fd + fb + fr;
+            if (L.flux) L.flux[size_t(pair) * n + t0 + i] = f;
+            if (L.comps) {
+                L.comps[(size_t(0) * L.npairs + pair) * n + t0 + i] = fw;
+                L.comps[(size_t(1) * L.npairs + pair) * n + t0 + i] = fd;
+                L.comps[(size_t(2) * L.npairs + pair) * n + t0 + i] = fb;
+                L.comps[(size_t(3) * L.npairs + pair) * n + t0 + i] = fr;
+            }
+            if (CHI) {
+                const double r = (L.y[p] - f) / L.ye[p];
+                chi += isnan(f) ? INFINITY : r * r;
+            }
         }
-        if (CHI) {
-            const double r = (L.y[o0 + p] - f) / L.ye[o0 + p];
-            chi += isnan(f) ? INFINITY : r * r;
-        }
+        __syncthreads();  // tile buffers are rewritten by the next tile
     }
     if (CHI) {
         chi = wave_sum(chi);
-        __syncthreads();
-        if (lane == 0) red[4][wv] = chi;
+        if (lane == 0) red[2][wv] = chi;
         __syncthreads();
         if (tid == 0) {
             double tot = 0.0;
-            for (int i = 0; i < LIKE_BLOCK / 64; ++i) tot += red[4][i];
+            for (int i = 0; i < nw; ++i) tot += red[2][i];
             L.lle[pair] = -0.5 * tot;
         }
     }
@@ -649,7 +921,7 @@ int run_front(const SetupArgs& S, const Ws& ws, hipStream_t st)
     if (launch_ok() != LFG_OK) return LFG_E_LAUNCH;
     const long nthreads = long(npairs) * NUNIQ;
     hipLaunchKernelGGL(k_elements, dim3(unsigned((nthreads + ELEM_BLOCK - 1) / ELEM_BLOCK)), dim3(ELEM_BLOCK), 0,
-                       st, ws.geo, ws.status, npairs, ws.a, ws.b, ws.wgt, ws.donor);
+                       st, ws.geo, ws.status, npairs, ws.ab, ws.donor);
     return launch_ok();
 }
 
@@ -675,9 +947,9 @@ int lfg_flux(const double* pars, int W, int P, const double* x, const double* w,
     int rc = run_front(S, ws, st);
     if (rc) return rc;
     if (N > 0) {
-        LikeArgs L{ws.geo, ws.status, ws.a, ws.b, ws.wgt, ws.donor, 1, nullptr, N, x, nullptr, nullptr, w,
+        LikeArgs L{ws.geo, ws.status, ws.ab, ws.donor, 1, nullptr, N, x, nullptr, nullptr, w,
                    nsub, flux, comps, nullptr, W};
-        hipLaunchKernelGGL(k_lnlike<false>, dim3(W), dim3(LIKE_BLOCK), 0, st, L);
+        hipLaunchKernelGGL(k_lnlike<false>, dim3(W), dim3(LIKE_THREADS), 0, st, L);
         if ((rc = launch_ok())) return rc;
     }
     if (status && hipMemcpyAsync(status, ws.status, sizeof(int) * W, hipMemcpyDeviceToDevice, st) != hipSuccess)
@@ -706,13 +978,13 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
     mark(1);
     const long nthreads = long(npairs) * NUNIQ;
     hipLaunchKernelGGL(k_elements, dim3(unsigned((nthreads + ELEM_BLOCK - 1) / ELEM_BLOCK)), dim3(ELEM_BLOCK), 0,
-                       st, ws.geo, ws.status, npairs, ws.a, ws.b, ws.wgt, ws.donor);
+                       st, ws.geo, ws.status, npairs, ws.ab, ws.donor);
     if ((rc = launch_ok())) return rc;
     mark(2);
     double* lle = lnlike_e ? lnlike_e : ws.lle;
-    LikeArgs L{ws.geo, ws.status, ws.a, ws.b, ws.wgt, ws.donor, T->E, T->off, T->max_n, T->x, T->y, T->ye,
+    LikeArgs L{ws.geo, ws.status, ws.ab, ws.donor, T->E, T->off, T->max_n, T->x, T->y, T->ye,
                T->w, T->nsub, nullptr, nullptr, lle, npairs};
-    hipLaunchKernelGGL(k_lnlike<true>, dim3(npairs), dim3(LIKE_BLOCK), 0, st, L);
+    hipLaunchKernelGGL(k_lnlike<true>, dim3(npairs), dim3(LIKE_THREADS), 0, st, L);
     if ((rc = launch_ok())) return rc;
     mark(3);
     hipLaunchKernelGGL(k_combine, dim3((W + 255) / 256), dim3(256), 0, st, W, T->E, ws.prior, ws.geo, lle, lnp);
@@ -789,14 +1061,13 @@ int lfg_elements(const double* pars, int W, int P, double* a, double* b, double*
                 ws.geo, ws.status, ws.prior};
     int rc = run_front(S, ws, st);
     if (rc) return rc;
-    const size_t ne = size_t(W) * NEL * sizeof(double);
+    if (a || b || wgt || donor) {
+        const long nt = long(W) * NEL;
+        hipLaunchKernelGGL(k_expand, dim3(unsigned((nt + 255) / 256)), dim3(256), 0, st, ws.geo, ws.status, W, ws.ab,
+                           ws.donor, a, b, wgt, donor);
+        if ((rc = launch_ok())) return rc;
+    }
     bool ok = true;
-    if (a) ok &= hipMemcpyAsync(a, ws.a, ne, hipMemcpyDeviceToDevice, st) == hipSuccess;
-    if (b) ok &= hipMemcpyAsync(b, ws.b, ne, hipMemcpyDeviceToDevice, st) == hipSuccess;
-    if (wgt) ok &= hipMemcpyAsync(wgt, ws.wgt, ne, hipMemcpyDeviceToDevice, st) == hipSuccess;
-    if (donor)
-        ok &= hipMemcpyAsync(donor, ws.donor, size_t(W) * NDONOR * 3 * sizeof(double), hipMemcpyDeviceToDevice,
-                             st) == hipSuccess;
     if (geo)
         ok &= hipMemcpyAsync(geo, ws.geo, size_t(W) * LFG_NGEO * sizeof(double), hipMemcpyDeviceToDevice, st) ==
               hipSuccess;

@@ -272,11 +272,10 @@ struct ConePt {
     double phi, gth, F2, eHe, etHe, ethHeth, gtt, dX2;
 };
 
+// direction given by (cos theta, sin theta): no trig inside the Newton loops
 __device__ __forceinline__ void cone_point(const Roche& R, double Px, double Py, double Pz, double s,
-                                           double c, double th, double t, ConePt& o)
+                                           double c, double cs, double sn, double t, ConePt& o)
 {
-    double sn, cs;
-    sincos(th, &sn, &cs);
     const double ex = s * cs, ey = -s * sn;
     const double x = fma(t, ex, Px), y = fma(t, ey, Py), z = fma(t, c, Pz);
     const double r1s = x * x + y * y + z * z;
@@ -303,14 +302,28 @@ __device__ __forceinline__ void cone_point(const Roche& R, double Px, double Py,
     o.dX2 = r2s;
 }
 
+// rotate (cs, sn) by d, |d| <= 0.05: Taylor series, error < 1e-20
+__device__ __forceinline__ void rotate(double& cs, double& sn, double d)
+{
+    const double d2 = d * d;
+    const double sd = d * (1.0 - d2 * (1.0 / 6.0) * (1.0 - d2 * (1.0 / 20.0) * (1.0 - d2 * (1.0 / 42.0) *
+                                                                              (1.0 - d2 * (1.0 / 72.0)))));
+    const double cd = 1.0 - d2 * 0.5 * (1.0 - d2 * (1.0 / 12.0) * (1.0 - d2 * (1.0 / 30.0) *
+                                                                    (1.0 - d2 * (1.0 / 56.0) * (1.0 - d2 * (1.0 / 90.0)))));
+    const double c2 = cs * cd - sn * sd;
+    sn = fma(sn, cd, cs * sd);
+    cs = c2;
+}
+
 // 2-D Newton for one contact phase; returns false unless cleanly converged
-// to a tangency of the right kind (ingress: g falling with theta).
+// to a tangency of the right kind (ingress: g falling with theta).  th is the
+// running angle; (cs, sn) its cosine and sine, advanced by rotation.
 __device__ inline bool tangency(const Roche& R, double Px, double Py, double Pz, double s, double c,
-                                bool ingress, double& th, double& t)
+                                bool ingress, double& th, double cs, double sn, double& t)
 {
     for (int it = 0; it < 16; ++it) {
         ConePt o;
-        cone_point(R, Px, Py, Pz, s, c, th, t, o);
+        cone_point(R, Px, Py, Pz, s, c, cs, sn, t, o);
         const double F1 = o.phi - R.pl1;
         const double J11 = t * o.gth, J12 = o.F2;
         const double J21 = t * o.etHe + o.gth, J22 = o.eHe;
@@ -325,17 +338,18 @@ __device__ inline bool tangency(const Roche& R, double Px, double Py, double Pz,
         if (fabs(dth) <= TH_TOL) {
             return J22 > 0.0 && ((J11 < 0.0) == ingress) && t > 0.0 && o.dX2 < R.Rs2;
         }
+        rotate(cs, sn, dth);
     }
     return false;
 }
 
 // 0: not eclipsed, 1: eclipsed, -1: undecided (use the nested solver)
 __device__ inline int cone_exists(const Roche& R, double Px, double Py, double Pz, double s, double c,
-                                  double th, double t)
+                                  double cs, double sn, double t)
 {
     for (int it = 0; it < 16; ++it) {
         ConePt o;
-        cone_point(R, Px, Py, Pz, s, c, th, t, o);
+        cone_point(R, Px, Py, Pz, s, c, cs, sn, t, o);
         if (o.phi < R.pl1) return (o.dX2 < R.Rs2) ? 1 : -1;
         const double Gth = t * o.gth, Gt = o.F2;
         const double Htt = o.eHe, Hht = o.gth + t * o.etHe, Hhh = t * t * o.ethHeth + t * o.gtt;
@@ -349,51 +363,79 @@ __device__ inline int cone_exists(const Roche& R, double Px, double Py, double P
             dth *= 0.05 / big;
             dt *= 0.05 / big;
         }
-        th += dth;
         t += dt;
         if (fabs(dth) <= 1e-12 && fabs(dt) <= 1e-12) return 0;
+        rotate(cs, sn, dth);
     }
     return -1;
 }
 
 // element_interval with the fast path; Rcal = sphere radius reproducing the
-// WD-centre contact (initial guesses only)
+// WD-centre contact (initial guesses only).  Trig: one atan2 and one acos.
 __device__ inline bool element_interval_fast(const Roche& R, double Px, double Py, double Pz, double s,
-                                             double c, double Rcal, double Reff, double& a, double& b)
+                                             double c, double Rcal, double Reff, double& a, double& b,
+                                             bool* fallback = nullptr)
 {
     const double ux = 1.0 - Px, uy = -Py, uz = -Pz;
     const double uxy2 = ux * ux + uy * uy;
     const double uu = uxy2 + uz * uz;
     if (uu > R.Rs2 && uxy2 > 0.0 && s > 0.0) {
-        const double uxy = sqrt(uxy2);
-        const double thc = atan2(-uy, ux);
-        const double cosD = (sqrt(uu - R.Rs2) - c * uz) / (s * uxy);
+        const double iuxy = rsqrt(uxy2), uxy = uxy2 * iuxy;
+        const double cosD = (sqrt(uu - R.Rs2) - c * uz) * iuxy / s;
         if (cosD >= 1.0) { a = 1.0; b = -1.0; return false; }
-        double sc, cc;
-        sincos(thc, &sc, &cc);
-        const double tc = ux * s * cc - uy * s * sc + uz * c;
-        const int ex = cone_exists(R, Px, Py, Pz, s, c, thc, tc);
+        // theta_c = atan2(-uy, ux): closest approach of the line of sight to D
+        const double cc = ux * iuxy, sc = -uy * iuxy;
+        const double tc = s * uxy + uz * c;
+        const int ex = cone_exists(R, Px, Py, Pz, s, c, cc, sc, tc);
         if (ex == 0) { a = 1.0; b = -1.0; return false; }
         if (ex == 1) {
-            const double Dm = (cosD <= -1.0) ? PI : acos(cosD);
-            const double ce = (sqrt(fmax(uu - Rcal * Rcal, 0.0)) - c * uz) / (s * uxy);
-            const double de = (ce > -1.0 && ce < 1.0) ? acos(ce) : 0.5 * Dm;
-            double thi = thc - de, tti, tho = thc + de, tto;
-            double si, ci, so, co;
-            sincos(thi, &si, &ci);
-            sincos(tho, &so, &co);
-            tti = ux * s * ci - uy * s * si + uz * c;
-            tto = ux * s * co - uy * s * so + uz * c;
-            const bool oki = tangency(R, Px, Py, Pz, s, c, true, thi, tti);
-            const bool oko = tangency(R, Px, Py, Pz, s, c, false, tho, tto);
-            if (oki && oko && thi < tho && thi > thc - Dm && tho < thc + Dm) {
-                a = thi * (1.0 / TWO_PI);
-                b = tho * (1.0 / TWO_PI);
-                return true;
+            const double ce = (sqrt(fmax(uu - Rcal * Rcal, 0.0)) - c * uz) * iuxy / s;
+            if (ce > -1.0 && ce < 1.0) {
+                const double se = sqrt(1.0 - ce * ce);
+                const double thc = atan2(-uy, ux), de = acos(ce);
+                // cos/sin of thc -+ de; t at closest approach to D along each ray
+                double ci = cc * ce + sc * se, si = sc * ce - cc * se;
+                double co = cc * ce - sc * se, so = sc * ce + cc * se;
+                double thi = thc - de, tho = thc + de;
+                double tti = s * (ux * ci - uy * si) + uz * c;
+                double tto = s * (ux * co - uy * so) + uz * c;
+                const bool oki = tangency(R, Px, Py, Pz, s, c, true, thi, ci, si, tti);
+                const bool oko = tangency(R, Px, Py, Pz, s, c, false, tho, co, so, tto);
+                const double Dm = (cosD <= -1.0) ? PI : acos(cosD);
+                if (oki && oko && thi < tho && thi > thc - Dm && tho < thc + Dm) {
+                    a = thi * (1.0 / TWO_PI);
+                    b = tho * (1.0 / TWO_PI);
+                    return true;
+                }
             }
         }
     }
+    if (fallback) *fallback = true;
     return element_interval(R, Px, Py, Pz, s, c, Reff, a, b);
+}
+
+// findphi / findi with the same 2-D tangency Newton, nested solver fallback
+__device__ inline int findphi(const Roche& R, double inc_deg, double& dphi);
+
+__device__ inline int findphi_fast(const Roche& R, double inc_deg, double& dphi)
+{
+    double s, c;
+    sincos(inc_deg * DEG, &s, &c);
+    const double cosD = sqrt(1.0 - R.Rs2) / s;
+    if (s > 0.0 && cosD < 1.0) {
+        const double Dm = acos(cosD);
+        const double R0 = eggleton(R.q);
+        const double c0 = sqrt(1.0 - R0 * R0) / s;
+        double th = (c0 < 1.0) ? acos(c0) : 0.5 * Dm;
+        double sn, cs;
+        sincos(th, &sn, &cs);
+        double t = s * cs;
+        if (tangency(R, 0.0, 0.0, 0.0, s, c, false, th, cs, sn, t) && th > 0.0 && th < Dm) {
+            dphi = th / PI;
+            return ST_OK;
+        }
+    }
+    return findphi(R, inc_deg, dphi);
 }
 
 // MODEL_SPEC 4.4: full phase width of the WD-centre eclipse
@@ -455,26 +497,6 @@ __device__ inline int findi(const Roche& R, double dphi, double& inc_deg)
     }
     inc_deg = acos(c) / DEG;
     return ST_OK;
-}
-
-// findphi / findi with the same 2-D tangency Newton, nested solver fallback
-__device__ inline int findphi_fast(const Roche& R, double inc_deg, double& dphi)
-{
-    double s, c;
-    sincos(inc_deg * DEG, &s, &c);
-    const double cosD = sqrt(1.0 - R.Rs2) / s;
-    if (s > 0.0 && cosD < 1.0) {
-        const double Dm = acos(cosD);
-        const double R0 = eggleton(R.q);
-        const double c0 = sqrt(1.0 - R0 * R0) / s;
-        double th = (c0 < 1.0) ? acos(c0) : 0.5 * Dm;
-        double t = s * cos(th);
-        if (tangency(R, 0.0, 0.0, 0.0, s, c, false, th, t) && th > 0.0 && th < Dm) {
-            dphi = th / PI;
-            return ST_OK;
-        }
-    }
-    return findphi(R, inc_deg, dphi);
 }
 
 __device__ inline int findi_fast(const Roche& R, double dphi, double& inc_deg)

@@ -137,3 +137,40 @@ def test_point_evaluation_and_edges(oracle):
     # empty phase array
     f, st = flux_batch(np.array([TRUTH18]), np.zeros(0), np.zeros(0))
     assert f.shape == (1, 0)
+
+
+def _grid_case(kind):
+    rng = np.random.default_rng(5)
+    if kind == "multi_tile":       # 3 sweep tiles, the last one ragged
+        x, w = phase_grid(1300, -0.25, 0.25)
+    elif kind == "shuffled":       # unsorted phases: the ring-scan path
+        x, w = phase_grid(300)
+        perm = rng.permutation(len(x))
+        x, w = x[perm], w[perm]
+    elif kind == "wide_exposures":  # exposures overlap many neighbours
+        x, w = phase_grid(200, -0.15, 0.15)
+        w = w * 9.0
+    elif kind == "ragged_widths":  # sorted lo/hi with varying widths
+        x = np.sort(rng.uniform(-0.2, 0.2, 400))
+        w = np.full_like(x, 4e-4)
+    else:                          # phases wrap through +-0.5 inside the data
+        x, w = phase_grid(300, 0.2, 0.8)
+    return x, w
+
+
+@pytest.mark.parametrize("kind", ["multi_tile", "shuffled", "wide_exposures", "ragged_widths", "wrap"])
+def test_flux_phase_layouts(oracle, kind):
+    """Sweep (sorted tiles) and ring-scan (unsorted) paths both match the oracle."""
+    from lfit_python_amd.lfit import flux_batch
+    x, w = _grid_case(kind)
+    pars = random_pars(6, complex_bs=True, seed=3)
+    flux, status = flux_batch(pars, x, w, nsub=3)
+    flux, status = flux.cpu().numpy(), status.cpu().numpy()
+    n_ok = 0
+    for i, p in enumerate(pars):
+        st, f = oracle.flux(p, x, w, nsub=3)
+        assert status[i] == st
+        if st == 0:
+            n_ok += 1
+            assert _rel(flux[i], f, np.max(np.abs(f))) < FLUX_RTOL
+    assert n_ok >= 4
