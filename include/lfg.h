@@ -156,6 +156,21 @@ int lfg_stretch_accept(double* pos, double* lnp, int W, int ndim, int half,
                        const double* lnp_new, unsigned long long seed,
                        unsigned long long step, int* naccept, void* stream);
 
+/*
+ * The same two moves with the step counter read from device memory
+ * (step_dev [dev] 1 x uint64), so that one emcee iteration can be captured
+ * in a HIP graph and replayed; the caller advances *step_dev after half 1.
+ */
+int lfg_stretch_propose_dev(const double* pos, int W, int ndim, int half,
+                            double a, unsigned long long seed,
+                            const unsigned long long* step_dev, double* q,
+                            double* zfac, void* stream);
+int lfg_stretch_accept_dev(double* pos, double* lnp, int W, int ndim, int half,
+                           const double* q, const double* zfac,
+                           const double* lnp_new, unsigned long long seed,
+                           const unsigned long long* step_dev, int* naccept,
+                           void* stream);
+
 /* hipEvent helpers for hosts without a HIP binding (ctypes) */
 int lfg_event_create(void** ev);
 int lfg_event_destroy(void* ev);

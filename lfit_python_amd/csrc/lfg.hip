@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
+
 #include "lfg.h"
 #include "lfg_device.hpp"
 #include "lfg_tables.hpp"
@@ -24,7 +26,14 @@ using namespace lfg;
 namespace {
 
 constexpr int SETUP_BLOCK = 64;
+constexpr int LFG_MAX_DEVICES = 64;
 constexpr int ELEM_BLOCK = 256;
+// per-pair weight block written by k_elements: disc ring weights, the disc
+// total 2 pi [P(rdisc) - P(rin)], spot element weights
+constexpr int WT_DISC = 0, WT_TD = NDISC_R, WT_BS = 24, WT_N = WT_BS + NBS;
+// per unique donor tile: vx, vy, vz, arc centre, arc half-width (phase units)
+constexpr int DON_STRIDE = 5;
+
 
 __device__ const int kIdentityGather[18] = {0, 1, 2, 3, 4, 5, 6, 7, 8,
                                             9, 10, 11, 12, 13, 14, 15, 16, 17};
@@ -32,8 +41,10 @@ __device__ const int kIdentityGather[18] = {0, 1, 2, 3, 4, 5, 6, 7, 8,
 struct Ws {
     double* geo;
     int* status;
+    int* bstatus;   // [pairs] stream status (k_bspot), folded into status by the spot elements
     double2* ab;    // [pairs][NEL] eclipse intervals (a, b)
-    double* donor;  // [pairs][NDONOR/4][3] symmetry-unique donor tiles
+    double* donor;  // [pairs][NDONOR/4][DON_STRIDE] symmetry-unique donor tiles
+    double* wts;    // [pairs][WT_N] ring / spot weights
     double* prior;
     double* lle;
     size_t total;
@@ -50,8 +61,10 @@ Ws carve(void* base, int W, int E)
     auto take = [&](size_t bytes) { char* r = p ? p + off : nullptr; off += align256(bytes); return r; };
     ws.geo = reinterpret_cast<double*>(take(pairs * LFG_NGEO * sizeof(double)));
     ws.status = reinterpret_cast<int*>(take(pairs * sizeof(int)));
+    ws.bstatus = reinterpret_cast<int*>(take(pairs * sizeof(int)));
     ws.ab = reinterpret_cast<double2*>(take(pairs * NEL * sizeof(double2)));
-    ws.donor = reinterpret_cast<double*>(take(pairs * (NDONOR / 4) * 3 * sizeof(double)));
+    ws.donor = reinterpret_cast<double*>(take(pairs * (NDONOR / 4) * DON_STRIDE * sizeof(double)));
+    ws.wts = reinterpret_cast<double*>(take(pairs * WT_N * sizeof(double)));
     ws.prior = reinterpret_cast<double*>(take(size_t(W) * sizeof(double)));
     ws.lle = reinterpret_cast<double*>(take(pairs * sizeof(double)));
     ws.total = off;
@@ -132,29 +145,16 @@ __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
 #else
 #define LFG_STAMP(v)
 #endif
-    double bs[4] = {0.0, 0.0, 0.0, 0.0};
-    int bst = ST_BAD_STREAM;
     LFG_STAMP(tp1);
     if (st == ST_OK) {
-        const double rdisc_a = p[6] * R.xl1;
-        bst = bspot(R, rdisc_a, bs);
-        LFG_STAMP(tp2);
-        // SimpleEclipse.ln_prior Roche checks (CVModel.py:215-316)
-        if (rdisc_a > DISC_MAX_A) rprior = -INFINITY;
+        // SimpleEclipse.ln_prior Roche checks not involving the stream (CVModel.py:215-316)
+        if (p[6] * R.xl1 > DISC_MAX_A) rprior = -INFINITY;
         const double rwd = p[8], scale = p[9];
         if (scale > rwd * 3.0 || scale < rwd / 3.0) rprior = -INFINITY;
-        if (bst != ST_OK) rprior = -INFINITY;
-        else {
-            double alpha = atan2(bs[1], bs[0]) / DEG;
-            if (alpha < 0.0) alpha = 90.0 - alpha;
-            const double tangent = alpha + 90.0;
-            const double minaz = fmax(0.0, tangent - AZ_SLOPE), maxaz = fmin(178.0, tangent + AZ_SLOPE);
-            if (p[10] < minaz || p[10] > maxaz) rprior = -INFINITY;
-        }
     } else {
         rprior = -INFINITY;
     }
-
+    LFG_STAMP(tp2);
     double inc = 0.0;
     if (st == ST_OK) st = findi_fast(R, p[5], inc);
     LFG_STAMP(tp3);
@@ -167,7 +167,6 @@ __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
         const double um = bs_umax(p[14], p[15], p[14] * log(pow(p[14] / p[15], 1.0 / p[15])) - p[14] / p[15]);
         const unsigned long long tc2 = __builtin_amdgcn_s_memtime();
         G[42] = double(tp1 - tp0);
-        G[43] = double(tp2 - tp1);
         G[44] = double(tp3 - tp2);
         G[45] = double(tb - ta);
         G[46] = double(tc2 - tb) + 0.0 * um;
@@ -176,7 +175,6 @@ __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
     const double rwd_a = p[8] * R.xl1, rdisc_a = p[6] * R.xl1;
     if (st == ST_OK && (!(rwd_a > 0.0) || !(rdisc_a > rwd_a) || !(rdisc_a < R.xl1))) st = ST_BAD_GEOMETRY;
     if (st == ST_OK && (!(p[9] > 0.0) || !(p[14] > 0.0) || !(p[15] > 0.0))) st = ST_BAD_GEOMETRY;
-    if (st == ST_OK && bst != ST_OK) st = bst;
 
     A.status[t] = st;
     G[G_RPRIOR] = A.roche_priors ? rprior : 0.0;
@@ -200,7 +198,6 @@ __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
     G[G_S] = s; G[G_C] = c; G[G_INC] = inc;
     G[G_RWD] = rwd_a; G[G_RDISC] = rdisc_a; G[G_REFF] = eggleton(R.q);
     G[G_ULIMB] = p[7]; G[G_DEXP] = p[12];
-    G[G_BSX] = bs[0]; G[G_BSY] = bs[1]; G[G_BSVX] = bs[2]; G[G_BSVY] = bs[3];
     G[G_L] = p[9] * R.xl1; G[G_UPK] = upk; G[G_UMAX] = bs_umax(a1, a2, lnpk); G[G_LNPK] = lnpk;
     G[G_EXP1] = a1; G[G_EXP2] = a2; G[G_CAZ] = caz; G[G_SAZ] = saz;
     G[G_NB0] = st_ * cp_; G[G_NB1] = st_ * sp_; G[G_NB2] = ct_;
@@ -209,6 +206,46 @@ __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
     G[G_WDF] = p[0]; G[G_DF] = p[1]; G[G_SF] = p[2]; G[G_RSF] = p[3];
     const double sce = s * cos(PI * p[5]);
     G[G_RCAL] = sqrt(1.0 - sce * sce);
+}
+
+// ---------------------------------------------------------------- k_bspot
+// One lane per (walker, eclipse): the ballistic stream to the disc edge and
+// the spot-dependent Roche prior (CVModel.py:215-316).  Needs only q and
+// rdisc, so it runs on a side stream concurrently with k_setup and the WD,
+// disc and donor elements; only the spot elements wait for it.
+__global__ __launch_bounds__(SETUP_BLOCK) void k_bspot(SetupArgs A, int* __restrict__ bstatus)
+{
+    const int t = blockIdx.x * SETUP_BLOCK + threadIdx.x;
+    if (t >= A.W * A.E) return;
+    const int* gat = A.gather ? A.gather : kIdentityGather;
+    const int w = t / A.E, e = t - w * A.E;
+    const double q = gather_par(A, w, gat[e * 18 + 4]);
+    const double rdisc = gather_par(A, w, gat[e * 18 + 6]);
+    const double az = gather_par(A, w, gat[e * 18 + 10]);
+    double* G = A.geo + size_t(t) * LFG_NGEO;
+#ifdef LFG_PROFILE_SETUP
+    const unsigned long long tp0 = __builtin_amdgcn_s_memtime();
+#endif
+    Roche R;
+    int st = (isfinite(q) && isfinite(rdisc) && isfinite(az)) ? roche_init(R, q) : ST_BAD_ARGS;
+    double bs[4] = {0.0, 0.0, 0.0, 0.0};
+    if (st == ST_OK) st = bspot(R, rdisc * R.xl1, bs);
+    double rprior = 0.0;
+    if (st != ST_OK) {
+        rprior = -INFINITY;
+    } else {
+        double alpha = atan2(bs[1], bs[0]) / DEG;
+        if (alpha < 0.0) alpha = 90.0 - alpha;
+        const double tangent = alpha + 90.0;
+        const double minaz = fmax(0.0, tangent - AZ_SLOPE), maxaz = fmin(178.0, tangent + AZ_SLOPE);
+        if (az < minaz || az > maxaz) rprior = -INFINITY;
+    }
+    G[G_BSX] = bs[0]; G[G_BSY] = bs[1]; G[G_BSVX] = bs[2]; G[G_BSVY] = bs[3];
+    G[G_RPRIOR_BS] = A.roche_priors ? rprior : 0.0;
+    bstatus[t] = st;
+#ifdef LFG_PROFILE_SETUP
+    G[43] = double(__builtin_amdgcn_s_memtime() - tp0);
+#endif
 }
 
 // ------------------------------------------------------------- k_elements
@@ -221,6 +258,8 @@ __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
 // vectors; weights depend on ring only and are formed in k_lnlike.
 constexpr int U_WD = NWD / 2, U_DISC = NDISC / 2, U_BS = NBS, U_DON = NDONOR / 4;
 constexpr int NUNIQ = U_WD + U_DISC + U_BS + U_DON;
+// unique-item order: WD, disc, donor (need k_setup only), then the spot (needs k_bspot)
+constexpr int U_MAIN = U_WD + U_DISC + U_DON;
 
 __device__ __forceinline__ int wd_ring_of(int u)  // ring of unique WD tile u (ring ir starts at 2 ir^2)
 {
@@ -230,21 +269,56 @@ __device__ __forceinline__ int wd_ring_of(int u)  // ring of unique WD tile u (r
     return ir;
 }
 
-__global__ __launch_bounds__(ELEM_BLOCK) void k_elements(const double* __restrict__ geo,
-                                                         const int* __restrict__ status, int npairs,
-                                                         double2* __restrict__ AB, double* __restrict__ DON)
+// element weights (MODEL_SPEC 5.1-5.3): per WD ring, per disc ring, per spot element
+__device__ inline double wd_ring_weight(int ir, double ul) { return fma(kWdA[ir], 1.0 - ul, kWdB[ir] * ul); }
+
+// radial integral of r^(1 - dexp) dr over the disc annuli (MODEL_SPEC 5.2):
+// the boundary term P(r) = r^ex / ex, or ln r when ex = 2 - dexp vanishes
+__device__ inline double disc_boundary(int i, const double* G)
 {
+    const double rin = G[G_RWD];
+    const double r = rin + i * ((G[G_RDISC] - rin) / NDISC_R);
+    const double ex = 2.0 - G[G_DEXP];
+    return (fabs(ex) < 1e-10) ? log(r) : pow(r, ex) / ex;
+}
+
+__device__ inline double disc_ring_weight(int ir, const double* G)
+{
+    return (TWO_PI / NDISC_AZ) * (disc_boundary(ir + 1, G) - disc_boundary(ir, G));
+}
+
+__device__ inline double bs_weight(int j, const double* G)
+{
+    const double uk = (j + 0.5) * (G[G_UMAX] / NBS);
+    return exp(G[G_EXP1] * log(uk) - pow(uk, G[G_EXP2]) - G[G_LNPK]);
+}
+
+__global__ __launch_bounds__(ELEM_BLOCK) void k_elements(const double* __restrict__ geo,
+                                                         const int* status, int npairs,
+                                                         double2* __restrict__ AB, double* __restrict__ DON,
+                                                         double* __restrict__ WT, int u0, int nu,
+                                                         const int* __restrict__ bstatus, int* mstatus)
+{
+    // lanes cover unique items [u0, u0 + nu) of every pair; the spot launch
+    // (u0 = U_MAIN) also folds the stream status into the pair status
     const long t = long(blockIdx.x) * ELEM_BLOCK + threadIdx.x;
-    const int pair = int(t / NUNIQ);
-    const int u = int(t - long(pair) * NUNIQ);
+    const int pair = int(t / nu);
+    const int u = u0 + int(t - long(pair) * nu);
     if (pair >= npairs) return;
     if (status[pair] != ST_OK) return;
+    if (bstatus) {
+        const int bst = bstatus[pair];
+        if (bst != ST_OK) {
+            if (u == u0) mstatus[pair] = bst;
+            return;
+        }
+    }
     const double* G = geo + size_t(pair) * LFG_NGEO;
     const Roche R{G[G_Q], G[G_CA], G[G_CB], G[G_MU], G[G_XL1], G[G_PL1], G[G_RS], G[G_RS2]};
     const double s = G[G_S], c = G[G_C];
 
-    if (u >= U_WD + U_DISC + U_BS) {  // donor tile (MODEL_SPEC 5.4), phi' in (0, pi/2)
-        const int uu = u - (U_WD + U_DISC + U_BS);
+    if (u >= U_WD + U_DISC && u < U_MAIN) {  // donor tile (MODEL_SPEC 5.4), phi' in (0, pi/2)
+        const int uu = u - (U_WD + U_DISC);
         const int it = uu / (NDONOR_P / 4), ip = uu - it * (NDONOR_P / 4);
         const double stc = kDonSt[it], ctc = kDonCt[it];
         const double dx = -ctc, dy = stc * kDonCp[ip], dz = stc * kDonSp[ip];
@@ -267,10 +341,17 @@ __global__ __launch_bounds__(ELEM_BLOCK) void k_elements(const double* __restric
         const double ig = rsqrt(gx * gx + gy * gy + gz * gz);
         const double nx = gx * ig, ny = gy * ig, nz = gz * ig;
         const double dA = r * r * kDonOmega[it] / (nx * dx + ny * dy + nz * dz);
-        double* D = DON + (size_t(pair) * U_DON + uu) * 3;
-        D[0] = dA * nx;
-        D[1] = dA * ny;
-        D[2] = dA * nz;
+        const double vx = dA * nx, vy = dA * ny, vz = dA * nz;
+        // visibility arc: v.e = s rho cos(theta + alpha) + c vz > 0 with
+        // rho cos(alpha) = vx, rho sin(alpha) = vy  ->  |theta + alpha| < acos(kappa)
+        const double srho = s * sqrt(vx * vx + vy * vy);
+        const double kap = (srho > 0.0) ? -c * vz / srho : (c * vz > 0.0 ? -2.0 : 2.0);
+        double* D = DON + (size_t(pair) * U_DON + uu) * DON_STRIDE;
+        D[0] = vx;
+        D[1] = vy;
+        D[2] = vz;
+        D[3] = -atan2(vy, vx) * (1.0 / TWO_PI);
+        D[4] = acos(fmin(fmax(kap, -1.0), 1.0)) * (1.0 / TWO_PI);
         return;
     }
 
@@ -296,13 +377,19 @@ __global__ __launch_bounds__(ELEM_BLOCK) void k_elements(const double* __restric
         km = NWD + ir * NDISC_AZ + NDISC_AZ - 1 - j;
         const double rin = G[G_RWD];
         const double rc = rin + (ir + 0.5) * ((G[G_RDISC] - rin) / NDISC_R);
+        if (j == 0) {
+            double* Wp = WT + size_t(pair) * WT_N;
+            Wp[WT_DISC + ir] = disc_ring_weight(ir, G);
+            if (ir == 0) Wp[WT_TD] = TWO_PI * (disc_boundary(NDISC_R, G) - disc_boundary(0, G));
+        }
         Px = rc * kDiscCos[j];
         Py = rc * kDiscSin[j];
         Pz = 0.0;
     } else {  // bright-spot strip (MODEL_SPEC 5.3): no mirror partner
-        const int j = u - U_WD - U_DISC;
+        const int j = u - U_MAIN;
         k = km = NWD + NDISC + j;
         const double uk = (j + 0.5) * (G[G_UMAX] / NBS);
+        WT[size_t(pair) * WT_N + WT_BS + j] = bs_weight(j, G);
         const double off = G[G_L] * (uk - G[G_UPK]);
         Px = fma(off, G[G_CAZ], G[G_BSX]);
         Py = fma(off, G[G_SAZ], G[G_BSY]);
@@ -322,30 +409,6 @@ __global__ __launch_bounds__(ELEM_BLOCK) void k_elements(const double* __restric
         const bool ecl = a < b;
         AB[o + km] = ecl ? make_double2(-b, -a) : make_double2(1.0, -1.0);
     }
-}
-
-// element weights (MODEL_SPEC 5.1-5.3): per WD ring, per disc ring, per spot element
-__device__ inline double wd_ring_weight(int ir, double ul) { return fma(kWdA[ir], 1.0 - ul, kWdB[ir] * ul); }
-
-// radial integral of r^(1 - dexp) dr over the disc annuli (MODEL_SPEC 5.2):
-// the boundary term P(r) = r^ex / ex, or ln r when ex = 2 - dexp vanishes
-__device__ inline double disc_boundary(int i, const double* G)
-{
-    const double rin = G[G_RWD];
-    const double r = rin + i * ((G[G_RDISC] - rin) / NDISC_R);
-    const double ex = 2.0 - G[G_DEXP];
-    return (fabs(ex) < 1e-10) ? log(r) : pow(r, ex) / ex;
-}
-
-__device__ inline double disc_ring_weight(int ir, const double* G)
-{
-    return (TWO_PI / NDISC_AZ) * (disc_boundary(ir + 1, G) - disc_boundary(ir, G));
-}
-
-__device__ inline double bs_weight(int j, const double* G)
-{
-    const double uk = (j + 0.5) * (G[G_UMAX] / NBS);
-    return exp(G[G_EXP1] * log(uk) - pow(uk, G[G_EXP2]) - G[G_LNPK]);
 }
 
 // test/inspection only: per-element weights and the full 400-tile donor
@@ -374,7 +437,7 @@ __global__ void k_expand(const double* __restrict__ geo, const int* __restrict__
     if (WG) WG[size_t(pair) * NEL + k] = w;
     if (DFULL && k < U_DON) {
         const int it = k / (NDONOR_P / 4), ip = k - it * (NDONOR_P / 4);
-        const double* v = DON + (size_t(pair) * U_DON + k) * 3;
+        const double* v = DON + (size_t(pair) * U_DON + k) * DON_STRIDE;
         const int base = it * NDONOR_P;
         const int ks[4] = {base + ip, base + NDONOR_P - 1 - ip, base + NDONOR_P / 2 - 1 - ip,
                            base + NDONOR_P / 2 + ip};
@@ -400,6 +463,7 @@ struct LikeArgs {
     const int* status;
     const double2* AB;
     const double* DON;
+    const double* WT;
     int E;
     const int* off;  // nullptr: every pair uses x[0..N)
     int N;
@@ -414,118 +478,139 @@ struct LikeArgs {
     int npairs;
 };
 
-// element groups with their own [min a, max b] window: 10 WD rings, 20 disc
-// rings, 5 spot blocks of 20 -- a point only scans the groups it overlaps
-constexpr int NG_WD = NWD_RINGS, NG_DISC = NDISC_R, NG_BS = 5, NGROUP = NG_WD + NG_DISC + NG_BS;
-
-__device__ __forceinline__ int group_start(int g)
-{
-    return g < NG_WD ? 4 * g * g : (g < NG_WD + NG_DISC ? NWD + (g - NG_WD) * NDISC_AZ
-                                                       : NWD + NDISC + (g - NG_WD - NG_DISC) * (NBS / NG_BS));
-}
-
-__device__ __forceinline__ double ov1(double2 e, double lo, double hi)
-{
-    return fmax(fmin(e.y, hi) - fmax(e.x, lo), 0.0);
-}
-
-// sum over k in [k0, k1) of |[a_k, b_k] n [lo, hi]|; four independent chains
-// keep four 128-bit LDS reads in flight
-__device__ __forceinline__ double overlap_sum(const double2* __restrict__ ab, int k0, int k1, double lo,
-                                              double hi)
-{
-    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-    int k = k0;
-#pragma unroll 1
-    for (; k + 3 < k1; k += 4) {
-        const double2 e0 = ab[k], e1 = ab[k + 1], e2 = ab[k + 2], e3 = ab[k + 3];
-        s0 += ov1(e0, lo, hi);
-        s1 += ov1(e1, lo, hi);
-        s2 += ov1(e2, lo, hi);
-        s3 += ov1(e3, lo, hi);
-    }
-#pragma unroll 1
-    for (; k < k1; ++k) s0 += ov1(ab[k], lo, hi);
-    return (s0 + s1) + (s2 + s3);
-}
-
-// weighted variant for the spot strip (per-element weights wt[k - k0])
-__device__ __forceinline__ double overlap_wsum(const double2* __restrict__ ab, const double* __restrict__ wt,
-                                               int k0, int k1, double lo, double hi)
-{
-    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-    int k = k0;
-#pragma unroll 1
-    for (; k + 3 < k1; k += 4) {
-        const double2 e0 = ab[k], e1 = ab[k + 1], e2 = ab[k + 2], e3 = ab[k + 3];
-        const int i = k - k0;
-        s0 = fma(wt[i], ov1(e0, lo, hi), s0);
-        s1 = fma(wt[i + 1], ov1(e1, lo, hi), s1);
-        s2 = fma(wt[i + 2], ov1(e2, lo, hi), s2);
-        s3 = fma(wt[i + 3], ov1(e3, lo, hi), s3);
-    }
-#pragma unroll 1
-    for (; k < k1; ++k) s0 = fma(wt[k - k0], ov1(ab[k], lo, hi), s0);
-    return (s0 + s1) + (s2 + s3);
-}
-
-// bit g set when group g's eclipse window meets [lo, hi]
-__device__ __forceinline__ unsigned long long group_mask(const double2* __restrict__ gb, int g0, int g1, double lo,
-                                                         double hi)
-{
-    unsigned long long m = 0;
-#pragma unroll 5
-    for (int g = g0; g < g1; ++g) {
-        const double2 b = gb[g];
-        m |= (hi >= b.x && lo <= b.y) ? (1ull << g) : 0ull;
-    }
-    return m;
-}
-
-__device__ __forceinline__ double inside_count(const double2* __restrict__ ab, const double* wt, int k0, int k1,
-                                               double ph)
-{
-    double s = 0.0;
-    for (int k = k0; k < k1; ++k) s += (ph > ab[k].x && ph < ab[k].y) ? (wt ? wt[k - k0] : 1.0) : 0.0;
-    return s;
-}
-
-// ---- sweep over a phase-sorted tile of points (MODEL_SPEC 6.1 restated) ----
-// With lo_p = phase_p - w_p and hi_p = phase_p + w_p both non-decreasing in p,
-// the points an element [a, b] overlaps form the contiguous range [P1, P4),
-// and those it covers whole form [P2, P3):
-//   P1 = #{hi <= a}, P2 = #{lo < a}, P3 = #{hi <= b}, P4 = #{lo < b}.
-// Covered points gain the element's normalised weight through a difference
-// array; the (few) partly covered points gain w |[a,b] n [lo,hi]| / (hi - lo)
-// directly.  Contributions are 2^-61 fixed point in int64 so that LDS atomics
-// sum them exactly and the result is independent of summation order.
-constexpr int LIKE_THREADS = 256;
-constexpr int LIKE_TILE = 2 * LIKE_THREADS;  // points per sweep tile
+// ---- sweeps over phase-sorted tiles of points (MODEL_SPEC 6 restated) ----
+// Every eclipse / visibility term is a sum over elements of w_k g_k(p), where
+// g_k is non-zero on a contiguous run of points once the points are sorted:
+//  * window mode (exposure windows [lo_p, hi_p], lo and hi non-decreasing):
+//    element [a, b] overlaps points [P1, P4) and covers [P2, P3) whole, with
+//    P1 = #{hi <= a}, P2 = #{lo < a}, P3 = #{hi <= b}, P4 = #{lo < b};
+//  * point mode (zero widths, or the donor's visibility arcs): a < ph < b on
+//    points [#{ph <= a}, #{ph < b}).
+// Whole-covered runs go into a difference array, partly covered points get
+// w |[a,b] n [lo,hi]| / (hi - lo) directly.  Sums are 2^-61 fixed point in
+// int64 so LDS atomics add them exactly, independent of order.
+constexpr int LIKE_THREADS = 512;
+constexpr int LIKE_TILE = LIKE_THREADS;  // one point per thread per tile
+constexpr int LIKE_NC = 2 * LIKE_TILE;   // cells of the phase index
 constexpr double FX_SCALE = 2305843009213693952.0;  // 2^61
 constexpr double FX_INV = 1.0 / FX_SCALE;
 
-__device__ __forceinline__ void count4(const double* __restrict__ lo, const double* __restrict__ hi, int m,
-                                       double a, double b, int& P1, int& P2, int& P3, int& P4)
+struct PhaseIndex {  // sorted phases v[0..m) with a uniform-cell start table
+    const double* v;
+    const int* cell;
+    int m;
+    double t0, ginv;
+};
+
+__device__ __forceinline__ int cell_of(const PhaseIndex& X, double v)
 {
-    // branch-free lower bounds; the trip count depends on m only (wave-uniform)
-    int b1 = 0, b2 = 0, b3 = 0, b4 = 0, len = m;
-    while (len > 1) {
-        const int half = len >> 1;
-        b1 += (hi[b1 + half - 1] <= a) ? half : 0;
-        b2 += (lo[b2 + half - 1] < a) ? half : 0;
-        b3 += (hi[b3 + half - 1] <= b) ? half : 0;
-        b4 += (lo[b4 + half - 1] < b) ? half : 0;
-        len -= half;
-    }
-    P1 = b1 + (hi[b1] <= a);
-    P2 = b2 + (lo[b2] < a);
-    P3 = b3 + (hi[b3] <= b);
-    P4 = b4 + (lo[b4] < b);
+    const double u = (v - X.t0) * X.ginv;
+    return u <= 0.0 ? 0 : (u >= double(LIKE_NC) ? LIKE_NC : int(u));
 }
+
+template <bool LE>
+__device__ __forceinline__ bool below(double v, double x) { return LE ? v <= x : v < x; }
+
+template <bool LE>  // #{v_p < x}, or #{v_p <= x} when LE
+__device__ __forceinline__ int count_below(const PhaseIndex& X, double x)
+{
+    int j = X.cell[cell_of(X, x)];
+    // cells are finer than the mean point spacing: two branch-free steps
+    // usually finish, the walks below only run for clustered points
+    const int last = X.m - 1;
+    j += (j <= last && below<LE>(X.v[min(j, last)], x)) ? 1 : 0;
+    j += (j <= last && below<LE>(X.v[min(j, last)], x)) ? 1 : 0;
+    if (LE) {
+        while (j > 0 && X.v[j - 1] > x) --j;
+        while (j < X.m && X.v[j] <= x) ++j;
+    } else {
+        while (j > 0 && X.v[j - 1] >= x) --j;
+        while (j < X.m && X.v[j] < x) ++j;
+    }
+    return j;
+}
+
+// #{hi <= x} given J = #{lo < x}: hi > lo, so the answer is <= J
+__device__ __forceinline__ int count_le_back(const double* __restrict__ hi, int J, double x)
+{
+    J -= (J > 0 && hi[max(J - 1, 0)] > x) ? 1 : 0;
+    while (J > 0 && hi[J - 1] > x) --J;
+    return J;
+}
+
+// cell[g] ~ #{v < t0 + g / ginv}: point p fills the cells between its
+// predecessor's and its own (the walks in count_below absorb rounding)
+__device__ __forceinline__ PhaseIndex phase_index(const double* v, const int* cell, int m)
+{
+    const double span = v[m - 1] - v[0];
+    return PhaseIndex{v, cell, m, v[0], span > 0.0 ? LIKE_NC / span : 0.0};
+}
+
+__device__ __forceinline__ void build_cells(const double* __restrict__ v, int m, int* __restrict__ cell, int tid)
+{
+    const PhaseIndex X = phase_index(v, cell, m);
+    const double t0 = X.t0, ginv = X.ginv;
+    auto ci = [&](double x) {
+        const double u = (x - t0) * ginv;
+        return u < 0.0 ? -1 : (u >= double(LIKE_NC) ? LIKE_NC : int(u));
+    };
+    if (tid < m) {
+        const int g0 = tid ? ci(v[tid - 1]) : -1, g1 = ci(v[tid]);
+        for (int g = g0 + 1; g <= g1; ++g) cell[g] = tid;
+        if (tid == m - 1)
+            for (int g = g1 + 1; g <= LIKE_NC; ++g) cell[g] = m;
+    }
+}
+
+__device__ __forceinline__ long long to_fx(double x) { return static_cast<long long>(rint(x * FX_SCALE)); }
 
 __device__ __forceinline__ void fx_add(unsigned long long* acc, int p, long long q)
 {
     atomicAdd(acc + p, static_cast<unsigned long long>(q));
+}
+
+// the runs of element [a, b] over the tile's windows [lo_p, hi_p] (lo, hi
+// sorted, hi >= lo): it overlaps [P1, P4) and covers [P2, P3) whole.  A
+// zero-width window is a point: covered when a <= ph <= b, never partial.
+struct Runs {
+    int P1, P2, P3, P4;
+};
+
+__device__ __forceinline__ Runs element_runs(double a, double b, const PhaseIndex& X, const double* __restrict__ hi)
+{
+    Runs R;
+    R.P2 = count_below<false>(X, a);
+    R.P4 = count_below<false>(X, b);
+    R.P1 = count_le_back(hi, R.P2, a);
+    R.P3 = count_le_back(hi, R.P4, b);
+    return R;
+}
+
+// adds wn * (covered fraction) of element [a, b] given its runs
+__device__ __forceinline__ void apply_runs(const Runs& R, double a, double b, double wn, const PhaseIndex& X,
+                                           const double* __restrict__ hi, const double* __restrict__ iw,
+                                           unsigned long long* acc)
+{
+    const int P1 = R.P1, P2 = R.P2, P3 = R.P3, P4 = R.P4;
+    int e0 = P4, s1 = P4;  // partial runs [P1, e0) and [s1, P4)
+    if (P2 < P3) {         // whole-covered run (slot m is never read)
+        const long long q = to_fx(wn);
+        fx_add(acc, P2, q);
+        if (P3 < X.m) fx_add(acc, P3, -q);
+        e0 = P2;
+        s1 = P3;
+    }
+    for (int r = 0; r < 2; ++r) {
+        const int pe = r ? P4 : e0;
+        for (int p = r ? s1 : P1; p < pe; ++p) {
+            const double ov = fmin(b, hi[p]) - fmax(a, X.v[p]);
+            if (ov > 0.0) {
+                const long long q = to_fx(wn * ov * iw[p]);
+                fx_add(acc, p, q);
+                if (p + 1 < X.m) fx_add(acc, p + 1, -q);
+            }
+        }
+    }
 }
 
 __device__ __forceinline__ long long wave_scan_incl(long long v, int lane)
@@ -537,20 +622,137 @@ __device__ __forceinline__ long long wave_scan_incl(long long v, int lane)
     return v;
 }
 
+// inclusive prefix of NA difference arrays at index tid (one entry per thread)
+template <int NA>
+__device__ __forceinline__ void block_scan(unsigned long long (*acc)[LIKE_TILE + 1], long long (*part)[LIKE_THREADS / 64],
+                                           int tid, long long* out)
+{
+    const int lane = tid & 63, wv = tid >> 6;
+    long long w[NA];
+    for (int i = 0; i < NA; ++i) {
+        w[i] = wave_scan_incl(static_cast<long long>(acc[i][tid]), lane);
+        if (lane == 63) part[i][wv] = w[i];
+    }
+    __syncthreads();
+    for (int i = 0; i < NA; ++i) {
+        long long b = 0;
+        for (int k = 0; k < wv; ++k) b += part[i][k];
+        out[i] = w[i] + b;
+    }
+}
+
+__device__ __forceinline__ double wrap_phase(double ph) { return ph - floor(ph + 0.5); }
+
+// tile buffers of one sweep pass: windows [lo, hi] with inverse widths, and
+// the sub-bin centre phases (donor), each with its cell index
+struct TileBufs {
+    double lo[LIKE_TILE], hi[LIKE_TILE], iw[LIKE_TILE];
+    int cell[LIKE_NC + 1];
+};
+
+// writes this thread's window; returns 4 for an invalid width (check_sorted
+// returns 4 for an out-of-order window): either sends the tile to the direct path
+__device__ __forceinline__ int put_window(TileBufs& T, int tid, bool own, double ph, double hw)
+{
+    if (!own) return 0;
+    T.lo[tid] = ph - hw;
+    T.hi[tid] = ph + hw;
+    T.iw[tid] = 1.0 / (2.0 * hw);
+    return (hw >= 0.0) ? 0 : 4;  // negative or NaN widths take the direct path
+}
+
+__device__ __forceinline__ int check_sorted(const TileBufs& T, int tid, bool own)
+{
+    return (own && tid && (T.lo[tid] < T.lo[tid - 1] || T.hi[tid] < T.hi[tid - 1])) ? 4 : 0;
+}
+
+// spot element (lane < NBS) and donor tile (last NDONOR lanes) contributions
+// of one sub-bin pass into acc[0] (spot eclipse) and acc[1..3] (donor sum v)
+__device__ __forceinline__ void sweep_spot_donor(int tid, const PhaseIndex& XW, const TileBufs& TW,
+                                                 const PhaseIndex& XP, double2 abB, double wB,
+                                                 const double* dq, double ivs,
+                                                 unsigned long long (*acc)[LIKE_TILE + 1])
+{
+    if (tid < NBS) {
+        if (abB.x < abB.y) apply_runs(element_runs(abB.x, abB.y, XW, TW.hi), abB.x, abB.y, wB, XW, TW.hi, TW.iw, acc[0]);
+    } else if (tid >= LIKE_THREADS - NDONOR) {
+        const int mr = (tid - (LIKE_THREADS - NDONOR)) & 3;
+        const double vx = dq[0], vy = (mr & 1) ? -dq[1] : dq[1], vz = (mr & 2) ? -dq[2] : dq[2];
+        const double cen = (mr & 1) ? -dq[3] : dq[3];
+        const double hw = (mr & 2) ? 0.5 - dq[4] : dq[4];
+        if (hw > 0.0) {
+            const long long qx = to_fx(vx * ivs), qy = to_fx(vy * ivs), qz = to_fx(vz * ivs);
+            // visible for phases in (cen - hw, cen + hw) mod 1
+            double x1 = -INFINITY, x2 = INFINITY, y1 = 0.0, y2 = 0.0;
+            bool two = false;
+            if (hw < 0.5) {
+                const double lo = cen - hw, hi = cen + hw;
+                if (lo < -0.5) { x2 = hi; y1 = lo + 1.0; y2 = INFINITY; two = true; }
+                else if (hi > 0.5) { x1 = lo; y1 = -INFINITY; y2 = hi - 1.0; two = true; }
+                else { x1 = lo; x2 = hi; }
+            }
+            for (int i = 0; i < (two ? 2 : 1); ++i) {
+                const int P = count_below<true>(XP, i ? y1 : x1), Q = count_below<false>(XP, i ? y2 : x2);
+                if (P < Q) {
+                    fx_add(acc[1], P, qx);
+                    fx_add(acc[2], P, qy);
+                    fx_add(acc[3], P, qz);
+                    if (Q < XP.m) {
+                        fx_add(acc[1], Q, -qx);
+                        fx_add(acc[2], Q, -qy);
+                        fx_add(acc[3], Q, -qz);
+                    }
+                }
+            }
+        }
+    }
+}
+
+// direct (point-major) spot eclipse fraction and donor sum for one point
+__device__ inline void direct_spot_donor(const double2* __restrict__ ABs, const double* __restrict__ sbw,
+                                         const double* __restrict__ DONp, double ph, double h, double e0,
+                                         double e1, double c, double itb, double& eb, double& D)
+{
+    eb = 0.0;
+    D = 0.0;
+    const double l2 = ph - h, h2 = ph + h;
+    for (int k = 0; k < NBS; ++k) {
+        const double2 ab = ABs[k];
+        eb = fma(sbw[k], (h > 0.0) ? fmax(fmin(ab.y, h2) - fmax(ab.x, l2), 0.0)
+                                   : ((ph > ab.x && ph < ab.y) ? 1.0 : 0.0), eb);
+    }
+    eb *= ((h > 0.0) ? 1.0 / (2.0 * h) : 1.0) * itb;
+    for (int q = 0; q < U_DON; ++q) {
+        // max(A + Y, 0) + max(A - Y, 0) = max(A + max(Y, A), 0), A = vx e0 +- vz c
+        const double* d5 = DONp + q * DON_STRIDE;
+        const double y = fabs(d5[1] * e1), z = d5[2] * c;
+        const double A1 = fma(d5[0], e0, z), A2 = fma(d5[0], e0, -z);
+        D += fmax(A1 + fmax(y, A1), 0.0) + fmax(A2 + fmax(y, A2), 0.0);
+    }
+}
+
+#ifdef LFG_PROFILE_LIKE  // diagnostic build only: phase stamps (first tile) into spare geo slots 41..45
+#define LIKE_STAMP(i)                                                                                       \
+    if (tid == 0 && t0 == 0) const_cast<double*>(G)[41 + (i)] = double(__builtin_amdgcn_s_memtime() - tstart)
+#else
+#define LIKE_STAMP(i)
+#endif
+
 template <bool CHI>
 __global__ __launch_bounds__(LIKE_THREADS) void k_lnlike(LikeArgs L)
 {
-    __shared__ double2 sab[NEL];
+#ifdef LFG_PROFILE_LIKE
+    const unsigned long long tstart = __builtin_amdgcn_s_memtime();
+#endif
+    __shared__ double swr[NWD_RINGS + NDISC_R];
     __shared__ double sbw[NBS];
-    __shared__ double swr[NG_WD + NG_DISC];
-    __shared__ double sdb[NDISC_R + 1];
-    __shared__ double2 sgb[NGROUP];
-    __shared__ double2 sdxy[U_DON];
-    __shared__ double sdz[U_DON];
-    __shared__ double slo[LIKE_TILE], shi[LIKE_TILE];
-    __shared__ unsigned long long sacc[2][LIKE_TILE + 1];
-    __shared__ long long sscan[2][LIKE_THREADS / 64];
-    __shared__ double red[4][LIKE_THREADS / 64];
+    __shared__ TileBufs TA, TB;      // WD/disc windows; spot windows of the current sub-bin
+    __shared__ double sph[LIKE_TILE];  // sub-bin centre phases (donor)
+    __shared__ int scp[LIKE_NC + 1];
+    __shared__ unsigned long long sacc[6][LIKE_TILE + 1];
+    __shared__ long long spart[6][LIKE_THREADS / 64];
+    __shared__ double red[3][LIKE_THREADS / 64];
+    __shared__ int sflag[2];
 
     constexpr int nt = LIKE_THREADS, nw = LIKE_THREADS / 64;
     const int pair = blockIdx.x;
@@ -569,59 +771,67 @@ __global__ __launch_bounds__(LIKE_THREADS) void k_lnlike(LikeArgs L)
         return;
     }
     const double* G = L.geo + size_t(pair) * LFG_NGEO;
+    const double* Wt = L.WT + size_t(pair) * WT_N;
+    const double2* AB = L.AB + size_t(pair) * NEL;
+    const double* DONp = L.DON + size_t(pair) * U_DON * DON_STRIDE;
     const double s = G[G_S], c = G[G_C];
 
-    // stage: intervals, spot weights, disc annulus boundaries, donor quads
-    const double2* ABp = L.AB + size_t(pair) * NEL;
-    for (int k = tid; k < NEL; k += nt) sab[k] = ABp[k];
-    double tb = 0.0, dn = 0.0;
-    for (int i = tid; i < NBS + NDISC_R + 1 + NG_WD; i += nt) {
-        if (i < NBS) {
-            const double w = bs_weight(i, G);
-            sbw[i] = w;
-            tb += w;
-        } else if (i < NBS + NDISC_R + 1) {
-            sdb[i - NBS] = disc_boundary(i - NBS, G);
-        } else {
-            swr[i - NBS - NDISC_R - 1] = wd_ring_weight(i - NBS - NDISC_R - 1, G[G_ULIMB]);
+    // tile-0 point data first, so that its latency overlaps the staging loads
+    double px = 0.0, pw = 0.0, py = 0.0, pye = 1.0;
+    if (tid < n) {
+        px = L.x[o0 + tid];
+        pw = L.w ? L.w[o0 + tid] : 0.0;
+        if (CHI) {
+            py = L.y[o0 + tid];
+            pye = L.ye[o0 + tid];
         }
     }
-    const double* Dp = L.DON + size_t(pair) * U_DON * 3;
-    for (int q = tid; q < U_DON; q += nt) {
-        const double vx = Dp[3 * q], vy = Dp[3 * q + 1], vz = Dp[3 * q + 2];
-        sdxy[q] = make_double2(vx, vy);
-        const double zc = vz * c;
-        sdz[q] = zc;
-        // donor normalisation at quadrature (theta = pi/2): X = +-vz c, Y = vy s
-        const double ay = fabs(vy * s);
-        dn += fmax(zc + ay, 0.0) + fmax(zc - ay, 0.0) + fmax(-zc + ay, 0.0) + fmax(-zc - ay, 0.0);
+    // this thread's sweep items, held in registers for every tile: WD/disc
+    // elements tid + i nt, spot element tid (< NBS), donor tile (last lanes)
+    constexpr int NI = (NWD + NDISC + nt - 1) / nt;
+    double2 abk[NI];
+    for (int i = 0; i < NI; ++i) {
+        const int k = tid + i * nt;
+        abk[i] = (k < NWD + NDISC) ? AB[k] : make_double2(1.0, -1.0);
     }
+    double2 abB = make_double2(1.0, -1.0);
+    double wB = 0.0;
+    double dq[DON_STRIDE] = {0.0, 0.0, 0.0, 0.0, 0.0};
+    double tb = 0.0, dn = 0.0, vs = 0.0;
+    if (tid < NBS) {
+        abB = AB[NWD + NDISC + tid];
+        wB = Wt[WT_BS + tid];
+        sbw[tid] = wB;
+        tb = wB;
+    } else if (tid >= nt - NDONOR) {
+        const int t = tid - (nt - NDONOR), mr = t & 3;
+        for (int i = 0; i < DON_STRIDE; ++i) dq[i] = DONp[(t >> 2) * DON_STRIDE + i];
+        // donor normalisation at quadrature (theta = pi/2): e = (0, -s, c)
+        const double vy = (mr & 1) ? -dq[1] : dq[1], vz = (mr & 2) ? -dq[2] : dq[2];
+        dn = fmax(-s * vy + c * vz, 0.0);
+        vs = fabs(dq[0]) + fabs(dq[1]) + fabs(dq[2]);
+    }
+    if (tid >= NBS && tid < NBS + NWD_RINGS) swr[tid - NBS] = wd_ring_weight(tid - NBS, G[G_ULIMB]);
+    else if (tid >= NBS + NWD_RINGS && tid < NBS + NWD_RINGS + NDISC_R)
+        swr[tid - NBS] = Wt[WT_DISC + tid - NBS - NWD_RINGS];
     tb = wave_sum(tb);
     dn = wave_sum(dn);
-    if (lane == 0) { red[0][wv] = tb; red[1][wv] = dn; }
+    vs = wave_sum(vs);
+    if (lane == 0) { red[0][wv] = tb; red[1][wv] = dn; red[2][wv] = vs; }
     __syncthreads();
-    if (tid < NDISC_R) swr[NG_WD + tid] = (TWO_PI / NDISC_AZ) * (sdb[tid + 1] - sdb[tid]);
-    for (int g = wv; g < NGROUP; g += nw) {  // eclipse window of each group, one wave per group
-        const int k0 = group_start(g), k1 = group_start(g + 1);
-        double lo = INFINITY, hi = -INFINITY;
-        for (int k = k0 + lane; k < k1; k += 64) {
-            const double2 ab = sab[k];
-            if (ab.x < ab.y) { lo = fmin(lo, ab.x); hi = fmax(hi, ab.y); }
-        }
-        for (int sh = 32; sh > 0; sh >>= 1) {
-            lo = fmin(lo, __shfl_xor(lo, sh, 64));
-            hi = fmax(hi, __shfl_xor(hi, sh, 64));
-        }
-        if (lane == 0) sgb[g] = make_double2(lo, hi);
-    }
-    // totals telescope: WD 2 pi [F(1) - F(0)], disc 2 pi [P(rdisc) - P(rin)]
+    tb = dn = vs = 0.0;
+    for (int i = 0; i < nw; ++i) { tb += red[0][i]; dn += red[1][i]; vs += red[2][i]; }
     const double ul = G[G_ULIMB];
-    const double twd = TWO_PI * ((1.0 - ul) * 0.5 + ul / 3.0);
-    const double td = TWO_PI * (sdb[NDISC_R] - sdb[0]);
-    tb = dn = 0.0;
-    for (int i = 0; i < nw; ++i) { tb += red[0][i]; dn += red[1][i]; }
-    __syncthreads();
-    const double iwd = 1.0 / twd, id = 1.0 / td;
+    const double twd = TWO_PI * ((1.0 - ul) * 0.5 + ul / 3.0);  // 2 pi [F(1) - F(0)]
+    const double td = Wt[WT_TD];
+    const double iwd = 1.0 / twd, id = 1.0 / td, itb = 1.0 / tb, ivs = 1.0 / vs;
+    double wn[NI];
+    for (int i = 0; i < NI; ++i) {
+        const int k = tid + i * nt;
+        wn[i] = (k < NWD) ? swr[kWdRingOf[k]] * iwd
+                          : (k < NWD + NDISC ? swr[NWD_RINGS + (k - NWD) / NDISC_AZ] * id : 0.0);
+    }
+    wB *= itb;
 
     const double wdF = G[G_WDF], dF = G[G_DF], sF = G[G_SF], rsF = G[G_RSF];
     const double phi0 = G[G_PHI0], fis = G[G_FIS], bden = G[G_BDEN];
@@ -630,168 +840,127 @@ __global__ __launch_bounds__(LIKE_THREADS) void k_lnlike(LikeArgs L)
     double chi = 0.0;
     for (int t0 = 0; t0 < n; t0 += LIKE_TILE) {
         const int m = min(LIKE_TILE, n - t0);
-        // tile phases; the sweep needs lo, hi non-decreasing and widths > 0
-        int bad = 0;
-        for (int i = tid; i < m; i += nt) {
-            const int p = o0 + t0 + i;
-            const double wk = L.w ? L.w[p] : 0.0;
-            const double ph0 = L.x[p] - phi0;
-            const double phc = ph0 - floor(ph0 + 0.5);
-            slo[i] = phc - wk;
-            shi[i] = phc + wk;
-            bad |= !(wk > 0.0);
-            sacc[0][i] = 0ull;
-            sacc[1][i] = 0ull;
+        LIKE_STAMP(0);
+        const bool own = tid < m;
+        const int p = o0 + t0 + tid;
+        if (t0 > 0 && own) {
+            px = L.x[p];
+            pw = L.w ? L.w[p] : 0.0;
+            if (CHI) {
+                py = L.y[p];
+                pye = L.ye[p];
+            }
         }
-        __syncthreads();
-        for (int i = tid + 1; i < m; i += nt) bad |= (slo[i] < slo[i - 1]) || (shi[i] < shi[i - 1]);
-        const bool sweep = !__syncthreads_or(bad);
-        if (sweep) {
-            const double tlo = slo[0], thi = shi[m - 1];
-            for (int k = tid; k < NWD + NDISC; k += nt) {
-                const double2 ab = sab[k];
-                if (!(ab.x < ab.y) || ab.y <= tlo || ab.x >= thi) continue;
-                int comp, ring;
-                if (k < NWD) {
-                    ring = int(sqrt(k * 0.25));
-                    if (4 * (ring + 1) * (ring + 1) <= k) ++ring;
-                    if (4 * ring * ring > k) --ring;
-                    comp = 0;
-                } else {
-                    ring = NG_WD + (k - NWD) / NDISC_AZ;
-                    comp = 1;
-                }
-                const double wn = swr[ring] * (comp ? id : iwd);
-                int P1, P2, P3, P4;
-                count4(slo, shi, m, ab.x, ab.y, P1, P2, P3, P4);
-                unsigned long long* acc = sacc[comp];
-                int e0 = P4, s1 = P4;  // partial ranges [P1, e0) and [s1, P4)
-                if (P2 < P3) {
-                    const long long q = llrint(wn * FX_SCALE);
-                    fx_add(acc, P2, q);
-                    fx_add(acc, P3, -q);
-                    e0 = P2;
-                    s1 = P3;
-                }
-                for (int r = 0; r < 2; ++r) {
-                    const int pe = r ? P4 : e0;
-                    for (int p = r ? s1 : P1; p < pe; ++p) {
-                        const double lo = slo[p], hi = shi[p];
-                        const double ov = fmin(ab.y, hi) - fmax(ab.x, lo);
-                        if (ov > 0.0) {
-                            const long long q = llrint(wn * (ov / (hi - lo)) * FX_SCALE);
-                            fx_add(acc, p, q);
-                            fx_add(acc, p + 1, -q);
+        const double wk = own ? pw : 0.0;
+        const double ph0 = own ? px - phi0 : 0.0;
+        const double phc = wrap_phase(ph0);
+        const double h = wk / S;
+        double fw = 0.0, fd = 0.0, sbs = 0.0, srs = 0.0;
+        // pass j = 0 also carries the WD and disc; passes j > 0 the spot and donor only
+        for (int j = 0; j < S; ++j) {
+            const double ph = wrap_phase(ph0 - wk + (2 * j + 1) * h);
+            if (tid == 0) { sflag[0] = 0; sflag[1] = 0; }
+            int flA = (j == 0) ? put_window(TA, tid, own, phc, wk) : 0;
+            int flB = put_window(TB, tid, own, ph, h);
+            if (own) sph[tid] = ph;
+            for (int i = (j == 0) ? 0 : 2; i < 6; ++i) sacc[i][tid] = 0ull;
+            if (tid == 0)
+                for (int i = (j == 0) ? 0 : 2; i < 6; ++i) sacc[i][nt] = 0ull;
+            __syncthreads();
+            if (j == 0) {
+                flA |= check_sorted(TA, tid, own);
+                if (flA) atomicOr(&sflag[0], flA);
+                build_cells(TA.lo, m, TA.cell, tid);
+            }
+            flB |= check_sorted(TB, tid, own) | ((own && tid && sph[tid] < sph[tid - 1]) ? 4 : 0);
+            if (flB) atomicOr(&sflag[1], flB);
+            build_cells(TB.lo, m, TB.cell, tid);
+            build_cells(sph, m, scp, tid);
+            __syncthreads();
+            const bool swA = (j == 0) && sflag[0] == 0, swB = sflag[1] == 0;  // sweep, else direct
+            LIKE_STAMP(1);
+            if (swA) {
+                const PhaseIndex X = phase_index(TA.lo, TA.cell, m);
+#pragma unroll
+                for (int i = 0; i < NI; ++i)
+                    if (abk[i].x < abk[i].y)
+                        apply_runs(element_runs(abk[i].x, abk[i].y, X, TA.hi), abk[i].x, abk[i].y, wn[i], X,
+                                   TA.hi, TA.iw, sacc[(tid + i * nt < NWD) ? 0 : 1]);
+            }
+            if (swB) {
+                const PhaseIndex XW = phase_index(TB.lo, TB.cell, m), XP = phase_index(sph, scp, m);
+                sweep_spot_donor(tid, XW, TB, XP, abB, wB, dq, ivs, sacc + 2);
+            }
+            __syncthreads();
+            LIKE_STAMP(2);
+            long long r[6];
+            block_scan<6>(sacc, spart, tid, r);
+            LIKE_STAMP(3);
+            if (j == 0) {
+                if (swA) {
+                    fw = double(r[0]) * FX_INV;
+                    fd = double(r[1]) * FX_INV;
+                } else if (own) {  // unsorted / mixed widths: every element against this point
+                    double ewd = 0.0, ed = 0.0;
+                    const double lo = phc - wk, hi = phc + wk;
+                    for (int ring = 0; ring < NWD_RINGS + NDISC_R; ++ring) {
+                        const int k0 = ring < NWD_RINGS ? 4 * ring * ring : NWD + (ring - NWD_RINGS) * NDISC_AZ;
+                        const int k1 = ring < NWD_RINGS ? 4 * (ring + 1) * (ring + 1) : k0 + NDISC_AZ;
+                        double acc = 0.0;
+                        for (int k = k0; k < k1; ++k) {
+                            const double2 ab = AB[k];
+                            acc += (wk > 0.0) ? fmax(fmin(ab.y, hi) - fmax(ab.x, lo), 0.0)
+                                              : ((phc > ab.x && phc < ab.y) ? 1.0 : 0.0);
                         }
+                        if (ring < NWD_RINGS) ewd = fma(swr[ring], acc, ewd); else ed = fma(swr[ring], acc, ed);
                     }
+                    const double nrm = (wk > 0.0) ? 1.0 / (2.0 * wk) : 1.0;
+                    fw = ewd * nrm * iwd;
+                    fd = ed * nrm * id;
                 }
             }
-            __syncthreads();
-            // inclusive scan of both difference arrays (2 entries per thread)
-            long long v0[2], v1[2];
-            for (int j = 0; j < 2; ++j) {
-                const int i = 2 * tid + j;
-                v0[j] = (i < m) ? static_cast<long long>(sacc[0][i]) : 0;
-                v1[j] = (i < m) ? static_cast<long long>(sacc[1][i]) : 0;
+            double sn, cs;
+            sincospi(2.0 * ph, &sn, &cs);  // |2 ph| <= 1: cheap exact reduction
+            const double e0 = s * cs, e1 = -s * sn;
+            double eb = 0.0, D = 0.0;
+            if (swB) {
+                eb = double(r[2]) * FX_INV;
+                D = (e0 * double(r[3]) + e1 * double(r[4]) + c * double(r[5])) * (FX_INV * vs);
+            } else if (own) {
+                direct_spot_donor(AB + NWD + NDISC, sbw, DONp, ph, h, e0, e1, c, itb, eb, D);
             }
-            v0[1] += v0[0];
-            v1[1] += v1[0];
-            const long long w0 = wave_scan_incl(v0[1], lane), w1 = wave_scan_incl(v1[1], lane);
-            if (lane == 63) { sscan[0][wv] = w0; sscan[1][wv] = w1; }
-            __syncthreads();
-            long long b0 = w0 - v0[1], b1 = w1 - v1[1];
-            for (int i = 0; i < wv; ++i) { b0 += sscan[0][i]; b1 += sscan[1][i]; }
-            if (2 * tid < m) { sacc[0][2 * tid] = b0 + v0[0]; sacc[1][2 * tid] = b1 + v1[0]; }
-            if (2 * tid + 1 < m) { sacc[0][2 * tid + 1] = b0 + v0[1]; sacc[1][2 * tid + 1] = b1 + v1[1]; }
-            __syncthreads();
+            double beam = 0.0;
+            if (bden > 0.0) beam = (fis + (1.0 - fis) * fmax(nb0 * e0 + nb1 * e1 + nb2 * c, 0.0)) / bden;
+            sbs += beam * (1.0 - eb);
+            srs += D / dn;
+            __syncthreads();  // the next pass rewrites the tile buffers
         }
-        for (int i = tid; i < m; i += nt) {
-            const int p = o0 + t0 + i;
-            const double lo = slo[i], hi = shi[i];
-            const double wk = L.w ? L.w[p] : 0.0;
-            const double phc = 0.5 * (lo + hi);
-            double fwd, fdd;  // eclipsed fractions of WD and disc
-            if (sweep) {
-                fwd = double(static_cast<long long>(sacc[0][i])) * FX_INV;
-                fdd = double(static_cast<long long>(sacc[1][i])) * FX_INV;
-            } else {  // unsorted points or zero widths: scan the overlapping rings
-                double ewd = 0.0, ed = 0.0;
-                for (unsigned long long msk = group_mask(sgb, 0, NG_WD + NG_DISC, lo, hi); msk; msk &= msk - 1) {
-                    const int g = __builtin_ctzll(msk);
-                    const int k0 = group_start(g), k1 = group_start(g + 1);
-                    const double ov = (wk > 0.0) ? overlap_sum(sab, k0, k1, lo, hi)
-                                                 : inside_count(sab, nullptr, k0, k1, phc);
-                    if (g < NG_WD) ewd = fma(swr[g], ov, ewd); else ed = fma(swr[g], ov, ed);
-                }
-                if (wk > 0.0) {
-                    ewd /= 2.0 * wk;
-                    ed /= 2.0 * wk;
-                }
-                fwd = ewd * iwd;
-                fdd = ed * id;
-            }
-            const double fw = wdF * (1.0 - fwd);
-            const double fd = dF * (1.0 - fdd);
-            const double ph0 = L.x[p] - phi0;
-            const double h = wk / S;
-            double sbs = 0.0, srs = 0.0;
-#pragma unroll 1
-            for (int j = 0; j < S; ++j) {
-                double ph = ph0 - wk + (2 * j + 1) * h;
-                ph -= floor(ph + 0.5);
-                double sn, cs;
-                sincospi(2.0 * ph, &sn, &cs);  // |2 ph| <= 1: cheap exact reduction
-                const double e0 = s * cs, e1 = -s * sn;
-                double beam = 0.0;
-                if (bden > 0.0) beam = (fis + (1.0 - fis) * fmax(nb0 * e0 + nb1 * e1 + nb2 * c, 0.0)) / bden;
-                double eb = 0.0;
-                const double l2 = ph - h, h2 = ph + h;
-                for (unsigned long long msk = group_mask(sgb, NG_WD + NG_DISC, NGROUP, l2, h2); msk;
-                     msk &= msk - 1) {
-                    const int g = __builtin_ctzll(msk);
-                    const int k0 = group_start(g), k1 = group_start(g + 1);
-                    const double* wt = sbw + (k0 - NWD - NDISC);
-                    eb += (h > 0.0) ? overlap_wsum(sab, wt, k0, k1, l2, h2) : inside_count(sab, wt, k0, k1, ph);
-                }
-                if (h > 0.0) eb /= 2.0 * h;
-                sbs += beam * (1.0 - eb / tb);
-                // donor: 100 quads of mirror tiles (vx, +-vy, +-vz); for A = vx e0 +- vz c and
-                // Y = |vy e1|: max(A + Y, 0) + max(A - Y, 0) = max(A + max(Y, A), 0)
-                double d0 = 0.0, d1 = 0.0;
-#pragma unroll 4
-                for (int q = 0; q < U_DON; ++q) {
-                    const double2 v = sdxy[q];
-                    const double z = sdz[q];
-                    const double y = fabs(v.y * e1);
-                    const double A1 = fma(v.x, e0, z), A2 = fma(v.x, e0, -z);
-                    d0 += fmax(A1 + fmax(y, A1), 0.0);
-                    d1 += fmax(A2 + fmax(y, A2), 0.0);
-                }
-                srs += (d0 + d1) / dn;
-            }
+        if (own) {
+            const double fwv = wdF * (1.0 - fw), fdv = dF * (1.0 - fd);
             const double fb = sF * sbs / S, fr = rsF * srs / S;
-            const double f = fw + fd + fb + fr;
-            if (L.flux) L.flux[size_t(pair) * n + t0 + i] = f;
+            const double f = fwv + fdv + fb + fr;
+            const int pi = t0 + tid;
+            if (L.flux) L.flux[size_t(pair) * n + pi] = f;
             if (L.comps) {
-                L.comps[(size_t(0) * L.npairs + pair) * n + t0 + i] = fw;
-                L.comps[(size_t(1) * L.npairs + pair) * n + t0 + i] = fd;
-                L.comps[(size_t(2) * L.npairs + pair) * n + t0 + i] = fb;
-                L.comps[(size_t(3) * L.npairs + pair) * n + t0 + i] = fr;
+                L.comps[(size_t(0) * L.npairs + pair) * n + pi] = fwv;
+                L.comps[(size_t(1) * L.npairs + pair) * n + pi] = fdv;
+                L.comps[(size_t(2) * L.npairs + pair) * n + pi] = fb;
+                L.comps[(size_t(3) * L.npairs + pair) * n + pi] = fr;
             }
             if (CHI) {
-                const double r = (L.y[p] - f) / L.ye[p];
+                const double r = (py - f) / pye;
                 chi += isnan(f) ? INFINITY : r * r;
             }
         }
-        __syncthreads();  // tile buffers are rewritten by the next tile
+        LIKE_STAMP(4);
     }
     if (CHI) {
         chi = wave_sum(chi);
-        if (lane == 0) red[2][wv] = chi;
+        if (lane == 0) red[0][wv] = chi;
         __syncthreads();
         if (tid == 0) {
             double tot = 0.0;
-            for (int i = 0; i < nw; ++i) tot += red[2][i];
+            for (int i = 0; i < nw; ++i) tot += red[0][i];
             L.lle[pair] = -0.5 * tot;
         }
     }
@@ -804,7 +973,10 @@ __global__ void k_combine(int W, int E, const double* __restrict__ prior, const 
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= W) return;
     double lp = prior[w];
-    for (int e = 0; e < E; ++e) lp += geo[(size_t(w) * E + e) * LFG_NGEO + G_RPRIOR];
+    for (int e = 0; e < E; ++e) {
+        const double* G = geo + (size_t(w) * E + e) * LFG_NGEO;
+        lp += G[G_RPRIOR] + G[G_RPRIOR_BS];
+    }
     if (!isfinite(lp)) {
         for (int e = 0; e < E; ++e) lle[size_t(w) * E + e] = -INFINITY;
         lnp[w] = -INFINITY;
@@ -843,13 +1015,17 @@ __device__ inline uint4 draw(unsigned long long seed, unsigned long long step, i
 
 // emcee StretchMove.get_proposal: z = ((a-1) u + 1)^2 / a,
 // q = c_j - (c_j - s) z = c_j + z (s - c_j), factor = (ndim - 1) ln z
+// step counter: by value, or (stepp != nullptr) from device memory so that
+// a captured HIP graph replays with the current step
 __global__ void k_propose(const double* __restrict__ pos, int W, int ndim, int half, double a,
-                          unsigned long long seed, unsigned long long step, double* __restrict__ q,
+                          unsigned long long seed, unsigned long long step,
+                          const unsigned long long* __restrict__ stepp, double* __restrict__ q,
                           double* __restrict__ zfac)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int ns = W / 2;
     if (i >= ns) return;
+    if (stepp) step = *stepp;
     const uint4 r = draw(seed, step, half, 0, i);
     const double u = u53(r.x, r.y);
     const double zr = (a - 1.0) * u + 1.0;
@@ -866,11 +1042,12 @@ __global__ void k_propose(const double* __restrict__ pos, int W, int ndim, int h
 __global__ void k_accept(double* __restrict__ pos, double* __restrict__ lnp, int W, int ndim, int half,
                          const double* __restrict__ q, const double* __restrict__ zfac,
                          const double* __restrict__ lnp_new, unsigned long long seed, unsigned long long step,
-                         int* __restrict__ naccept)
+                         const unsigned long long* __restrict__ stepp, int* __restrict__ naccept)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int ns = W / 2;
     if (i >= ns) return;
+    if (stepp) step = *stepp;
     const int w = half * ns + i;
     const uint4 r = draw(seed, step, half, 1, i);
     const double lu = log(u53(r.x, r.y));
@@ -913,16 +1090,68 @@ __global__ void k_roche(int op, const double* __restrict__ a, const double* __re
 
 inline int launch_ok() { return hipGetLastError() == hipSuccess ? LFG_OK : LFG_E_LAUNCH; }
 
-int run_front(const SetupArgs& S, const Ws& ws, hipStream_t st)
+// Library-owned side stream (one per device) for the bright-spot branch:
+//   caller stream:  k_setup -> [geo] -> k_elements(WD, disc, donor) -> wait(join)
+//   side stream:    wait(fork) -> k_bspot -> wait(geo) -> k_elements(spot) -> [join]
+struct SideStream {
+    hipStream_t s = nullptr;
+    hipEvent_t fork = nullptr, geo = nullptr, join = nullptr;
+    std::mutex mu;  // serialises the record/wait sequence of concurrent host callers
+};
+
+SideStream* side_stream()
 {
+    static std::mutex init_mu;
+    static SideStream tab[LFG_MAX_DEVICES];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= LFG_MAX_DEVICES) return nullptr;
+    SideStream& d = tab[dev];
+    std::lock_guard<std::mutex> g(init_mu);
+    if (!d.s) {
+        hipStream_t s;
+        if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+        if (hipEventCreateWithFlags(&d.fork, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&d.geo, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&d.join, hipEventDisableTiming) != hipSuccess)
+            return nullptr;
+        d.s = s;
+    }
+    return &d;
+}
+
+// k_setup + k_bspot + k_elements with the fork/join above; ev (nullable):
+// events 1 and 2 are recorded on the caller stream after k_setup and after the join
+int run_front(const SetupArgs& S, const Ws& ws, hipStream_t st, void* const* ev)
+{
+    SideStream* sd = side_stream();
+    if (!sd) return LFG_E_LAUNCH;
+    std::lock_guard<std::mutex> g(sd->mu);
+    auto mark = [&](int i) {
+        if (ev && ev[i]) (void)hipEventRecord(static_cast<hipEvent_t>(ev[i]), st);
+    };
     const int npairs = S.W * S.E;
     const int nlanes = npairs + S.W;
+    if (hipEventRecord(sd->fork, st) != hipSuccess || hipStreamWaitEvent(sd->s, sd->fork, 0) != hipSuccess)
+        return LFG_E_LAUNCH;
+    hipLaunchKernelGGL(k_bspot, dim3((npairs + SETUP_BLOCK - 1) / SETUP_BLOCK), dim3(SETUP_BLOCK), 0, sd->s, S,
+                       ws.bstatus);
+    if (launch_ok() != LFG_OK) return LFG_E_LAUNCH;
     hipLaunchKernelGGL(k_setup, dim3((nlanes + SETUP_BLOCK - 1) / SETUP_BLOCK), dim3(SETUP_BLOCK), 0, st, S);
     if (launch_ok() != LFG_OK) return LFG_E_LAUNCH;
-    const long nthreads = long(npairs) * NUNIQ;
-    hipLaunchKernelGGL(k_elements, dim3(unsigned((nthreads + ELEM_BLOCK - 1) / ELEM_BLOCK)), dim3(ELEM_BLOCK), 0,
-                       st, ws.geo, ws.status, npairs, ws.ab, ws.donor);
-    return launch_ok();
+    mark(1);
+    if (hipEventRecord(sd->geo, st) != hipSuccess || hipStreamWaitEvent(sd->s, sd->geo, 0) != hipSuccess)
+        return LFG_E_LAUNCH;
+    const long nmain = long(npairs) * U_MAIN, nbs = long(npairs) * U_BS;
+    hipLaunchKernelGGL(k_elements, dim3(unsigned((nmain + ELEM_BLOCK - 1) / ELEM_BLOCK)), dim3(ELEM_BLOCK), 0, st,
+                       ws.geo, ws.status, npairs, ws.ab, ws.donor, ws.wts, 0, U_MAIN, nullptr, nullptr);
+    if (launch_ok() != LFG_OK) return LFG_E_LAUNCH;
+    hipLaunchKernelGGL(k_elements, dim3(unsigned((nbs + ELEM_BLOCK - 1) / ELEM_BLOCK)), dim3(ELEM_BLOCK), 0, sd->s,
+                       ws.geo, ws.status, npairs, ws.ab, ws.donor, ws.wts, U_MAIN, U_BS, ws.bstatus, ws.status);
+    if (launch_ok() != LFG_OK) return LFG_E_LAUNCH;
+    if (hipEventRecord(sd->join, sd->s) != hipSuccess || hipStreamWaitEvent(st, sd->join, 0) != hipSuccess)
+        return LFG_E_LAUNCH;
+    mark(2);
+    return LFG_OK;
 }
 
 }  // namespace
@@ -944,10 +1173,10 @@ int lfg_flux(const double* pars, int W, int P, const double* x, const double* w,
     hipStream_t st = static_cast<hipStream_t>(stream);
     SetupArgs S{pars, W, P, 1, P, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
                 ws.geo, ws.status, ws.prior};
-    int rc = run_front(S, ws, st);
+    int rc = run_front(S, ws, st, nullptr);
     if (rc) return rc;
     if (N > 0) {
-        LikeArgs L{ws.geo, ws.status, ws.ab, ws.donor, 1, nullptr, N, x, nullptr, nullptr, w,
+        LikeArgs L{ws.geo, ws.status, ws.ab, ws.donor, ws.wts, 1, nullptr, N, x, nullptr, nullptr, w,
                    nsub, flux, comps, nullptr, W};
         hipLaunchKernelGGL(k_lnlike<false>, dim3(W), dim3(LIKE_THREADS), 0, st, L);
         if ((rc = launch_ok())) return rc;
@@ -970,19 +1199,11 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
     SetupArgs S{walkers, W, T->ndim, T->E, 18, T->gather, T->npars, T->consts, T->prior_type, T->prior_p1,
                 T->prior_p2, T->prior_norm, T->roche_priors, ws.geo, ws.status, ws.prior};
     const int npairs = W * T->E;
-    const int nlanes = npairs + W;
     mark(0);
-    hipLaunchKernelGGL(k_setup, dim3((nlanes + SETUP_BLOCK - 1) / SETUP_BLOCK), dim3(SETUP_BLOCK), 0, st, S);
-    int rc = launch_ok();
+    int rc = run_front(S, ws, st, ev);
     if (rc) return rc;
-    mark(1);
-    const long nthreads = long(npairs) * NUNIQ;
-    hipLaunchKernelGGL(k_elements, dim3(unsigned((nthreads + ELEM_BLOCK - 1) / ELEM_BLOCK)), dim3(ELEM_BLOCK), 0,
-                       st, ws.geo, ws.status, npairs, ws.ab, ws.donor);
-    if ((rc = launch_ok())) return rc;
-    mark(2);
     double* lle = lnlike_e ? lnlike_e : ws.lle;
-    LikeArgs L{ws.geo, ws.status, ws.ab, ws.donor, T->E, T->off, T->max_n, T->x, T->y, T->ye,
+    LikeArgs L{ws.geo, ws.status, ws.ab, ws.donor, ws.wts, T->E, T->off, T->max_n, T->x, T->y, T->ye,
                T->w, T->nsub, nullptr, nullptr, lle, npairs};
     hipLaunchKernelGGL(k_lnlike<true>, dim3(npairs), dim3(LIKE_THREADS), 0, st, L);
     if ((rc = launch_ok())) return rc;
@@ -1005,27 +1226,56 @@ int lfg_lnprob_timed(const double* walkers, int W, const lfg_tree* T, double* ln
     return lnprob_impl(walkers, W, T, lnp, lnlike_e, wsp, ws_bytes, stream, ev);
 }
 
-int lfg_stretch_propose(const double* pos, int W, int ndim, int half, double a, unsigned long long seed,
-                        unsigned long long step, double* q, double* zfac, void* stream)
+static int propose_impl(const double* pos, int W, int ndim, int half, double a, unsigned long long seed,
+                        unsigned long long step, const unsigned long long* stepp, double* q, double* zfac,
+                        void* stream)
 {
     if (W < 4 || (W & 1) || ndim <= 0 || (half != 0 && half != 1) || !(a > 1.0) || !pos || !q || !zfac)
         return LFG_E_ARGS;
     const int ns = W / 2;
     hipLaunchKernelGGL(k_propose, dim3((ns + 63) / 64), dim3(64), 0, static_cast<hipStream_t>(stream), pos, W,
-                       ndim, half, a, seed, step, q, zfac);
+                       ndim, half, a, seed, step, stepp, q, zfac);
     return launch_ok();
+}
+
+static int accept_impl(double* pos, double* lnp, int W, int ndim, int half, const double* q, const double* zfac,
+                       const double* lnp_new, unsigned long long seed, unsigned long long step,
+                       const unsigned long long* stepp, int* naccept, void* stream)
+{
+    if (W < 4 || (W & 1) || ndim <= 0 || (half != 0 && half != 1) || !pos || !lnp || !q || !zfac || !lnp_new)
+        return LFG_E_ARGS;
+    const int ns = W / 2;
+    hipLaunchKernelGGL(k_accept, dim3((ns + 63) / 64), dim3(64), 0, static_cast<hipStream_t>(stream), pos, lnp,
+                       W, ndim, half, q, zfac, lnp_new, seed, step, stepp, naccept);
+    return launch_ok();
+}
+
+int lfg_stretch_propose(const double* pos, int W, int ndim, int half, double a, unsigned long long seed,
+                        unsigned long long step, double* q, double* zfac, void* stream)
+{
+    return propose_impl(pos, W, ndim, half, a, seed, step, nullptr, q, zfac, stream);
 }
 
 int lfg_stretch_accept(double* pos, double* lnp, int W, int ndim, int half, const double* q, const double* zfac,
                        const double* lnp_new, unsigned long long seed, unsigned long long step, int* naccept,
                        void* stream)
 {
-    if (W < 4 || (W & 1) || ndim <= 0 || (half != 0 && half != 1) || !pos || !lnp || !q || !zfac || !lnp_new)
-        return LFG_E_ARGS;
-    const int ns = W / 2;
-    hipLaunchKernelGGL(k_accept, dim3((ns + 63) / 64), dim3(64), 0, static_cast<hipStream_t>(stream), pos, lnp,
-                       W, ndim, half, q, zfac, lnp_new, seed, step, naccept);
-    return launch_ok();
+    return accept_impl(pos, lnp, W, ndim, half, q, zfac, lnp_new, seed, step, nullptr, naccept, stream);
+}
+
+int lfg_stretch_propose_dev(const double* pos, int W, int ndim, int half, double a, unsigned long long seed,
+                            const unsigned long long* step_dev, double* q, double* zfac, void* stream)
+{
+    if (!step_dev) return LFG_E_ARGS;
+    return propose_impl(pos, W, ndim, half, a, seed, 0, step_dev, q, zfac, stream);
+}
+
+int lfg_stretch_accept_dev(double* pos, double* lnp, int W, int ndim, int half, const double* q,
+                           const double* zfac, const double* lnp_new, unsigned long long seed,
+                           const unsigned long long* step_dev, int* naccept, void* stream)
+{
+    if (!step_dev) return LFG_E_ARGS;
+    return accept_impl(pos, lnp, W, ndim, half, q, zfac, lnp_new, seed, 0, step_dev, naccept, stream);
 }
 
 int lfg_event_create(void** ev)
@@ -1059,7 +1309,7 @@ int lfg_elements(const double* pars, int W, int P, double* a, double* b, double*
     hipStream_t st = static_cast<hipStream_t>(stream);
     SetupArgs S{pars, W, P, 1, P, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
                 ws.geo, ws.status, ws.prior};
-    int rc = run_front(S, ws, st);
+    int rc = run_front(S, ws, st, nullptr);
     if (rc) return rc;
     if (a || b || wgt || donor) {
         const long nt = long(W) * NEL;

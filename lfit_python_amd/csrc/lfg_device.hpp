@@ -52,6 +52,7 @@ enum Geo {
     G_BSX, G_BSY, G_BSVX, G_BSVY, G_L, G_UPK, G_UMAX, G_LNPK,
     G_EXP1, G_EXP2, G_CAZ, G_SAZ, G_NB0, G_NB1, G_NB2, G_BDEN,
     G_FIS, G_PHI0, G_WDF, G_DF, G_SF, G_RSF, G_RPRIOR, G_RCAL,
+    G_RPRIOR_BS,  // bright-spot part of the eclipse Roche prior (k_bspot)
     G_COUNT
 };
 static_assert(G_COUNT <= 48, "LFG_NGEO");

@@ -63,6 +63,20 @@ class HipStretchOps:
                                        self._vp(naccept), _native.stream_ptr(self.device))
         _native.check(rc, "lfg_stretch_accept")
 
+    # step counter in device memory (int64 tensor of one element): HIP-graph capturable
+    def propose_dev(self, pos, half, a, seed, step_dev, q, zfac):
+        W, ndim = pos.shape
+        rc = self.L.lfg_stretch_propose_dev(self._vp(pos), W, ndim, half, a, seed, self._vp(step_dev),
+                                            self._vp(q), self._vp(zfac), _native.stream_ptr(self.device))
+        _native.check(rc, "lfg_stretch_propose_dev")
+
+    def accept_dev(self, pos, lnp, half, q, zfac, lnp_new, seed, step_dev, naccept):
+        W, ndim = pos.shape
+        rc = self.L.lfg_stretch_accept_dev(self._vp(pos), self._vp(lnp), W, ndim, half, self._vp(q),
+                                           self._vp(zfac), self._vp(lnp_new), seed, self._vp(step_dev),
+                                           self._vp(naccept), _native.stream_ptr(self.device))
+        _native.check(rc, "lfg_stretch_accept_dev")
+
 
 class EnsembleSampler:
     """evaluator(x [n, ndim] tensor, out=None) -> ln_prob [n] on evaluator.device.
@@ -97,6 +111,13 @@ class EnsembleSampler:
         self.chain = None
         self.lnprob_chain = None
         self.timer = None  # optional callable(walkers) -> lnp used instead of self.ev
+        # HIP-graph replay of whole iterations (single rank, HIP ops): the first
+        # step() after enabling runs eagerly, the next captures, later ones replay
+        self.use_graph = False
+        self._graph = None
+        self._step_dev = None
+        self._dev_iter = 0
+        self._warm = False  # one eager iteration (allocations, side stream) before capture
 
     def _gather(self, out, mine):
         import torch.distributed as dist
@@ -129,8 +150,40 @@ class EnsembleSampler:
         self._gather(out, mine)
         return out
 
+    def _graphable(self):
+        return (self.use_graph and self.world == 1 and self.timer is None
+                and isinstance(self.ops, HipStretchOps) and self.dev.type == "cuda")
+
+    def _graph_body(self):
+        for half in (0, 1):
+            self.ops.propose_dev(self.pos, half, self.a, self.seed, self._step_dev, self.q, self.zfac)
+            self.ev(self.q, out=self.lnp_new)
+            self.ops.accept_dev(self.pos, self.lnp, half, self.q, self.zfac, self.lnp_new, self.seed,
+                                self._step_dev, self.naccept)
+        self._step_dev.add_(1)
+
+    def _graph_step(self):
+        import torch
+        if self._graph is None:
+            self._step_dev = torch.full((1,), self.iteration, dtype=torch.int64, device=self.dev)
+            self._dev_iter = self.iteration
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._graph_body()
+            self._graph = g
+        if self._dev_iter != self.iteration:  # iteration changed from outside (reset)
+            self._step_dev.fill_(self.iteration)
+            self._dev_iter = self.iteration
+        self._graph.replay()
+        self.iteration += 1
+        self._dev_iter += 1
+
     def step(self):
         """One emcee iteration: both halves, in place."""
+        if self._graphable() and self._warm:
+            self._graph_step()
+            return
+        self._warm = True
         for half in (0, 1):
             self.ops.propose(self.pos, half, self.a, self.seed, self.iteration, self.q, self.zfac)
             if self.world == 1:

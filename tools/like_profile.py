@@ -1,0 +1,32 @@
+"""Diagnostic: per-phase cycle stamps of k_lnlike (build with -DLFG_PROFILE_LIKE,
+load via LFG_LIB).  Stamps (s_memtime ticks from kernel entry, thread 0 of each
+block, first tile, last sub-bin pass): 0 staged, 1 phases + cells,
+2 sweep, 3 scan, 4 tile end."""
+import os, sys, ctypes
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np, torch
+from lfit_python_amd import _native
+from tests.helpers import random_pars, phase_grid
+L = _native.lib()
+dev = torch.device('cuda', 0)
+W = int(sys.argv[1]) if len(sys.argv) > 1 else 512
+pars = torch.as_tensor(random_pars(W, complex_bs=True, seed=1), device=dev).contiguous()
+x, w = phase_grid(300)
+X = torch.as_tensor(x, device=dev); Wd = torch.as_tensor(w, device=dev)
+flux = torch.empty((W, len(x)), dtype=torch.float64, device=dev)
+st = torch.empty(W, dtype=torch.int32, device=dev)
+ws = torch.empty(L.lfg_workspace_size(W, 1), dtype=torch.uint8, device=dev)
+vp = lambda t: ctypes.c_void_p(t.data_ptr())
+for _ in range(3):
+    rc = L.lfg_flux(vp(pars), W, 18, vp(X), vp(Wd), len(x), 1, vp(flux), None, vp(st), vp(ws), ws.numel(),
+                    _native.stream_ptr())
+    assert rc == 0
+torch.cuda.synchronize()
+g = ws[:W * 48 * 8].view(torch.float64).view(W, 48).cpu().numpy()
+ok = st.cpu().numpy() == 0
+names = ['staged', 'cells', 'sweep', 'scan', 'end']
+prev = np.zeros(ok.sum())
+for i, nm in enumerate(names):
+    v = g[ok, 41 + i]
+    print('%-8s cum mean %8.0f  max %8.0f   delta mean %8.0f' % (nm, v.mean(), v.max(), (v - prev).mean()))
+    prev = v
