@@ -299,12 +299,16 @@ __global__ __launch_bounds__(ELEM_BLOCK) void k_elements(const double* __restric
                                                          double* __restrict__ WT, int u0, int nu,
                                                          const int* __restrict__ bstatus, int* mstatus)
 {
-    // lanes cover unique items [u0, u0 + nu) of every pair; the spot launch
-    // (u0 = U_MAIN) also folds the stream status into the pair status
-    const long t = long(blockIdx.x) * ELEM_BLOCK + threadIdx.x;
-    const int pair = int(t / nu);
-    const int u = u0 + int(t - long(pair) * nu);
-    if (pair >= npairs) return;
+    // blocks cover unique items [u0, u0 + nu) of every pair in chunks of
+    // blockDim.x; block b takes pair b % npairs, so that (with npairs a
+    // multiple of 8 and blocks dealt round-robin over the XCDs) a pair's
+    // tables are written on the XCD whose L2 k_lnlike block `pair` reads them
+    // from -- speed only.  The spot launch (u0 = U_MAIN) also folds the
+    // stream status into the pair status.
+    const int pair = int(blockIdx.x % unsigned(npairs));
+    const int ui = int(blockIdx.x / unsigned(npairs)) * int(blockDim.x) + int(threadIdx.x);
+    if (ui >= nu) return;
+    const int u = u0 + ui;
     if (status[pair] != ST_OK) return;
     if (bstatus) {
         const int bst = bstatus[pair];
@@ -508,38 +512,80 @@ __device__ __forceinline__ int cell_of(const PhaseIndex& X, double v)
     return u <= 0.0 ? 0 : (u >= double(LIKE_NC) ? LIKE_NC : int(u));
 }
 
+// #{v_p < x} (or #{v_p <= x} when LE).  cell[ci(x)] counts the points whose
+// cell index is below x's, all of which lie below x (ci is monotone), so the
+// walk only goes forward: usually zero or one point, two unrolled steps
 template <bool LE>
-__device__ __forceinline__ bool below(double v, double x) { return LE ? v <= x : v < x; }
-
-template <bool LE>  // #{v_p < x}, or #{v_p <= x} when LE
 __device__ __forceinline__ int count_below(const PhaseIndex& X, double x)
 {
     int j = X.cell[cell_of(X, x)];
-    // cells are finer than the mean point spacing: two branch-free steps
-    // usually finish, the walks below only run for clustered points
     const int last = X.m - 1;
-    j += (j <= last && below<LE>(X.v[min(j, last)], x)) ? 1 : 0;
-    j += (j <= last && below<LE>(X.v[min(j, last)], x)) ? 1 : 0;
-    if (LE) {
-        while (j > 0 && X.v[j - 1] > x) --j;
-        while (j < X.m && X.v[j] <= x) ++j;
-    } else {
-        while (j > 0 && X.v[j - 1] >= x) --j;
-        while (j < X.m && X.v[j] < x) ++j;
+    bool adv = false;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const double vj = X.v[min(j, last)];
+        adv = (j <= last) & (LE ? (vj <= x) : (vj < x));
+        j += adv ? 1 : 0;
     }
+    if (adv)  // clustered points: keep walking
+        while (j <= last && (LE ? (X.v[j] <= x) : (X.v[j] < x))) ++j;
     return j;
 }
 
-// #{hi <= x} given J = #{lo < x}: hi > lo, so the answer is <= J
+// count_below<false> for Q queries in lockstep, so that their LDS chains overlap
+template <int Q>
+__device__ __forceinline__ void count_lt_multi(const PhaseIndex& X, const double (&x)[Q], int (&j)[Q])
+{
+    const int last = X.m - 1;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) j[q] = X.cell[cell_of(X, x[q])];
+    bool adv[Q];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const double vj = X.v[min(j[q], last)];
+            adv[q] = (j[q] <= last) & (vj < x[q]);
+            j[q] += adv[q] ? 1 : 0;
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < Q; ++q)
+        if (adv[q])
+            while (j[q] <= last && X.v[j[q]] < x[q]) ++j[q];
+}
+
+// count_le_back for Q queries in lockstep
+template <int Q>
+__device__ __forceinline__ void count_le_back_multi(const double* __restrict__ hi, const double (&x)[Q],
+                                                    const int (&J)[Q], int (&out)[Q])
+{
+    bool back[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        back[q] = (J[q] > 0) & (hi[max(J[q] - 1, 0)] > x[q]);
+        out[q] = J[q] - (back[q] ? 1 : 0);
+    }
+#pragma unroll
+    for (int q = 0; q < Q; ++q)
+        if (back[q])
+            while (out[q] > 0 && hi[out[q] - 1] > x[q]) --out[q];
+}
+
+// #{hi <= x} given J = #{lo < x}: hi > lo, so the answer is <= J; the points
+// straddling x (usually one) are stepped over backwards
 __device__ __forceinline__ int count_le_back(const double* __restrict__ hi, int J, double x)
 {
-    J -= (J > 0 && hi[max(J - 1, 0)] > x) ? 1 : 0;
-    while (J > 0 && hi[J - 1] > x) --J;
+    const bool back = (J > 0) & (hi[max(J - 1, 0)] > x);
+    J -= back ? 1 : 0;
+    if (back)
+        while (J > 0 && hi[J - 1] > x) --J;
     return J;
 }
 
-// cell[g] ~ #{v < t0 + g / ginv}: point p fills the cells between its
-// predecessor's and its own (the walks in count_below absorb rounding)
+// cell[g] = #{p : ci(v_p) < g} with ci(v) = floor((v - t0) ginv) clamped to
+// [-1, NC] exactly as cell_of computes it: point p fills the cells
+// (ci(v_{p-1}), ci(v_p)], the last point also the cells above its own
 __device__ __forceinline__ PhaseIndex phase_index(const double* v, const int* cell, int m)
 {
     const double span = v[m - 1] - v[0];
@@ -612,6 +658,11 @@ __device__ __forceinline__ void apply_runs(const Runs& R, double a, double b, do
         }
     }
 }
+
+// WD/disc element of sweep slot g: a stride-37 permutation of [0, NWD + NDISC)
+// so that the lanes of a wave take elements of different rings and azimuths
+// (their runs start at different points: fewer same-address LDS atomics)
+__device__ __forceinline__ int sweep_item(int g) { return g < NWD + NDISC ? (g * 37) % (NWD + NDISC) : g; }
 
 __device__ __forceinline__ long long wave_scan_incl(long long v, int lane)
 {
@@ -731,7 +782,7 @@ __device__ inline void direct_spot_donor(const double2* __restrict__ ABs, const 
     }
 }
 
-#ifdef LFG_PROFILE_LIKE  // diagnostic build only: phase stamps (first tile) into spare geo slots 41..45
+#ifdef LFG_PROFILE_LIKE  // diagnostic build only: phase stamps (first tile) into spare geo slots 41..46
 #define LIKE_STAMP(i)                                                                                       \
     if (tid == 0 && t0 == 0) const_cast<double*>(G)[41 + (i)] = double(__builtin_amdgcn_s_memtime() - tstart)
 #else
@@ -760,24 +811,17 @@ __global__ __launch_bounds__(LIKE_THREADS) void k_lnlike(LikeArgs L)
     const int e = pair % L.E;
     const int o0 = L.off ? L.off[e] : 0;
     const int n = L.off ? L.off[e + 1] - o0 : L.N;
-    const int st = L.status[pair];
-    if (st != ST_OK) {
-        for (int p = tid; p < n; p += nt) {
-            if (L.flux) L.flux[size_t(pair) * n + p] = NAN;
-            if (L.comps)
-                for (int m = 0; m < 4; ++m) L.comps[(size_t(m) * L.npairs + pair) * n + p] = NAN;
-        }
-        if (CHI && tid == 0) L.lle[pair] = -INFINITY;
-        return;
-    }
     const double* G = L.geo + size_t(pair) * LFG_NGEO;
     const double* Wt = L.WT + size_t(pair) * WT_N;
     const double2* AB = L.AB + size_t(pair) * NEL;
     const double* DONp = L.DON + size_t(pair) * U_DON * DON_STRIDE;
-    const double s = G[G_S], c = G[G_C];
 
-    // tile-0 point data first, so that its latency overlaps the staging loads
-    double px = 0.0, pw = 0.0, py = 0.0, pye = 1.0;
+    // every global load of the prologue is issued before anything waits on
+    // one (the status included): a single memory round trip
+    const int st = L.status[pair];
+    const double s = G[G_S], c = G[G_C], ul = G[G_ULIMB];
+    const double td = Wt[WT_TD];
+    double px = 0.0, pw = 0.0, py = 0.0, pye = 1.0;  // tile-0 point of this thread
     if (tid < n) {
         px = L.x[o0 + tid];
         pw = L.w ? L.w[o0 + tid] : 0.0;
@@ -787,33 +831,59 @@ __global__ __launch_bounds__(LIKE_THREADS) void k_lnlike(LikeArgs L)
         }
     }
     // this thread's sweep items, held in registers for every tile: WD/disc
-    // elements tid + i nt, spot element tid (< NBS), donor tile (last lanes)
+    // elements sweep_item(tid + i nt) with their ring weights, spot element
+    // tid (< NBS), donor tile (last NDONOR lanes)
     constexpr int NI = (NWD + NDISC + nt - 1) / nt;
     double2 abk[NI];
+    double wr[NI];
     for (int i = 0; i < NI; ++i) {
-        const int k = tid + i * nt;
+        const int k = sweep_item(tid + i * nt);
         abk[i] = (k < NWD + NDISC) ? AB[k] : make_double2(1.0, -1.0);
+        if (k < NWD) {
+            int r = int(sqrtf(float(k) * 0.25f));  // WD ring: 4 r^2 <= k < 4 (r + 1)^2
+            r += (4 * (r + 1) * (r + 1) <= k) ? 1 : 0;
+            r -= (4 * r * r > k) ? 1 : 0;
+            wr[i] = wd_ring_weight(r, ul);
+        } else {
+            wr[i] = (k < NWD + NDISC) ? Wt[WT_DISC + (k - NWD) / NDISC_AZ] : 0.0;
+        }
     }
     double2 abB = make_double2(1.0, -1.0);
     double wB = 0.0;
     double dq[DON_STRIDE] = {0.0, 0.0, 0.0, 0.0, 0.0};
-    double tb = 0.0, dn = 0.0, vs = 0.0;
     if (tid < NBS) {
         abB = AB[NWD + NDISC + tid];
         wB = Wt[WT_BS + tid];
+    } else if (tid >= nt - NDONOR) {
+        const int t = tid - (nt - NDONOR);
+        for (int i = 0; i < DON_STRIDE; ++i) dq[i] = DONp[(t >> 2) * DON_STRIDE + i];
+    }
+    double wring = 0.0;  // ring weights for the direct path
+    if (tid >= NBS && tid < NBS + NWD_RINGS) wring = wd_ring_weight(tid - NBS, ul);
+    else if (tid >= NBS + NWD_RINGS && tid < NBS + NWD_RINGS + NDISC_R)
+        wring = Wt[WT_DISC + tid - NBS - NWD_RINGS];
+
+    if (st != ST_OK) {
+        for (int p = tid; p < n; p += nt) {
+            if (L.flux) L.flux[size_t(pair) * n + p] = NAN;
+            if (L.comps)
+                for (int m = 0; m < 4; ++m) L.comps[(size_t(m) * L.npairs + pair) * n + p] = NAN;
+        }
+        if (CHI && tid == 0) L.lle[pair] = -INFINITY;
+        return;
+    }
+    double tb = 0.0, dn = 0.0, vs = 0.0;
+    if (tid < NBS) {
         sbw[tid] = wB;
         tb = wB;
     } else if (tid >= nt - NDONOR) {
-        const int t = tid - (nt - NDONOR), mr = t & 3;
-        for (int i = 0; i < DON_STRIDE; ++i) dq[i] = DONp[(t >> 2) * DON_STRIDE + i];
         // donor normalisation at quadrature (theta = pi/2): e = (0, -s, c)
+        const int mr = (tid - (nt - NDONOR)) & 3;
         const double vy = (mr & 1) ? -dq[1] : dq[1], vz = (mr & 2) ? -dq[2] : dq[2];
         dn = fmax(-s * vy + c * vz, 0.0);
         vs = fabs(dq[0]) + fabs(dq[1]) + fabs(dq[2]);
     }
-    if (tid >= NBS && tid < NBS + NWD_RINGS) swr[tid - NBS] = wd_ring_weight(tid - NBS, G[G_ULIMB]);
-    else if (tid >= NBS + NWD_RINGS && tid < NBS + NWD_RINGS + NDISC_R)
-        swr[tid - NBS] = Wt[WT_DISC + tid - NBS - NWD_RINGS];
+    if (tid >= NBS && tid < NBS + NWD_RINGS + NDISC_R) swr[tid - NBS] = wring;
     tb = wave_sum(tb);
     dn = wave_sum(dn);
     vs = wave_sum(vs);
@@ -821,16 +891,10 @@ __global__ __launch_bounds__(LIKE_THREADS) void k_lnlike(LikeArgs L)
     __syncthreads();
     tb = dn = vs = 0.0;
     for (int i = 0; i < nw; ++i) { tb += red[0][i]; dn += red[1][i]; vs += red[2][i]; }
-    const double ul = G[G_ULIMB];
     const double twd = TWO_PI * ((1.0 - ul) * 0.5 + ul / 3.0);  // 2 pi [F(1) - F(0)]
-    const double td = Wt[WT_TD];
     const double iwd = 1.0 / twd, id = 1.0 / td, itb = 1.0 / tb, ivs = 1.0 / vs;
     double wn[NI];
-    for (int i = 0; i < NI; ++i) {
-        const int k = tid + i * nt;
-        wn[i] = (k < NWD) ? swr[kWdRingOf[k]] * iwd
-                          : (k < NWD + NDISC ? swr[NWD_RINGS + (k - NWD) / NDISC_AZ] * id : 0.0);
-    }
+    for (int i = 0; i < NI; ++i) wn[i] = wr[i] * ((sweep_item(tid + i * nt) < NWD) ? iwd : id);
     wB *= itb;
 
     const double wdF = G[G_WDF], dF = G[G_DF], sF = G[G_SF], rsF = G[G_RSF];
@@ -881,21 +945,31 @@ __global__ __launch_bounds__(LIKE_THREADS) void k_lnlike(LikeArgs L)
             LIKE_STAMP(1);
             if (swA) {
                 const PhaseIndex X = phase_index(TA.lo, TA.cell, m);
+                double qx[2 * NI];
+                int J[2 * NI], Jb[2 * NI];
+#pragma unroll
+                for (int i = 0; i < NI; ++i) {
+                    qx[2 * i] = abk[i].x;
+                    qx[2 * i + 1] = abk[i].y;
+                }
+                count_lt_multi<2 * NI>(X, qx, J);
+                count_le_back_multi<2 * NI>(TA.hi, qx, J, Jb);
 #pragma unroll
                 for (int i = 0; i < NI; ++i)
                     if (abk[i].x < abk[i].y)
-                        apply_runs(element_runs(abk[i].x, abk[i].y, X, TA.hi), abk[i].x, abk[i].y, wn[i], X,
-                                   TA.hi, TA.iw, sacc[(tid + i * nt < NWD) ? 0 : 1]);
+                        apply_runs(Runs{Jb[2 * i], J[2 * i], Jb[2 * i + 1], J[2 * i + 1]}, abk[i].x, abk[i].y,
+                                   wn[i], X, TA.hi, TA.iw, sacc[(sweep_item(tid + i * nt) < NWD) ? 0 : 1]);
             }
+            LIKE_STAMP(2);
             if (swB) {
                 const PhaseIndex XW = phase_index(TB.lo, TB.cell, m), XP = phase_index(sph, scp, m);
                 sweep_spot_donor(tid, XW, TB, XP, abB, wB, dq, ivs, sacc + 2);
             }
             __syncthreads();
-            LIKE_STAMP(2);
+            LIKE_STAMP(3);
             long long r[6];
             block_scan<6>(sacc, spart, tid, r);
-            LIKE_STAMP(3);
+            LIKE_STAMP(4);
             if (j == 0) {
                 if (swA) {
                     fw = double(r[0]) * FX_INV;
@@ -952,7 +1026,7 @@ __global__ __launch_bounds__(LIKE_THREADS) void k_lnlike(LikeArgs L)
                 chi += isnan(f) ? INFINITY : r * r;
             }
         }
-        LIKE_STAMP(4);
+        LIKE_STAMP(5);
     }
     if (CHI) {
         chi = wave_sum(chi);
@@ -1141,12 +1215,13 @@ int run_front(const SetupArgs& S, const Ws& ws, hipStream_t st, void* const* ev)
     mark(1);
     if (hipEventRecord(sd->geo, st) != hipSuccess || hipStreamWaitEvent(sd->s, sd->geo, 0) != hipSuccess)
         return LFG_E_LAUNCH;
-    const long nmain = long(npairs) * U_MAIN, nbs = long(npairs) * U_BS;
-    hipLaunchKernelGGL(k_elements, dim3(unsigned((nmain + ELEM_BLOCK - 1) / ELEM_BLOCK)), dim3(ELEM_BLOCK), 0, st,
-                       ws.geo, ws.status, npairs, ws.ab, ws.donor, ws.wts, 0, U_MAIN, nullptr, nullptr);
+    constexpr int main_chunks = (U_MAIN + ELEM_BLOCK - 1) / ELEM_BLOCK, BS_BLOCK = 128;
+    hipLaunchKernelGGL(k_elements, dim3(unsigned(npairs) * main_chunks), dim3(ELEM_BLOCK), 0, st, ws.geo,
+                       ws.status, npairs, ws.ab, ws.donor, ws.wts, 0, U_MAIN, nullptr, nullptr);
     if (launch_ok() != LFG_OK) return LFG_E_LAUNCH;
-    hipLaunchKernelGGL(k_elements, dim3(unsigned((nbs + ELEM_BLOCK - 1) / ELEM_BLOCK)), dim3(ELEM_BLOCK), 0, sd->s,
-                       ws.geo, ws.status, npairs, ws.ab, ws.donor, ws.wts, U_MAIN, U_BS, ws.bstatus, ws.status);
+    static_assert(U_BS <= BS_BLOCK, "one spot chunk per pair");
+    hipLaunchKernelGGL(k_elements, dim3(unsigned(npairs)), dim3(BS_BLOCK), 0, sd->s, ws.geo, ws.status, npairs,
+                       ws.ab, ws.donor, ws.wts, U_MAIN, U_BS, ws.bstatus, ws.status);
     if (launch_ok() != LFG_OK) return LFG_E_LAUNCH;
     if (hipEventRecord(sd->join, sd->s) != hipSuccess || hipStreamWaitEvent(st, sd->join, 0) != hipSuccess)
         return LFG_E_LAUNCH;

@@ -1,7 +1,7 @@
 """Diagnostic: per-phase cycle stamps of k_lnlike (build with -DLFG_PROFILE_LIKE,
 load via LFG_LIB).  Stamps (s_memtime ticks from kernel entry, thread 0 of each
 block, first tile, last sub-bin pass): 0 staged, 1 phases + cells,
-2 sweep, 3 scan, 4 tile end."""
+2 WD/disc sweep (thread 0 only), 3 spot/donor sweep + barrier, 4 scan, 5 tile end."""
 import os, sys, ctypes
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch
@@ -24,7 +24,7 @@ for _ in range(3):
 torch.cuda.synchronize()
 g = ws[:W * 48 * 8].view(torch.float64).view(W, 48).cpu().numpy()
 ok = st.cpu().numpy() == 0
-names = ['staged', 'cells', 'sweep', 'scan', 'end']
+names = ['staged', 'cells', 'sweepWD', 'sweepBD', 'scan', 'end']
 prev = np.zeros(ok.sum())
 for i, nm in enumerate(names):
     v = g[ok, 41 + i]
