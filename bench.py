@@ -4,10 +4,17 @@ emcee loop, on BASELINE.json's metric config (single eclipse, complex bright
 spot, 300-point phase grid; config 2 = 1024 walkers per GPU).
 
 A step is one emcee iteration of the whole ensemble: two half-steps of
-propose -> batched ln_prob (lfg_lnprob: setup, elements, lnlike, combine
-kernels) -> all_gather -> accept.  value = walkers x steps / time, max over
-ranks, inputs resident in HBM.  Per-GPU work is fixed (weak scaling):
---walkers per GPU, total = walkers x N.
+propose -> batched ln_prob (lfg_lnprob: k_setup, k_bspot, k_elements,
+k_lnlike, k_combine) -> all_gather -> accept.  value = walkers x steps /
+time, max over ranks, inputs resident in HBM.  Per-GPU work is fixed (weak
+scaling): --walkers per GPU, total = walkers x N.
+
+Kernel timing: the last warmup step records HIP events around every kernel
+(include/lfg.h LFG_NEV; on the caller stream and on the library's side
+stream) and picks the dominant kernel; every ln_prob call of the timed region
+then records a start/stop event pair around that kernel only, on the stream
+it runs on.  (A timing event is a queue barrier: events around all kernels
+cost ~20 % of the step, so they stay out of the timed region.)
 
   python bench.py [--gpus N --steps K --warmup W]
   torchrun --nproc-per-node N bench.py --gpus N ...
@@ -27,6 +34,26 @@ sys.path.insert(0, ROOT)
 # MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md; FP64 vector = spec)
 HBM_PEAK_GBS = 8000.0
 FP64_PEAK_TFLOPS = 78.6
+PMC_FILE = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
+
+NEV = 9  # LFG_NEV (include/lfg.h)
+# (name as rocprofv3 prints it, start event, end event)
+KERNELS = [("k_setup", 0, 1), ("k_elements<false>", 1, 2), ("k_bspot", 3, 4),
+           ("k_elements<true>", 4, 5), ("k_lnlike<true>", 6, 7), ("k_combine", 7, 8)]
+
+# Algorithmic HBM bytes per (walker, eclipse) pair of each kernel (DESIGN.md
+# section 3): what the kernel must read and write, counted once.
+NEL, NBS, NWD_DISC, U_DON, DON_STRIDE = 1500, 100, 1400, 100, 5
+GEO_SETUP, GEO_BSPOT, GEO_READ = 41, 5, 40   # geometry doubles written / read
+WT_DISC, WT_N = 21, 124                       # weight doubles per pair
+PER_PAIR = {
+    "k_setup": 18 * 8 + GEO_SETUP * 8 + 4,
+    "k_bspot": 3 * 8 + GEO_BSPOT * 8 + 4,
+    "k_elements<false>": GEO_READ * 8 + 4 + NWD_DISC * 16 + U_DON * DON_STRIDE * 8 + WT_DISC * 8,
+    "k_elements<true>": GEO_READ * 8 + 8 + NBS * 16 + NBS * 8,
+    "k_lnlike<true>": GEO_READ * 8 + 4 + NEL * 16 + U_DON * DON_STRIDE * 8 + WT_N * 8 + 8,
+    "k_combine": 0,
+}
 
 
 def parse():
@@ -42,6 +69,27 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--seed", type=int, default=20261015)
     return ap.parse_args()
+
+
+def algo_bytes(kernel, pairs, walkers, ndim, E, npts):
+    b = PER_PAIR[kernel] * pairs
+    if kernel == "k_setup":
+        b += walkers * (ndim * 8 + 8)          # per-walker prior lane
+    if kernel == "k_lnlike<true>":
+        b += E * npts * 4 * 8                   # x, y, ye, w once per launch
+    if kernel == "k_combine":
+        b += walkers * (8 * 2 + E * 8 * 3)      # prior, lnp; per eclipse 2 Roche priors + ln_like
+    return b
+
+
+def pmc_row(kernel):
+    """Counter-derived bytes / FLOPs per launch of `kernel` (profiles/), or None."""
+    try:
+        d = json.load(open(PMC_FILE))
+    except (OSError, ValueError):
+        return None, None
+    row = d.get("kernels", {}).get(kernel)
+    return row, d.get("meta", {})
 
 
 def main():
@@ -78,23 +126,23 @@ def main():
     S = sampler.EnsembleSampler(W, tree.ndim, ev, seed=args.seed)
     S.set_state(init)
 
-    # kernel timing: HIP events around each kernel of every lfg_lnprob call
-    # in the timed region, on the stream the kernels run on
-    events, pending = [], []
+    # HIP events around kernels of lfg_lnprob calls (include/lfg.h LFG_NEV)
+    events = []
+    want = [True] * NEV  # which events to record
 
     def make_evs():
-        evs = (ctypes.c_void_p * 5)()
-        for i in range(5):
-            h = ctypes.c_void_p()
-            _native.check(L.lfg_event_create(ctypes.byref(h)), "lfg_event_create")
-            evs[i] = h.value
+        evs = (ctypes.c_void_p * NEV)()
+        for i in range(NEV):
+            if want[i]:
+                h = ctypes.c_void_p()
+                _native.check(L.lfg_event_create(ctypes.byref(h)), "lfg_event_create")
+                evs[i] = h.value
         return evs
 
     def timed_eval(x, out=None):
         if out is None:
             out = torch.empty(x.shape[0], dtype=torch.float64, device=dev)
-        ev._ensure(x.shape[0])
-        evs = pending.pop() if pending else make_evs()
+        evs = make_evs()
         events.append((evs, x.shape[0]))
         rc = L.lfg_lnprob_timed(ctypes.c_void_p(x.data_ptr()), x.shape[0], ctypes.byref(ev.ctree),
                                 ctypes.c_void_p(out.data_ptr()), None, ctypes.c_void_p(ev._ws.data_ptr()),
@@ -102,10 +150,39 @@ def main():
         _native.check(rc, "lfg_lnprob_timed")
         return out
 
-    for _ in range(args.warmup):
+    def kernel_ms(kernels):
+        """mean ms per launch of each (name, a, b) over the recorded calls; frees the events"""
+        tot = np.zeros(len(kernels))
+        fms = ctypes.c_float()
+        for evs, _ in events:
+            for k, (_, a, b) in enumerate(kernels):
+                _native.check(L.lfg_event_elapsed_ms(evs[a], evs[b], ctypes.byref(fms)), "elapsed")
+                tot[k] += fms.value
+        n = len(events)
+        for evs, _ in events:
+            for i in range(NEV):
+                if evs[i]:
+                    L.lfg_event_destroy(evs[i])
+        return tot / max(n, 1), n
+
+    ev._ensure(W)
+    for i in range(args.warmup):
+        if i == args.warmup - 1:
+            S.timer = timed_eval  # calibration: every kernel
         S.step()
     torch.cuda.synchronize()
+    S.timer = None
+    dom = 1  # k_elements<false> unless calibrated
+    calib = {}
+    if events:
+        cal_ms, _ = kernel_ms(KERNELS)
+        calib = {n: float(m) for (n, _, _), m in zip(KERNELS, cal_ms)}
+        dom = int(np.argmax(cal_ms))
+    events.clear()
+    kname, ea, eb = KERNELS[dom]
+    want[:] = [i in (ea, eb) for i in range(NEV)]
     S.timer = timed_eval
+
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -123,35 +200,30 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # per-kernel device time over the timed region
-    names = ["k_setup", "k_elements", "k_lnlike", "k_combine"]
-    tot = np.zeros(4)
-    fms = ctypes.c_float()
-    for evs, n in events:
-        for k in range(4):
-            _native.check(L.lfg_event_elapsed_ms(evs[k], evs[k + 1], ctypes.byref(fms)), "elapsed")
-            tot[k] += fms.value
-    ncalls = len(events)
-    avg_ms = tot / max(ncalls, 1)
-    for evs, _ in events:
-        for i in range(5):
-            L.lfg_event_destroy(evs[i])
-    dom = int(np.argmax(tot))
+    # the dominant kernel's device time over the timed region
     shard = events[0][1] if events else W // 2
+    dom_ms, ncalls = kernel_ms([KERNELS[dom]])
+    avg_dom = float(dom_ms[0])
     E = tree.E
-    # algorithmic HBM bytes per launch
-    NEL, NDON, NGEO = 1500, 400, 48
     npts = int(np.max(np.diff(tree.offsets)))
-    bytes_per_pair = {
-        "k_setup": 18 * 8 + (NGEO * 8 + 4),
-        "k_elements": NGEO * 8 + 4 + NEL * 3 * 8 + NDON * 3 * 8,
-        "k_lnlike": NGEO * 8 + 4 + NEL * 3 * 8 + NDON * 3 * 8 + npts * 4 * 8 + 8,
-        "k_combine": 8 * 3,
-    }
-    algo_bytes = bytes_per_pair[names[dom]] * shard * E
-    achieved = algo_bytes / (avg_ms[dom] * 1e-3) / 1e9
+    algo = algo_bytes(kname, shard * E, shard, tree.ndim, E, npts)
+    achieved = algo / (avg_dom * 1e-3) / 1e9
     value = W * args.steps / elapsed
     acc = float(np.mean(S.acceptance_fraction))
+
+    # counter-derived traffic and executed FP64 FLOPs of the same kernel
+    # (rocprofv3 --pmc passes, tools/pmc_profile.sh -> profiles/r01/pmc_traffic.json)
+    row, meta = pmc_row(kname)
+    traffic = fp64 = None
+    if row and meta:
+        scale = shard * E / float(meta.get("pairs_per_launch", shard * E))
+        if "traffic_bytes" in row:
+            traffic = row["traffic_bytes"] * scale
+        if "fp64_flops" in row:
+            f = row["fp64_flops"] * scale
+            tf = f / (avg_dom * 1e-3) / 1e12
+            fp64 = {"executed_flops": f, "achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": tf / FP64_PEAK_TFLOPS, "source": os.path.relpath(PMC_FILE, ROOT)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -177,13 +249,16 @@ def main():
                                    % (args.npts, args.nsub, args.walkers),
                        "walkers_total": W, "eclipses": E, "ndim": tree.ndim,
                        "parallelism": "walker shards x%d, replicated Philox RNG, "
-                                      "all_gather of ln_prob per half-step" % world},
-            "roofline": {"bound": "hbm", "kernel": names[dom], "achieved": achieved,
+                                      "all_gather of ln_prob per half-step" % world,
+                       },
+            "roofline": {"bound": "hbm", "kernel": kname, "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": None, "algo_bytes_per_launch": algo_bytes,
-                         "avg_launch_ms": float(avg_ms[dom]),
-                         "note": "path is FP64-VALU bound (DESIGN.md 4); HBM fraction reported per contract"},
-            "kernel_ms_per_launch": {n: float(m) for n, m in zip(names, avg_ms)},
+                         "traffic": traffic, "algo_bytes_per_launch": algo,
+                         "avg_launch_ms": float(avg_dom),
+                         "fp64_valu": fp64,
+                         "note": "FP64-VALU bound root finding (DESIGN.md 3); HBM fraction reported per contract; "
+                                 "traffic = FETCH_SIZE x2 + WRITE_SIZE per launch from the committed PMC pass"},
+            "kernel_ms_per_launch_warmup": calib,
             "launches_timed": ncalls,
             "acceptance_fraction": acc,
             "cpu_baseline": cpu,
@@ -198,7 +273,6 @@ def cpu_baseline(tree, walkers, args):
     walkers, bounded to about args.cpu_seconds of work."""
     import subprocess
     import tempfile
-    sys.path.insert(0, ROOT)
     from oracle import oracle as orc
     path = os.path.join(tempfile.gettempdir(), "liblfg_oracle_native_%d.so" % os.getpid())
     try:

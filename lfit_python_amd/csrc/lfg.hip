@@ -293,12 +293,16 @@ __device__ inline double bs_weight(int j, const double* G)
     return exp(G[G_EXP1] * log(uk) - pow(uk, G[G_EXP2]) - G[G_LNPK]);
 }
 
+// SPOT = false: WD, disc and donor items [0, U_MAIN); SPOT = true: the spot
+// items [U_MAIN, NUNIQ) (distinct kernel names in rocprofv3 summaries)
+template <bool SPOT>
 __global__ __launch_bounds__(ELEM_BLOCK) void k_elements(const double* __restrict__ geo,
                                                          const int* status, int npairs,
                                                          double2* __restrict__ AB, double* __restrict__ DON,
-                                                         double* __restrict__ WT, int u0, int nu,
+                                                         double* __restrict__ WT,
                                                          const int* __restrict__ bstatus, int* mstatus)
 {
+    constexpr int u0 = SPOT ? U_MAIN : 0, nu = SPOT ? U_BS : U_MAIN;
     // blocks cover unique items [u0, u0 + nu) of every pair in chunks of
     // blockDim.x; block b takes pair b % npairs, so that (with npairs a
     // multiple of 8 and blocks dealt round-robin over the XCDs) a pair's
@@ -310,7 +314,7 @@ __global__ __launch_bounds__(ELEM_BLOCK) void k_elements(const double* __restric
     if (ui >= nu) return;
     const int u = u0 + ui;
     if (status[pair] != ST_OK) return;
-    if (bstatus) {
+    if (SPOT) {
         const int bst = bstatus[pair];
         if (bst != ST_OK) {
             if (u == u0) mstatus[pair] = bst;
@@ -1193,39 +1197,47 @@ SideStream* side_stream()
     return &d;
 }
 
-// k_setup + k_bspot + k_elements with the fork/join above; ev (nullable):
-// events 1 and 2 are recorded on the caller stream after k_setup and after the join
+// k_setup + k_bspot + both k_elements with the fork/join above.  ev
+// (nullable, LFG_NEV events): 0/1/2 on the caller stream before k_setup,
+// after k_setup, after k_elements<false>; 3/4/5 on the side stream before
+// k_bspot, after k_bspot, after k_elements<true>; 6 on the caller stream
+// after the join
 int run_front(const SetupArgs& S, const Ws& ws, hipStream_t st, void* const* ev)
 {
     SideStream* sd = side_stream();
     if (!sd) return LFG_E_LAUNCH;
     std::lock_guard<std::mutex> g(sd->mu);
-    auto mark = [&](int i) {
-        if (ev && ev[i]) (void)hipEventRecord(static_cast<hipEvent_t>(ev[i]), st);
+    auto mark = [&](int i, hipStream_t s) {
+        if (ev && ev[i]) (void)hipEventRecord(static_cast<hipEvent_t>(ev[i]), s);
     };
     const int npairs = S.W * S.E;
     const int nlanes = npairs + S.W;
+    mark(0, st);
     if (hipEventRecord(sd->fork, st) != hipSuccess || hipStreamWaitEvent(sd->s, sd->fork, 0) != hipSuccess)
         return LFG_E_LAUNCH;
+    mark(3, sd->s);
     hipLaunchKernelGGL(k_bspot, dim3((npairs + SETUP_BLOCK - 1) / SETUP_BLOCK), dim3(SETUP_BLOCK), 0, sd->s, S,
                        ws.bstatus);
     if (launch_ok() != LFG_OK) return LFG_E_LAUNCH;
+    mark(4, sd->s);
     hipLaunchKernelGGL(k_setup, dim3((nlanes + SETUP_BLOCK - 1) / SETUP_BLOCK), dim3(SETUP_BLOCK), 0, st, S);
     if (launch_ok() != LFG_OK) return LFG_E_LAUNCH;
-    mark(1);
+    mark(1, st);
     if (hipEventRecord(sd->geo, st) != hipSuccess || hipStreamWaitEvent(sd->s, sd->geo, 0) != hipSuccess)
         return LFG_E_LAUNCH;
     constexpr int main_chunks = (U_MAIN + ELEM_BLOCK - 1) / ELEM_BLOCK, BS_BLOCK = 128;
-    hipLaunchKernelGGL(k_elements, dim3(unsigned(npairs) * main_chunks), dim3(ELEM_BLOCK), 0, st, ws.geo,
-                       ws.status, npairs, ws.ab, ws.donor, ws.wts, 0, U_MAIN, nullptr, nullptr);
+    hipLaunchKernelGGL(k_elements<false>, dim3(unsigned(npairs) * main_chunks), dim3(ELEM_BLOCK), 0, st, ws.geo,
+                       ws.status, npairs, ws.ab, ws.donor, ws.wts, nullptr, nullptr);
     if (launch_ok() != LFG_OK) return LFG_E_LAUNCH;
+    mark(2, st);
     static_assert(U_BS <= BS_BLOCK, "one spot chunk per pair");
-    hipLaunchKernelGGL(k_elements, dim3(unsigned(npairs)), dim3(BS_BLOCK), 0, sd->s, ws.geo, ws.status, npairs,
-                       ws.ab, ws.donor, ws.wts, U_MAIN, U_BS, ws.bstatus, ws.status);
+    hipLaunchKernelGGL(k_elements<true>, dim3(unsigned(npairs)), dim3(BS_BLOCK), 0, sd->s, ws.geo, ws.status,
+                       npairs, ws.ab, ws.donor, ws.wts, ws.bstatus, ws.status);
     if (launch_ok() != LFG_OK) return LFG_E_LAUNCH;
+    mark(5, sd->s);
     if (hipEventRecord(sd->join, sd->s) != hipSuccess || hipStreamWaitEvent(st, sd->join, 0) != hipSuccess)
         return LFG_E_LAUNCH;
-    mark(2);
+    mark(6, st);
     return LFG_OK;
 }
 
@@ -1274,7 +1286,6 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
     SetupArgs S{walkers, W, T->ndim, T->E, 18, T->gather, T->npars, T->consts, T->prior_type, T->prior_p1,
                 T->prior_p2, T->prior_norm, T->roche_priors, ws.geo, ws.status, ws.prior};
     const int npairs = W * T->E;
-    mark(0);
     int rc = run_front(S, ws, st, ev);
     if (rc) return rc;
     double* lle = lnlike_e ? lnlike_e : ws.lle;
@@ -1282,10 +1293,10 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
                T->w, T->nsub, nullptr, nullptr, lle, npairs};
     hipLaunchKernelGGL(k_lnlike<true>, dim3(npairs), dim3(LIKE_THREADS), 0, st, L);
     if ((rc = launch_ok())) return rc;
-    mark(3);
+    mark(7);
     hipLaunchKernelGGL(k_combine, dim3((W + 255) / 256), dim3(256), 0, st, W, T->E, ws.prior, ws.geo, lle, lnp);
     rc = launch_ok();
-    mark(4);
+    mark(8);
     return rc;
 }
 

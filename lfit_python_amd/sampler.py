@@ -151,32 +151,52 @@ class EnsembleSampler:
         return out
 
     def _graphable(self):
-        return (self.use_graph and self.world == 1 and self.timer is None
-                and isinstance(self.ops, HipStretchOps) and self.dev.type == "cuda")
+        return (self.use_graph and self.timer is None and self._graph_ok())
 
-    def _graph_body(self):
+    def _graph_ok(self):
+        return self.world == 1 and isinstance(self.ops, HipStretchOps) and self.dev.type == "cuda"
+
+    def _graph_body(self, ev):
         for half in (0, 1):
             self.ops.propose_dev(self.pos, half, self.a, self.seed, self._step_dev, self.q, self.zfac)
-            self.ev(self.q, out=self.lnp_new)
+            ev(self.q, out=self.lnp_new)
             self.ops.accept_dev(self.pos, self.lnp, half, self.q, self.zfac, self.lnp_new, self.seed,
                                 self._step_dev, self.naccept)
         self._step_dev.add_(1)
 
-    def _graph_step(self):
+    def _sync_step_dev(self):
         import torch
-        if self._graph is None:
+        if self._step_dev is None:
             self._step_dev = torch.full((1,), self.iteration, dtype=torch.int64, device=self.dev)
             self._dev_iter = self.iteration
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self._graph_body()
-            self._graph = g
-        if self._dev_iter != self.iteration:  # iteration changed from outside (reset)
+        elif self._dev_iter != self.iteration:  # iteration changed from outside (reset)
             self._step_dev.fill_(self.iteration)
             self._dev_iter = self.iteration
-        self._graph.replay()
+
+    def capture_iteration(self, evaluator=None):
+        """A HIP graph of one whole emcee iteration (single rank, HIP ops) that
+        reads the step counter from device memory; `evaluator` (default: the
+        sampler's) is the ln_prob call captured inside.  Replay with replay()."""
+        import torch
+        if not self._graph_ok():
+            raise RuntimeError("graph capture needs a single rank and the HIP stretch kernels")
+        self._sync_step_dev()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._graph_body(evaluator or self.ev)
+        return g
+
+    def replay(self, g):
+        """One emcee iteration by replaying a graph from capture_iteration()."""
+        self._sync_step_dev()
+        g.replay()
         self.iteration += 1
         self._dev_iter += 1
+
+    def _graph_step(self):
+        if self._graph is None:
+            self._graph = self.capture_iteration()
+        self.replay(self._graph)
 
     def step(self):
         """One emcee iteration: both halves, in place."""
