@@ -256,6 +256,9 @@ __global__ __launch_bounds__(SETUP_BLOCK) void k_bspot(SetupArgs A, int* __restr
 // Unique items per (walker, eclipse): WD 200, disc 500, spot 100, donor 100.
 // Output: eclipse intervals as (a, b) pairs and the 100 unique donor tile
 // vectors; weights depend on ring only and are formed in k_lnlike.
+#ifdef LFG_COUNT_ITERS
+__device__ unsigned long long g_iter_dbg[64];
+#endif
 constexpr int U_WD = NWD / 2, U_DISC = NDISC / 2, U_BS = NBS, U_DON = NDONOR / 4;
 constexpr int NUNIQ = U_WD + U_DISC + U_BS + U_DON;
 // unique-item order: WD, disc, donor (need k_setup only), then the spot (needs k_bspot)
@@ -313,6 +316,13 @@ __global__ __launch_bounds__(ELEM_BLOCK) void k_elements(const double* __restric
     const int ui = int(blockIdx.x / unsigned(npairs)) * int(blockDim.x) + int(threadIdx.x);
     if (ui >= nu) return;
     const int u = u0 + ui;
+#if defined(LFG_EXP_NODONOR)  // experiment builds: time one region alone
+    if (!SPOT && u >= U_WD + U_DISC) return;
+#elif defined(LFG_EXP_ONLYDONOR)
+    if (!SPOT && u < U_WD + U_DISC) return;
+#elif defined(LFG_EXP_ONLYWD)
+    if (!SPOT && u >= U_WD) return;
+#endif
     if (status[pair] != ST_OK) return;
     if (SPOT) {
         const int bst = bstatus[pair];
@@ -335,15 +345,13 @@ __global__ __launch_bounds__(ELEM_BLOCK) void k_elements(const double* __restric
         double gx, gy, gz;
         for (int itr = 0; itr < ROOT_MAXIT; ++itr) {
             const double X0 = fma(r, dx, 1.0), X1 = r * dy, X2 = r * dz;
-            const double f = rpot(R, X0, X1, X2) - R.pl1;
-            rgrad(R, X0, X1, X2, gx, gy, gz);
+            const double f = rpot_grad(R, X0, X1, X2, gx, gy, gz) - R.pl1;
             const double df = gx * dx + gy * dy + gz * dz;
             if (f > 0.0) hi = r; else lo = r;
+            if (df > 0.0 && fabs(f / df) <= ROOT_LAST) { r -= f / df; break; }  // last Newton step
             double rn = (df > 0.0) ? r - f / df : 0.5 * (lo + hi);
             if (!(rn > lo && rn < hi)) rn = 0.5 * (lo + hi);
-            const double d = rn - r;
             r = rn;
-            if (fabs(d) <= 1e-15) break;
         }
         rgrad(R, fma(r, dx, 1.0), r * dy, r * dz, gx, gy, gz);
         const double ig = rsqrt(gx * gx + gy * gy + gz * gz);
@@ -404,10 +412,26 @@ __global__ __launch_bounds__(ELEM_BLOCK) void k_elements(const double* __restric
         Pz = 0.0;
     }
     double a, b;
-#ifdef LFG_MARK_FALLBACK
-    bool fb = false;  // diagnostic build: NaN-tagged b marks a slow-path element
-    element_interval_fast(R, Px, Py, Pz, s, c, G[G_RCAL], G[G_REFF], a, b, &fb);
-    if (fb) a = -a - 10.0;
+#ifdef LFG_COUNT_ITERS
+    // diagnostic build: per region (WD, disc, spot) sums of iterations
+    // [cone, ingress, egress], their per-wave maxima, fallbacks, items, eclipsed
+    bool fb = false;
+    int nit[3] = {0, 0, 0};
+    element_interval_fast(R, Px, Py, Pz, s, c, G[G_RCAL], G[G_REFF], a, b, &fb, nit);
+    {
+        const int reg = (u < U_WD) ? 0 : (u < U_WD + U_DISC ? 1 : 2);
+        unsigned long long* C = g_iter_dbg + reg * 16;
+        for (int i = 0; i < 3; ++i) {
+            atomicAdd(C + i, (unsigned long long)nit[i]);
+            int m = nit[i];
+            for (int off = 32; off > 0; off >>= 1) m = max(m, __shfl_xor(m, off, 64));
+            if ((threadIdx.x & 63) == 0) atomicAdd(C + 3 + i, (unsigned long long)m);
+        }
+        if ((threadIdx.x & 63) == 0) atomicAdd(C + 9, 1ull);
+        atomicAdd(C + 6, fb ? 1ull : 0ull);
+        atomicAdd(C + 7, 1ull);
+        atomicAdd(C + 8, (a < b) ? 1ull : 0ull);
+    }
 #else
     element_interval_fast(R, Px, Py, Pz, s, c, G[G_RCAL], G[G_REFF], a, b);
 #endif
@@ -1216,8 +1240,13 @@ int run_front(const SetupArgs& S, const Ws& ws, hipStream_t st, void* const* ev)
     if (hipEventRecord(sd->fork, st) != hipSuccess || hipStreamWaitEvent(sd->s, sd->fork, 0) != hipSuccess)
         return LFG_E_LAUNCH;
     mark(3, sd->s);
+#ifdef LFG_EXP_SERIAL  // experiment builds: the stream kernel alone, before everything else
+    hipLaunchKernelGGL(k_bspot, dim3((npairs + SETUP_BLOCK - 1) / SETUP_BLOCK), dim3(SETUP_BLOCK), 0, st, S,
+                       ws.bstatus);
+#else
     hipLaunchKernelGGL(k_bspot, dim3((npairs + SETUP_BLOCK - 1) / SETUP_BLOCK), dim3(SETUP_BLOCK), 0, sd->s, S,
                        ws.bstatus);
+#endif
     if (launch_ok() != LFG_OK) return LFG_E_LAUNCH;
     mark(4, sd->s);
     hipLaunchKernelGGL(k_setup, dim3((nlanes + SETUP_BLOCK - 1) / SETUP_BLOCK), dim3(SETUP_BLOCK), 0, st, S);
@@ -1421,5 +1450,16 @@ int lfg_roche(int op, const double* a, const double* b, int n, double* out, int*
 }
 
 const char* lfg_version(void) { return "lfg 0.1.0 gfx950 fp64"; }
+
+#ifdef LFG_COUNT_ITERS
+// diagnostic builds only: read and clear the iteration counters of k_elements
+int lfg_diag_iters(unsigned long long* out)
+{
+    if (hipDeviceSynchronize() != hipSuccess || hipMemcpyFromSymbol(out, HIP_SYMBOL(g_iter_dbg), sizeof(g_iter_dbg)) != hipSuccess)
+        return LFG_E_LAUNCH;
+    unsigned long long z[64] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_iter_dbg), z, sizeof(z)) == hipSuccess ? LFG_OK : LFG_E_LAUNCH;
+}
+#endif
 
 }  // extern "C"

@@ -20,6 +20,11 @@ constexpr double RAY_TOL = 1e-13;
 constexpr int RAY_MAXIT = 100;
 constexpr double TH_TOL = 1e-13;
 constexpr int ROOT_MAXIT = 100;
+// 1-D safeguarded Newton (L1, donor radius, stream crossing) stops after a
+// Newton step of at most ROOT_LAST: convergence is quadratic, so the error
+// left is ~ROOT_LAST^2.  (A tolerance near machine precision stalls on
+// rounding noise and falls back to bisection for tens of iterations.)
+constexpr double ROOT_LAST = 1e-9;
 constexpr int MIN_MAXIT = 100;
 constexpr double BS_TAIL = 16.0;
 constexpr double STREAM_DELTA = 1e-2;
@@ -69,6 +74,21 @@ __device__ __forceinline__ double rpot(const Roche& R, double x, double y, doubl
            - xc * xc - y * y;
 }
 
+// Phi and grad Phi at one point, sharing the two rsqrt
+__device__ __forceinline__ double rpot_grad(const Roche& R, double x, double y, double z, double& gx, double& gy,
+                                            double& gz)
+{
+    const double ir1 = rsqrt(x * x + y * y + z * z);
+    const double dx = x - 1.0;
+    const double ir2 = rsqrt(dx * dx + y * y + z * z);
+    const double i1 = R.cA * ir1 * ir1 * ir1, i2 = R.cB * ir2 * ir2 * ir2;
+    const double xc = x - R.mu;
+    gx = i1 * x + i2 * dx - 2.0 * xc;
+    gy = (i1 + i2 - 2.0) * y;
+    gz = (i1 + i2) * z;
+    return -R.cA * ir1 - R.cB * ir2 - xc * xc - y * y;
+}
+
 __device__ __forceinline__ void rgrad(const Roche& R, double x, double y, double z,
                                       double& gx, double& gy, double& gz)
 {
@@ -94,11 +114,11 @@ __device__ inline double xl1_solve(double q)
         const double f = cA * ix * ix - cB * io * io - 2.0 * (x - mu);
         const double df = -2.0 * cA * ix * ix * ix - 2.0 * cB * io * io * io - 2.0;
         if (f > 0.0) lo = x; else hi = x;
-        double xn = x - f / df;
+        const double step = f / df;
+        if (fabs(step) <= ROOT_LAST) { x -= step; break; }  // converged: last Newton step
+        double xn = x - step;
         if (!(xn > lo && xn < hi)) xn = 0.5 * (lo + hi);
-        const double d = xn - x;
         x = xn;
-        if (fabs(d) <= 1e-15) break;
     }
     return x;
 }
@@ -316,39 +336,77 @@ __device__ __forceinline__ void rotate(double& cs, double& sn, double d)
     cs = c2;
 }
 
-// 2-D Newton for one contact phase; returns false unless cleanly converged
-// to a tangency of the right kind (ingress: g falling with theta).  th is the
-// running angle; (cs, sn) its cosine and sine, advanced by rotation.
+// 2-D Newton for one contact phase.  Tan holds the running angle th, its
+// cosine and sine (advanced by rotation), the distance t along the line of
+// sight and the state: 0 running, 1 converged to a tangency of the right kind
+// (ingress: g falling with theta), -1 failed.  Newton converges
+// quadratically, so once |dth| and |dt| are <= TH_LAST the step just taken
+// leaves an error ~TH_LAST^2 << TH_TOL and the solve stops there (MODEL_SPEC 7).
+constexpr double TH_LAST = 3e-8;
+
+struct Tan {
+    double th, cs, sn, t;
+    int st;
+};
+
+// one branch-free step (two solves can run interleaved in one lane)
+__device__ __forceinline__ void tangency_step(const Roche& R, double Px, double Py, double Pz, double s, double c,
+                                              bool ingress, Tan& T)
+{
+    ConePt o;
+    cone_point(R, Px, Py, Pz, s, c, T.cs, T.sn, T.t, o);
+    const double F1 = o.phi - R.pl1;
+    const double J11 = T.t * o.gth, J12 = o.F2;
+    const double J21 = T.t * o.etHe + o.gth, J22 = o.eHe;
+    const double det = J11 * J22 - J12 * J21;
+    const bool bad = !(det != 0.0);
+    const double idet = 1.0 / det;
+    double dth = -(F1 * J22 - o.F2 * J12) * idet;
+    const double dt = -(J11 * o.F2 - J21 * F1) * idet;
+    dth = fmin(fmax(dth, -0.05), 0.05);
+    T.th += dth;
+    T.t += dt;
+    const bool conv = fmax(fabs(dth), fabs(dt)) <= TH_LAST;  // both Newton variables (t errs enter F1 squared)
+    const bool good = J22 > 0.0 && ((J11 < 0.0) == ingress) && T.t > 0.0 && o.dX2 < R.Rs2;
+    rotate(T.cs, T.sn, dth);
+    T.st = bad ? -1 : (conv ? (good ? 1 : -1) : 0);
+}
+
+// one contact phase on its own; false unless cleanly converged
 __device__ inline bool tangency(const Roche& R, double Px, double Py, double Pz, double s, double c,
-                                bool ingress, double& th, double cs, double sn, double& t)
+                                bool ingress, double& th, double cs, double sn, double& t, int* nit = nullptr)
+{
+    Tan T{th, cs, sn, t, 0};
+    for (int it = 0; it < 16 && T.st == 0; ++it) {
+        if (nit) ++*nit;  // diagnostic builds only
+        tangency_step(R, Px, Py, Pz, s, c, ingress, T);
+    }
+    th = T.th;
+    t = T.t;
+    return T.st == 1;
+}
+
+// ingress and egress in lockstep: two independent dependency chains per lane
+__device__ inline void tangency_pair(const Roche& R, double Px, double Py, double Pz, double s, double c, Tan& A,
+                                     Tan& B, int* nit = nullptr)
 {
     for (int it = 0; it < 16; ++it) {
-        ConePt o;
-        cone_point(R, Px, Py, Pz, s, c, cs, sn, t, o);
-        const double F1 = o.phi - R.pl1;
-        const double J11 = t * o.gth, J12 = o.F2;
-        const double J21 = t * o.etHe + o.gth, J22 = o.eHe;
-        const double det = J11 * J22 - J12 * J21;
-        if (!(det != 0.0)) return false;
-        const double idet = 1.0 / det;
-        double dth = -(F1 * J22 - o.F2 * J12) * idet;
-        const double dt = -(J11 * o.F2 - J21 * F1) * idet;
-        dth = fmin(fmax(dth, -0.05), 0.05);
-        th += dth;
-        t += dt;
-        if (fabs(dth) <= TH_TOL) {
-            return J22 > 0.0 && ((J11 < 0.0) == ingress) && t > 0.0 && o.dX2 < R.Rs2;
-        }
-        rotate(cs, sn, dth);
+        Tan A2 = A, B2 = B;
+        tangency_step(R, Px, Py, Pz, s, c, true, A2);
+        tangency_step(R, Px, Py, Pz, s, c, false, B2);
+        if (nit) { nit[0] += (A.st == 0); nit[1] += (B.st == 0); }  // diagnostic builds only
+        if (A.st == 0) A = A2;
+        if (B.st == 0) B = B2;
+        if (A.st != 0 && B.st != 0) break;
     }
-    return false;
 }
 
 // 0: not eclipsed, 1: eclipsed, -1: undecided (use the nested solver)
 __device__ inline int cone_exists(const Roche& R, double Px, double Py, double Pz, double s, double c,
-                                  double cs, double sn, double t)
+                                  double cs, double sn, double t, int* nit = nullptr)
 {
     for (int it = 0; it < 16; ++it) {
+        if (nit) ++*nit;
         ConePt o;
         cone_point(R, Px, Py, Pz, s, c, cs, sn, t, o);
         if (o.phi < R.pl1) return (o.dX2 < R.Rs2) ? 1 : -1;
@@ -375,8 +433,9 @@ __device__ inline int cone_exists(const Roche& R, double Px, double Py, double P
 // WD-centre contact (initial guesses only).  Trig: one atan2 and one acos.
 __device__ inline bool element_interval_fast(const Roche& R, double Px, double Py, double Pz, double s,
                                              double c, double Rcal, double Reff, double& a, double& b,
-                                             bool* fallback = nullptr)
+                                             bool* fallback = nullptr, int* nit = nullptr)
 {
+    // nit (diagnostic builds): iterations of the cone search, ingress and egress
     const double ux = 1.0 - Px, uy = -Py, uz = -Pz;
     const double uxy2 = ux * ux + uy * uy;
     const double uu = uxy2 + uz * uz;
@@ -387,7 +446,7 @@ __device__ inline bool element_interval_fast(const Roche& R, double Px, double P
         // theta_c = atan2(-uy, ux): closest approach of the line of sight to D
         const double cc = ux * iuxy, sc = -uy * iuxy;
         const double tc = s * uxy + uz * c;
-        const int ex = cone_exists(R, Px, Py, Pz, s, c, cc, sc, tc);
+        const int ex = cone_exists(R, Px, Py, Pz, s, c, cc, sc, tc, nit);
         if (ex == 0) { a = 1.0; b = -1.0; return false; }
         if (ex == 1) {
             const double ce = (sqrt(fmax(uu - Rcal * Rcal, 0.0)) - c * uz) * iuxy / s;
@@ -397,15 +456,13 @@ __device__ inline bool element_interval_fast(const Roche& R, double Px, double P
                 // cos/sin of thc -+ de; t at closest approach to D along each ray
                 double ci = cc * ce + sc * se, si = sc * ce - cc * se;
                 double co = cc * ce - sc * se, so = sc * ce + cc * se;
-                double thi = thc - de, tho = thc + de;
-                double tti = s * (ux * ci - uy * si) + uz * c;
-                double tto = s * (ux * co - uy * so) + uz * c;
-                const bool oki = tangency(R, Px, Py, Pz, s, c, true, thi, ci, si, tti);
-                const bool oko = tangency(R, Px, Py, Pz, s, c, false, tho, co, so, tto);
+                Tan In{thc - de, ci, si, s * (ux * ci - uy * si) + uz * c, 0};
+                Tan Out{thc + de, co, so, s * (ux * co - uy * so) + uz * c, 0};
+                tangency_pair(R, Px, Py, Pz, s, c, In, Out, nit ? nit + 1 : nullptr);
                 const double Dm = (cosD <= -1.0) ? PI : acos(cosD);
-                if (oki && oko && thi < tho && thi > thc - Dm && tho < thc + Dm) {
-                    a = thi * (1.0 / TWO_PI);
-                    b = tho * (1.0 / TWO_PI);
+                if (In.st == 1 && Out.st == 1 && In.th < Out.th && In.th > thc - Dm && Out.th < thc + Dm) {
+                    a = In.th * (1.0 / TWO_PI);
+                    b = Out.th * (1.0 / TWO_PI);
                     return true;
                 }
             }
@@ -540,7 +597,7 @@ __device__ inline int findi_fast(const Roche& R, double dphi, double& inc_deg)
                 dc = fmin(fmax(dc, -0.05), 0.05);
                 c += dc;
                 t += dt;
-                if (fabs(dc) <= TH_TOL) {
+                if (fmax(fabs(dc), fabs(dt)) <= TH_LAST) {
                     if (J22 > 0.0 && J11 > 0.0 && c >= 0.0 && c < cmax && t > 0.0 && r2s < R.Rs2) {
                         inc_deg = acos(c) / DEG;
                         return ST_OK;
@@ -641,11 +698,10 @@ __device__ inline int bspot(const Roche& R, double rad, double out[4])
                 const double f = p[0] * p[0] + p[1] * p[1] - r2;
                 const double df = 2.0 * dt * (p[0] * p[2] + p[1] * p[3]);
                 if (f > 0.0) lo = tau; else hi = tau;
+                if (df != 0.0 && fabs(f / df) <= ROOT_LAST) { tau -= f / df; break; }  // last Newton step
                 double tn = (df != 0.0) ? tau - f / df : 0.5 * (lo + hi);
                 if (!(tn > lo && tn < hi)) tn = 0.5 * (lo + hi);
-                const double dd = tn - tau;
                 tau = tn;
-                if (fabs(dd) <= 1e-15) break;
             }
             hermite(s, sn, dt, tau, out);
             return ST_OK;
@@ -669,7 +725,7 @@ __device__ inline double bs_umax(double a, double b, double lnpk)
         const double G = v - k * log(v) - C;
         const double dv = G / (1.0 - k / v);
         v -= dv;
-        if (fabs(dv) <= 1e-15 * v) break;
+        if (fabs(dv) <= ROOT_LAST * v) break;  // quadratic: the error left is ~1e-18 v
     }
     return exp(log(v) / b);
 }

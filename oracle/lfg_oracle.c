@@ -32,6 +32,7 @@
 #define RAY_MAXIT      100
 #define TH_TOL         1e-13
 #define ROOT_MAXIT     100
+#define ROOT_LAST      1e-9   /* 1-D Newton: stop after a Newton step <= this */
 #define MIN_MAXIT      100
 #define BS_TAIL        16.0
 #define STREAM_DELTA   1e-2
@@ -78,11 +79,11 @@ static double xl1_solve(double q)
         double f = cA / (x * x) - cB / (omx * omx) - 2.0 * (x - mu);
         double df = -2.0 * cA / (x * x * x) - 2.0 * cB / (omx * omx * omx) - 2.0;
         if (f > 0.0) lo = x; else hi = x;
-        double xn = x - f / df;
+        double step = f / df;
+        if (fabs(step) <= ROOT_LAST) { x -= step; break; } /* converged: last Newton step */
+        double xn = x - step;
         if (!(xn > lo && xn < hi)) xn = 0.5 * (lo + hi);
-        double d = xn - x;
         x = xn;
-        if (fabs(d) <= 1e-15) break;
     }
     return x;
 }
@@ -397,11 +398,10 @@ static int bspot_R(const Roche* R, double rad, double out[4])
                 double f = p[0] * p[0] + p[1] * p[1] - r2;
                 double df = 2.0 * dt * (p[0] * p[2] + p[1] * p[3]);
                 if (f > 0.0) lo = tau; else hi = tau;
+                if (df != 0.0 && fabs(f / df) <= ROOT_LAST) { tau -= f / df; break; }  /* last Newton step */
                 double tn = (df != 0.0) ? tau - f / df : 0.5 * (lo + hi);
                 if (!(tn > lo && tn < hi)) tn = 0.5 * (lo + hi);
-                double dd = tn - tau;
                 tau = tn;
-                if (fabs(dd) <= 1e-15) break;
             }
             hermite(s, sn, dt, tau, out);
             return LFO_OK;
@@ -500,7 +500,7 @@ static double bs_profile_root(double a, double b, double lnpk)
         double G = v - k * log(v) - C;
         double dv = G / (1.0 - k / v);
         v -= dv;
-        if (fabs(dv) <= 1e-15 * v) break;
+        if (fabs(dv) <= ROOT_LAST * v) break;  /* quadratic: the error left is ~1e-18 v */
     }
     return exp(log(v) / b);
 }
@@ -612,11 +612,10 @@ static void build_elements(Model* M)
                 grad_pot(R, X0, X1, X2, g);
                 double df = g[0] * d[0] + g[1] * d[1] + g[2] * d[2];
                 if (f > 0.0) hi = r; else lo = r;
+                if (df > 0.0 && fabs(f / df) <= ROOT_LAST) { r -= f / df; break; } /* last Newton step */
                 double rn = (df > 0.0) ? r - f / df : 0.5 * (lo + hi);
                 if (!(rn > lo && rn < hi)) rn = 0.5 * (lo + hi);
-                double dd = rn - r;
                 r = rn;
-                if (fabs(dd) <= 1e-15) break;
             }
             grad_pot(R, 1.0 + r * d[0], r * d[1], r * d[2], g);
             double gn = sqrt(g[0] * g[0] + g[1] * g[1] + g[2] * g[2]);

@@ -1,0 +1,23 @@
+#!/bin/bash
+# rocprofv3 kernel stats of tools/kernel_time.py for the main library and
+# each experiment build given on the command line (lfit_python_amd/_lib/liblfg_hip_<name>.so)
+R=$GRAFT_REPO_ROOT
+cd /tmp && export TMPDIR=/tmp
+rm -f $R/gpurun_out/kernel_time_walkers.npy
+for v in main "$@"; do
+  if [ "$v" = main ]; then lib=$R/lfit_python_amd/_lib/liblfg_hip.so; else lib=$R/lfit_python_amd/_lib/liblfg_hip_$v.so; fi
+  LFG_LIB=$lib timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/exp_$v -o run --output-format csv \
+    -- python3 $R/tools/kernel_time.py 30 > $R/gpurun_out/exp_$v.log 2>&1 || { echo "$v failed"; exit 3; }
+  echo "== $v"
+  python3 - $R/gpurun_out/exp_$v/run_kernel_trace.csv <<'PY'
+import csv, collections, sys
+d = collections.defaultdict(list)
+for r in csv.DictReader(open(sys.argv[1])):
+    n = r['Kernel_Name'].replace('(anonymous namespace)::', '').replace('void ', '').split('(')[0]
+    if r['Grid_Size_X'] and n.startswith('k_'):
+        d[(n, r['Grid_Size_X'])].append(int(r['End_Timestamp']) - int(r['Start_Timestamp']))
+for k, v in sorted(d.items()):
+    if len(v) >= 10:
+        v = sorted(v); print('  %-22s grid %8s n %3d median %7.1f us' % (k[0], k[1], len(v), v[len(v)//2] / 1e3))
+PY
+done
