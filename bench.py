@@ -10,10 +10,9 @@ time, max over ranks, inputs resident in HBM.  Per-GPU work is fixed (weak
 scaling): --walkers per GPU, total = walkers x N.
 
 Kernel timing: the last warmup step records HIP events around every kernel
-(include/lfg.h LFG_NEV; on the caller stream and on the library's side
-stream) and picks the dominant kernel; every ln_prob call of the timed region
-then records a start/stop event pair around that kernel only, on the stream
-it runs on.  (A timing event is a queue barrier: events around all kernels
+(include/lfg.h LFG_NEV, on the caller stream all kernels run on) and picks
+the dominant kernel; every ln_prob call of the timed region then records a
+start/stop event pair around that kernel only.  (A timing event is a queue barrier: events around all kernels
 cost ~20 % of the step, so they stay out of the timed region.)
 
   python bench.py [--gpus N --steps K --warmup W]
@@ -36,21 +35,18 @@ HBM_PEAK_GBS = 8000.0
 FP64_PEAK_TFLOPS = 78.6
 PMC_FILE = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
 
-NEV = 9  # LFG_NEV (include/lfg.h)
+NEV = 5  # LFG_NEV (include/lfg.h)
 # (name as rocprofv3 prints it, start event, end event)
-KERNELS = [("k_setup", 0, 1), ("k_elements<false>", 1, 2), ("k_bspot", 3, 4),
-           ("k_elements<true>", 4, 5), ("k_lnlike<true>", 6, 7), ("k_combine", 7, 8)]
+KERNELS = [("k_setup", 0, 1), ("k_elements", 1, 2), ("k_lnlike<true>", 2, 3), ("k_combine", 3, 4)]
 
 # Algorithmic HBM bytes per (walker, eclipse) pair of each kernel (DESIGN.md
 # section 3): what the kernel must read and write, counted once.
-NEL, NBS, NWD_DISC, U_DON, DON_STRIDE = 1500, 100, 1400, 100, 5
+NEL, U_DON, DON_STRIDE = 1500, 100, 5
 GEO_SETUP, GEO_BSPOT, GEO_READ = 41, 5, 40   # geometry doubles written / read
-WT_DISC, WT_N = 21, 124                       # weight doubles per pair
+WT_N = 124                                     # weight doubles per pair
 PER_PAIR = {
-    "k_setup": 18 * 8 + GEO_SETUP * 8 + 4,
-    "k_bspot": 3 * 8 + GEO_BSPOT * 8 + 4,
-    "k_elements<false>": GEO_READ * 8 + 4 + NWD_DISC * 16 + U_DON * DON_STRIDE * 8 + WT_DISC * 8,
-    "k_elements<true>": GEO_READ * 8 + 8 + NBS * 16 + NBS * 8,
+    "k_setup": 18 * 8 + GEO_SETUP * 8 + 4 + 3 * 8 + GEO_BSPOT * 8 + 4,   # setup + stream lanes
+    "k_elements": GEO_READ * 8 + 8 + NEL * 16 + U_DON * DON_STRIDE * 8 + WT_N * 8,
     "k_lnlike<true>": GEO_READ * 8 + 4 + NEL * 16 + U_DON * DON_STRIDE * 8 + WT_N * 8 + 8,
     "k_combine": 0,
 }
@@ -172,7 +168,7 @@ def main():
         S.step()
     torch.cuda.synchronize()
     S.timer = None
-    dom = 1  # k_elements<false> unless calibrated
+    dom = 2  # k_lnlike unless calibrated
     calib = {}
     if events:
         cal_ms, _ = kernel_ms(KERNELS)

@@ -127,15 +127,12 @@ int lfg_roche(int op, const double* a, const double* b, int n, double* out,
               int* status, void* stream);
 
 /*
- * Same as lfg_lnprob, recording LFG_NEV caller-created hipEvent_t events
- * around each kernel (bench timing).  On `stream`: ev[0] before k_setup,
- * ev[1] after k_setup, ev[2] after k_elements<false> (WD, disc, donor),
- * ev[6] after the side-stream join, ev[7] after k_lnlike, ev[8] after
- * k_combine.  On the library's side stream: ev[3] before k_bspot, ev[4] after
- * k_bspot, ev[5] after k_elements<true> (bright spot).  NULL entries are
- * skipped.
+ * Same as lfg_lnprob, recording LFG_NEV caller-created hipEvent_t events on
+ * `stream` around each kernel (bench timing): ev[0] before k_setup, ev[1]
+ * after k_setup, ev[2] after k_elements, ev[3] after k_lnlike, ev[4] after
+ * k_combine.  NULL entries are skipped.
  */
-#define LFG_NEV 9
+#define LFG_NEV 5
 int lfg_lnprob_timed(const double* walkers, int W, const lfg_tree* tree,
                      double* lnp, double* lnlike_e, void* ws, size_t ws_bytes,
                      void* stream, void* const* ev);

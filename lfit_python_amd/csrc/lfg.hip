@@ -1,9 +1,11 @@
 // lfg.hip -- MI355X (gfx950) kernels and the C ABI of liblfg_hip.so.
 //
-// Pipeline for one batch of walkers (one emcee half-step):
+// Pipeline for one batch of walkers (one emcee half-step), on the caller's
+// stream only:
 //   k_setup     one lane per (walker, eclipse): parameter gather, L1, findi,
-//               bright-spot stream, strip/beam frame, eclipse Roche priors;
-//               extra lanes per walker: LCModel dphi prior + Prior.ln_prob sum
+//               strip/beam frame, eclipse Roche priors; one lane per walker:
+//               LCModel dphi prior + Prior.ln_prob sum; one lane per
+//               (walker, eclipse): the ballistic stream to the disc edge
 //   k_elements  one lane per (walker, eclipse, element): eclipse interval of
 //               every WD / disc / bright-spot element, donor surface tiles
 //   k_lnlike    one workgroup per (walker, eclipse): element tables staged in
@@ -15,8 +17,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <mutex>
-
 #include "lfg.h"
 #include "lfg_device.hpp"
 #include "lfg_tables.hpp"
@@ -26,7 +26,6 @@ using namespace lfg;
 namespace {
 
 constexpr int SETUP_BLOCK = 64;
-constexpr int LFG_MAX_DEVICES = 64;
 constexpr int ELEM_BLOCK = 256;
 // per-pair weight block written by k_elements: disc ring weights, the disc
 // total 2 pi [P(rdisc) - P(rin)], spot element weights
@@ -41,7 +40,7 @@ __device__ const int kIdentityGather[18] = {0, 1, 2, 3, 4, 5, 6, 7, 8,
 struct Ws {
     double* geo;
     int* status;
-    int* bstatus;   // [pairs] stream status (k_bspot), folded into status by the spot elements
+    int* bstatus;   // [pairs] stream status (k_setup stream lanes), folded into status by k_elements
     double2* ab;    // [pairs][NEL] eclipse intervals (a, b)
     double* donor;  // [pairs][NDONOR/4][DON_STRIDE] symmetry-unique donor tiles
     double* wts;    // [pairs][WT_N] ring / spot weights
@@ -86,6 +85,7 @@ struct SetupArgs {
     double* geo;
     int* status;
     double* prior;
+    int* bstatus;  // stream lanes' status
 };
 
 __device__ inline double gather_par(const SetupArgs& A, int w, int g)
@@ -93,13 +93,56 @@ __device__ inline double gather_par(const SetupArgs& A, int w, int g)
     return g >= 0 ? A.walkers[size_t(w) * A.ndim + g] : A.consts[-1 - g];
 }
 
+// ------------------------------------------------------- stream lanes of k_setup
+// One lane per (walker, eclipse): the ballistic stream to the disc edge and
+// the spot-dependent Roche prior (CVModel.py:215-316).  Needs only q, rdisc
+// and az, so these lanes run beside the setup lanes of the same launch; the
+// stream status goes to bstatus and is folded into the pair status by
+// k_elements.
+__device__ inline void bspot_lane(const SetupArgs& A, int t)
+{
+    const int* gat = A.gather ? A.gather : kIdentityGather;
+    const int w = t / A.E, e = t - w * A.E;
+    const double q = gather_par(A, w, gat[e * 18 + 4]);
+    const double rdisc = gather_par(A, w, gat[e * 18 + 6]);
+    const double az = gather_par(A, w, gat[e * 18 + 10]);
+    double* G = A.geo + size_t(t) * LFG_NGEO;
+#ifdef LFG_PROFILE_SETUP
+    const unsigned long long tp0 = __builtin_amdgcn_s_memtime();
+#endif
+    Roche R;
+    int st = (isfinite(q) && isfinite(rdisc) && isfinite(az)) ? roche_init(R, q) : ST_BAD_ARGS;
+    double bs[4] = {0.0, 0.0, 0.0, 0.0};
+    if (st == ST_OK) st = bspot(R, rdisc * R.xl1, bs);
+    double rprior = 0.0;
+    if (st != ST_OK) {
+        rprior = -INFINITY;
+    } else {
+        double alpha = atan2(bs[1], bs[0]) / DEG;
+        if (alpha < 0.0) alpha = 90.0 - alpha;
+        const double tangent = alpha + 90.0;
+        const double minaz = fmax(0.0, tangent - AZ_SLOPE), maxaz = fmin(178.0, tangent + AZ_SLOPE);
+        if (az < minaz || az > maxaz) rprior = -INFINITY;
+    }
+    G[G_BSX] = bs[0]; G[G_BSY] = bs[1]; G[G_BSVX] = bs[2]; G[G_BSVY] = bs[3];
+    G[G_RPRIOR_BS] = A.roche_priors ? rprior : 0.0;
+    A.bstatus[t] = st;
+#ifdef LFG_PROFILE_SETUP
+    G[43] = double(__builtin_amdgcn_s_memtime() - tp0);
+#endif
+}
+
 __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
 {
     const int t = blockIdx.x * SETUP_BLOCK + threadIdx.x;
     const int npairs = A.W * A.E;
-    if (t >= npairs + A.W) return;
+    if (t >= 2 * npairs + A.W) return;
     const int* gat = A.gather ? A.gather : kIdentityGather;
 
+    if (t >= npairs + A.W) {  // stream lanes (own waves: npairs + W is a multiple of 64 in the bench)
+        bspot_lane(A, t - npairs - A.W);
+        return;
+    }
     if (t >= npairs) {
         // per-walker lane: LCModel.ln_prior dphi check (CVModel.py:452-473)
         // and Node.ln_prior over the variable parameters (model.py:439-449)
@@ -208,46 +251,6 @@ __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
     G[G_RCAL] = sqrt(1.0 - sce * sce);
 }
 
-// ---------------------------------------------------------------- k_bspot
-// One lane per (walker, eclipse): the ballistic stream to the disc edge and
-// the spot-dependent Roche prior (CVModel.py:215-316).  Needs only q and
-// rdisc, so it runs on a side stream concurrently with k_setup and the WD,
-// disc and donor elements; only the spot elements wait for it.
-__global__ __launch_bounds__(SETUP_BLOCK) void k_bspot(SetupArgs A, int* __restrict__ bstatus)
-{
-    const int t = blockIdx.x * SETUP_BLOCK + threadIdx.x;
-    if (t >= A.W * A.E) return;
-    const int* gat = A.gather ? A.gather : kIdentityGather;
-    const int w = t / A.E, e = t - w * A.E;
-    const double q = gather_par(A, w, gat[e * 18 + 4]);
-    const double rdisc = gather_par(A, w, gat[e * 18 + 6]);
-    const double az = gather_par(A, w, gat[e * 18 + 10]);
-    double* G = A.geo + size_t(t) * LFG_NGEO;
-#ifdef LFG_PROFILE_SETUP
-    const unsigned long long tp0 = __builtin_amdgcn_s_memtime();
-#endif
-    Roche R;
-    int st = (isfinite(q) && isfinite(rdisc) && isfinite(az)) ? roche_init(R, q) : ST_BAD_ARGS;
-    double bs[4] = {0.0, 0.0, 0.0, 0.0};
-    if (st == ST_OK) st = bspot(R, rdisc * R.xl1, bs);
-    double rprior = 0.0;
-    if (st != ST_OK) {
-        rprior = -INFINITY;
-    } else {
-        double alpha = atan2(bs[1], bs[0]) / DEG;
-        if (alpha < 0.0) alpha = 90.0 - alpha;
-        const double tangent = alpha + 90.0;
-        const double minaz = fmax(0.0, tangent - AZ_SLOPE), maxaz = fmin(178.0, tangent + AZ_SLOPE);
-        if (az < minaz || az > maxaz) rprior = -INFINITY;
-    }
-    G[G_BSX] = bs[0]; G[G_BSY] = bs[1]; G[G_BSVX] = bs[2]; G[G_BSVY] = bs[3];
-    G[G_RPRIOR_BS] = A.roche_priors ? rprior : 0.0;
-    bstatus[t] = st;
-#ifdef LFG_PROFILE_SETUP
-    G[43] = double(__builtin_amdgcn_s_memtime() - tp0);
-#endif
-}
-
 // ------------------------------------------------------------- k_elements
 // One lane per symmetry-unique element.  The WD/disc grids are mirror
 // symmetric under y -> -y and the donor grid under y -> -y and z -> -z; the
@@ -261,7 +264,7 @@ __device__ unsigned long long g_iter_dbg[64];
 #endif
 constexpr int U_WD = NWD / 2, U_DISC = NDISC / 2, U_BS = NBS, U_DON = NDONOR / 4;
 constexpr int NUNIQ = U_WD + U_DISC + U_BS + U_DON;
-// unique-item order: WD, disc, donor (need k_setup only), then the spot (needs k_bspot)
+// unique-item order: WD, disc, donor, then the spot
 constexpr int U_MAIN = U_WD + U_DISC + U_DON;
 
 __device__ __forceinline__ int wd_ring_of(int u)  // ring of unique WD tile u (ring ir starts at 2 ir^2)
@@ -296,40 +299,32 @@ __device__ inline double bs_weight(int j, const double* G)
     return exp(G[G_EXP1] * log(uk) - pow(uk, G[G_EXP2]) - G[G_LNPK]);
 }
 
-// SPOT = false: WD, disc and donor items [0, U_MAIN); SPOT = true: the spot
-// items [U_MAIN, NUNIQ) (distinct kernel names in rocprofv3 summaries)
-template <bool SPOT>
-__global__ __launch_bounds__(ELEM_BLOCK) void k_elements(const double* __restrict__ geo,
-                                                         const int* status, int npairs,
+__global__ __launch_bounds__(ELEM_BLOCK) void k_elements(const double* __restrict__ geo, int* status, int npairs,
                                                          double2* __restrict__ AB, double* __restrict__ DON,
-                                                         double* __restrict__ WT,
-                                                         const int* __restrict__ bstatus, int* mstatus)
+                                                         double* __restrict__ WT, const int* __restrict__ bstatus)
 {
-    constexpr int u0 = SPOT ? U_MAIN : 0, nu = SPOT ? U_BS : U_MAIN;
-    // blocks cover unique items [u0, u0 + nu) of every pair in chunks of
-    // blockDim.x; block b takes pair b % npairs, so that (with npairs a
-    // multiple of 8 and blocks dealt round-robin over the XCDs) a pair's
-    // tables are written on the XCD whose L2 k_lnlike block `pair` reads them
-    // from -- speed only.  The spot launch (u0 = U_MAIN) also folds the
-    // stream status into the pair status.
+    // blocks cover the NUNIQ unique items of every pair in chunks of
+    // blockDim.x (the spot items fill the last chunk); block b takes pair
+    // b % npairs, so that (with npairs a multiple of 8 and blocks dealt
+    // round-robin over the XCDs) a pair's tables are written on the XCD whose
+    // L2 k_lnlike block `pair` reads them from -- speed only.  Item 0 folds
+    // the stream lanes' status into the pair status (MODEL_SPEC 6 order:
+    // setup failures first); every item skips a pair that failed either.
     const int pair = int(blockIdx.x % unsigned(npairs));
-    const int ui = int(blockIdx.x / unsigned(npairs)) * int(blockDim.x) + int(threadIdx.x);
-    if (ui >= nu) return;
-    const int u = u0 + ui;
+    const int u = int(blockIdx.x / unsigned(npairs)) * int(blockDim.x) + int(threadIdx.x);
+    if (u >= NUNIQ) return;
 #if defined(LFG_EXP_NODONOR)  // experiment builds: time one region alone
-    if (!SPOT && u >= U_WD + U_DISC) return;
+    if (u >= U_WD + U_DISC && u < U_MAIN) return;
 #elif defined(LFG_EXP_ONLYDONOR)
-    if (!SPOT && u < U_WD + U_DISC) return;
+    if (u < U_WD + U_DISC || u >= U_MAIN) return;
 #elif defined(LFG_EXP_ONLYWD)
-    if (!SPOT && u >= U_WD) return;
+    if (u >= U_WD) return;
 #endif
-    if (status[pair] != ST_OK) return;
-    if (SPOT) {
-        const int bst = bstatus[pair];
-        if (bst != ST_OK) {
-            if (u == u0) mstatus[pair] = bst;
-            return;
-        }
+    const int st0 = status[pair], bst = bstatus[pair];
+    if (st0 != ST_OK) return;
+    if (bst != ST_OK) {
+        if (u == 0) status[pair] = bst;
+        return;
     }
     const double* G = geo + size_t(pair) * LFG_NGEO;
     const Roche R{G[G_Q], G[G_CA], G[G_CB], G[G_MU], G[G_XL1], G[G_PL1], G[G_RS], G[G_RS2]};
@@ -1192,81 +1187,25 @@ __global__ void k_roche(int op, const double* __restrict__ a, const double* __re
 
 inline int launch_ok() { return hipGetLastError() == hipSuccess ? LFG_OK : LFG_E_LAUNCH; }
 
-// Library-owned side stream (one per device) for the bright-spot branch:
-//   caller stream:  k_setup -> [geo] -> k_elements(WD, disc, donor) -> wait(join)
-//   side stream:    wait(fork) -> k_bspot -> wait(geo) -> k_elements(spot) -> [join]
-struct SideStream {
-    hipStream_t s = nullptr;
-    hipEvent_t fork = nullptr, geo = nullptr, join = nullptr;
-    std::mutex mu;  // serialises the record/wait sequence of concurrent host callers
-};
-
-SideStream* side_stream()
-{
-    static std::mutex init_mu;
-    static SideStream tab[LFG_MAX_DEVICES];
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= LFG_MAX_DEVICES) return nullptr;
-    SideStream& d = tab[dev];
-    std::lock_guard<std::mutex> g(init_mu);
-    if (!d.s) {
-        hipStream_t s;
-        if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
-        if (hipEventCreateWithFlags(&d.fork, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&d.geo, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&d.join, hipEventDisableTiming) != hipSuccess)
-            return nullptr;
-        d.s = s;
-    }
-    return &d;
-}
-
-// k_setup + k_bspot + both k_elements with the fork/join above.  ev
-// (nullable, LFG_NEV events): 0/1/2 on the caller stream before k_setup,
-// after k_setup, after k_elements<false>; 3/4/5 on the side stream before
-// k_bspot, after k_bspot, after k_elements<true>; 6 on the caller stream
-// after the join
+// k_setup (setup, prior and stream lanes) then k_elements, on the caller's
+// stream.  ev (nullable, LFG_NEV events): 0 before k_setup, 1 after k_setup,
+// 2 after k_elements
 int run_front(const SetupArgs& S, const Ws& ws, hipStream_t st, void* const* ev)
 {
-    SideStream* sd = side_stream();
-    if (!sd) return LFG_E_LAUNCH;
-    std::lock_guard<std::mutex> g(sd->mu);
-    auto mark = [&](int i, hipStream_t s) {
-        if (ev && ev[i]) (void)hipEventRecord(static_cast<hipEvent_t>(ev[i]), s);
+    auto mark = [&](int i) {
+        if (ev && ev[i]) (void)hipEventRecord(static_cast<hipEvent_t>(ev[i]), st);
     };
     const int npairs = S.W * S.E;
-    const int nlanes = npairs + S.W;
-    mark(0, st);
-    if (hipEventRecord(sd->fork, st) != hipSuccess || hipStreamWaitEvent(sd->s, sd->fork, 0) != hipSuccess)
-        return LFG_E_LAUNCH;
-    mark(3, sd->s);
-#ifdef LFG_EXP_SERIAL  // experiment builds: the stream kernel alone, before everything else
-    hipLaunchKernelGGL(k_bspot, dim3((npairs + SETUP_BLOCK - 1) / SETUP_BLOCK), dim3(SETUP_BLOCK), 0, st, S,
-                       ws.bstatus);
-#else
-    hipLaunchKernelGGL(k_bspot, dim3((npairs + SETUP_BLOCK - 1) / SETUP_BLOCK), dim3(SETUP_BLOCK), 0, sd->s, S,
-                       ws.bstatus);
-#endif
-    if (launch_ok() != LFG_OK) return LFG_E_LAUNCH;
-    mark(4, sd->s);
+    const int nlanes = 2 * npairs + S.W;
+    mark(0);
     hipLaunchKernelGGL(k_setup, dim3((nlanes + SETUP_BLOCK - 1) / SETUP_BLOCK), dim3(SETUP_BLOCK), 0, st, S);
     if (launch_ok() != LFG_OK) return LFG_E_LAUNCH;
-    mark(1, st);
-    if (hipEventRecord(sd->geo, st) != hipSuccess || hipStreamWaitEvent(sd->s, sd->geo, 0) != hipSuccess)
-        return LFG_E_LAUNCH;
-    constexpr int main_chunks = (U_MAIN + ELEM_BLOCK - 1) / ELEM_BLOCK, BS_BLOCK = 128;
-    hipLaunchKernelGGL(k_elements<false>, dim3(unsigned(npairs) * main_chunks), dim3(ELEM_BLOCK), 0, st, ws.geo,
-                       ws.status, npairs, ws.ab, ws.donor, ws.wts, nullptr, nullptr);
+    mark(1);
+    constexpr int chunks = (NUNIQ + ELEM_BLOCK - 1) / ELEM_BLOCK;
+    hipLaunchKernelGGL(k_elements, dim3(unsigned(npairs) * chunks), dim3(ELEM_BLOCK), 0, st, ws.geo, ws.status,
+                       npairs, ws.ab, ws.donor, ws.wts, ws.bstatus);
     if (launch_ok() != LFG_OK) return LFG_E_LAUNCH;
-    mark(2, st);
-    static_assert(U_BS <= BS_BLOCK, "one spot chunk per pair");
-    hipLaunchKernelGGL(k_elements<true>, dim3(unsigned(npairs)), dim3(BS_BLOCK), 0, sd->s, ws.geo, ws.status,
-                       npairs, ws.ab, ws.donor, ws.wts, ws.bstatus, ws.status);
-    if (launch_ok() != LFG_OK) return LFG_E_LAUNCH;
-    mark(5, sd->s);
-    if (hipEventRecord(sd->join, sd->s) != hipSuccess || hipStreamWaitEvent(st, sd->join, 0) != hipSuccess)
-        return LFG_E_LAUNCH;
-    mark(6, st);
+    mark(2);
     return LFG_OK;
 }
 
@@ -1288,7 +1227,7 @@ int lfg_flux(const double* pars, int W, int P, const double* x, const double* w,
     if (!wsp || ws_bytes < ws.total) return LFG_E_WORKSPACE;
     hipStream_t st = static_cast<hipStream_t>(stream);
     SetupArgs S{pars, W, P, 1, P, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
-                ws.geo, ws.status, ws.prior};
+                ws.geo, ws.status, ws.prior, ws.bstatus};
     int rc = run_front(S, ws, st, nullptr);
     if (rc) return rc;
     if (N > 0) {
@@ -1313,7 +1252,7 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
         if (ev && ev[i]) (void)hipEventRecord(static_cast<hipEvent_t>(ev[i]), st);
     };
     SetupArgs S{walkers, W, T->ndim, T->E, 18, T->gather, T->npars, T->consts, T->prior_type, T->prior_p1,
-                T->prior_p2, T->prior_norm, T->roche_priors, ws.geo, ws.status, ws.prior};
+                T->prior_p2, T->prior_norm, T->roche_priors, ws.geo, ws.status, ws.prior, ws.bstatus};
     const int npairs = W * T->E;
     int rc = run_front(S, ws, st, ev);
     if (rc) return rc;
@@ -1322,10 +1261,10 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
                T->w, T->nsub, nullptr, nullptr, lle, npairs};
     hipLaunchKernelGGL(k_lnlike<true>, dim3(npairs), dim3(LIKE_THREADS), 0, st, L);
     if ((rc = launch_ok())) return rc;
-    mark(7);
+    mark(3);
     hipLaunchKernelGGL(k_combine, dim3((W + 255) / 256), dim3(256), 0, st, W, T->E, ws.prior, ws.geo, lle, lnp);
     rc = launch_ok();
-    mark(8);
+    mark(4);
     return rc;
 }
 
@@ -1423,7 +1362,7 @@ int lfg_elements(const double* pars, int W, int P, double* a, double* b, double*
     if (!wsp || ws_bytes < ws.total) return LFG_E_WORKSPACE;
     hipStream_t st = static_cast<hipStream_t>(stream);
     SetupArgs S{pars, W, P, 1, P, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
-                ws.geo, ws.status, ws.prior};
+                ws.geo, ws.status, ws.prior, ws.bstatus};
     int rc = run_front(S, ws, st, nullptr);
     if (rc) return rc;
     if (a || b || wgt || donor) {
