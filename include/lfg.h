@@ -73,6 +73,17 @@ typedef struct lfg_tree {
     const double* prior_norm; /* [dev] ndim: Prior.normalise                */
     int roche_priors;         /* 1: LCModel + eclipse Roche priors
                                  (CVModel.py:193-324, 440-491)             */
+    /* Gaussian-process likelihood of GPLCModel trees (CVModel.py:494-711);
+     * gp = 0: chi^2 (gp_* unused).  Each eclipse's points must be sorted by
+     * phase (lfit_python_amd.batch sorts them). */
+    int gp;
+    const int* gp_gather;     /* [dev] E*3: ln_ampin_gp, ln_ampout_gp,
+                                 ln_tau_gp (walker column or -1-const)      */
+    const double* gp_base;    /* [dev] E*4: q, dphi, rwd of the changepoint
+                                 cache and its distance dist_cp
+                                 (CVModel.py:548-576)                       */
+    const int* gp_ecl;        /* [dev] E*2: first and last eclipse number of
+                                 the changepoint list (CVModel.py:582-590)  */
 } lfg_tree;
 
 /* scratch bytes needed for W parameter sets x E eclipses */
@@ -172,6 +183,31 @@ int lfg_stretch_accept_dev(double* pos, double* lnp, int W, int ndim, int half,
                            const double* lnp_new, unsigned long long seed,
                            const unsigned long long* step_dev, int* naccept,
                            void* stream);
+
+/*
+ * Batched trm.roche.wdphases(q, iangle, r1, ntheta) (CVModel.py:564): third
+ * and fourth contact phases of a sphere of radius r1 at the white dwarf.
+ * q, inc (degrees), r1, phi3, phi4, status: [dev] n.
+ */
+int lfg_wdphases(const double* q, const double* inc, const double* r1, int n,
+                 int ntheta, double* phi3, double* phi4, int* status,
+                 void* stream);
+
+/*
+ * Batched george GP log-likelihood of the kernel SimpleGPEclipse.create_GP
+ * builds (CVModel.py:603-648): ampin*Matern32(tau) + ampout*Matern32(tau) on
+ * each of nb closed blocks, plus ye^2 on the diagonal (gp.compute(x, ye),
+ * CVModel.py:687), for W residual vectors (gp.log_likelihood(r),
+ * CVModel.py:691).  Exact, O(N) per set (MODEL_SPEC 10.4).
+ *   x, ye   [dev] N, sorted by x (an unsorted x gives -inf)
+ *   res     [dev] W x N residuals
+ *   hyp     [dev] W x 3: ampin, ampout, tau (george's metric)
+ *   blocks  [dev] W x nb x 2: block [lo, hi] in x
+ *   lnlike  [dev] W (-inf where not positive definite or not finite)
+ */
+int lfg_gp_lnlike(const double* x, const double* ye, const double* res, int W,
+                  int N, const double* hyp, const double* blocks, int nb,
+                  double* lnlike, void* stream);
 
 /* hipEvent helpers for hosts without a HIP binding (ctypes) */
 int lfg_event_create(void** ev);

@@ -49,13 +49,16 @@ class LfgTree(ctypes.Structure):
         ("prior_type", ctypes.c_void_p), ("prior_p1", ctypes.c_void_p),
         ("prior_p2", ctypes.c_void_p), ("prior_norm", ctypes.c_void_p),
         ("roche_priors", ctypes.c_int),
+        ("gp", ctypes.c_int),
+        ("gp_gather", ctypes.c_void_p), ("gp_base", ctypes.c_void_p),
+        ("gp_ecl", ctypes.c_void_p),
     ]
 
 
 EXPORTS = ("lfg_workspace_size", "lfg_flux", "lfg_lnprob", "lfg_lnprob_timed",
            "lfg_elements", "lfg_roche", "lfg_stretch_propose", "lfg_stretch_accept",
-           "lfg_stretch_propose_dev", "lfg_stretch_accept_dev", "lfg_event_create", "lfg_event_destroy", "lfg_event_elapsed_ms",
-           "lfg_version")
+           "lfg_stretch_propose_dev", "lfg_stretch_accept_dev", "lfg_event_create", "lfg_event_destroy",
+           "lfg_event_elapsed_ms", "lfg_wdphases", "lfg_gp_lnlike", "lfg_version")
 
 
 def build(force=False, verbose=False):
@@ -120,6 +123,10 @@ def lib():
         L.lfg_event_destroy.argtypes = [vp]
         L.lfg_event_elapsed_ms.restype = ip
         L.lfg_event_elapsed_ms.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_float)]
+        L.lfg_wdphases.restype = ip
+        L.lfg_wdphases.argtypes = [vp, vp, vp, ip, ip, vp, vp, vp, vp]
+        L.lfg_gp_lnlike.restype = ip
+        L.lfg_gp_lnlike.argtypes = [vp, vp, vp, ip, ip, vp, vp, ip, vp, vp]
         L.lfg_version.restype = ctypes.c_char_p
         L.lfg_version.argtypes = []
         _lib = L

@@ -18,7 +18,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import _native
-from .cvmodel import LCModel, SimpleEclipse, ComplexEclipse, _GPLeaf
+from .cvmodel import LCModel, SimpleEclipse, SimpleGPEclipse
 
 
 @dataclass
@@ -42,6 +42,12 @@ class CompiledTree:
     roche_priors: bool = True
     fixed_invalid: bool = False
     leaf_labels: list = field(default_factory=list)
+    # GP likelihood (GPLCModel trees, CVModel.py:494-711)
+    gp: bool = False
+    gp_gather: np.ndarray = None   # [E, 3] int32: ln_ampin_gp, ln_ampout_gp, ln_tau_gp
+    gp_base: np.ndarray = None     # [E, 4] f64: q, dphi, rwd of the changepoint cache; dist_cp (device-filled)
+    gp_ecl: np.ndarray = None      # [E, 2] int32: first, last eclipse number of the changepoint list
+    order: list = field(default_factory=list)  # per eclipse: data order used (GP trees sort by phase)
 
     @property
     def max_n(self):
@@ -56,24 +62,51 @@ def compile_tree(model, nsub=1):
     leaves = [n for n in model.walk() if isinstance(n, SimpleEclipse)]
     if not leaves:
         raise ValueError("the tree has no eclipse leaves")
-    if any(isinstance(n, _GPLeaf) for n in leaves):
-        raise NotImplementedError("GP likelihood trees are out of scope this round (useGP = 0 only)")
+    gp = [isinstance(n, SimpleGPEclipse) for n in leaves]
+    if any(gp) and not all(gp):
+        raise ValueError("a tree mixes GP and chi^2 eclipses")
+    gp = all(gp)
     consts, gather, npars = [], np.zeros((len(leaves), 18), np.int32), []
+    gp_gather = np.zeros((len(leaves), 3), np.int32)
+    gp_base = np.zeros((len(leaves), 4))
+    gp_ecl = np.zeros((len(leaves), 2), np.int32)
+    orders = []
+
+    def slot(p):
+        if p.isVar:
+            return index[id(p)]
+        consts.append(float(p.currVal))
+        return -len(consts)
+
     xs, ys, yes, ws, offs = [], [], [], [], [0]
     for e, leaf in enumerate(leaves):
         d = leaf.ancestor_param_dict
         names = leaf.cv_parnames
         npars.append(len(names))
         for k, nm in enumerate(names):
-            p = d[nm]
-            if p.isVar:
-                gather[e, k] = index[id(p)]
-            else:
-                consts.append(float(p.currVal))
-                gather[e, k] = -len(consts)
+            gather[e, k] = slot(d[nm])
         for k in range(len(names), 18):
             gather[e, k] = gather[e, 0]
-        xs.append(leaf.lc.x); ys.append(leaf.lc.y); yes.append(leaf.lc.ye); ws.append(leaf.lc.w)
+        order = np.arange(leaf.lc.n_data)
+        if gp:
+            # the Kalman filter runs over phase-sorted points; the likelihood
+            # does not depend on the order
+            order = np.argsort(leaf.lc.x, kind="stable")
+            for k, nm in enumerate(('ln_ampin_gp', 'ln_ampout_gp', 'ln_tau_gp')):
+                gp_gather[e, k] = slot(d[nm])
+            # the changepoint cache: what the leaf holds, else the current values
+            # (the reference fills it at the first ln_like, mcmcfit.py:154)
+            cached = leaf._oldq < 9e99
+            gp_base[e, :3] = ((leaf._oldq, leaf._olddphi, leaf._oldrwd) if cached else
+                              (d['q'].currVal, d['dphi'].currVal, d['rwd'].currVal))
+            gp_base[e, 3] = leaf._dist_cp if cached else np.nan
+            x = leaf.lc.x
+            ecl = [k for k in range(int(np.floor(x.min())), int(np.ceil(x.max())) + 1)
+                   if x.min() < k < 1 + x.max()] if len(x) else []
+            gp_ecl[e] = (ecl[0], ecl[-1]) if ecl else (1, 0)
+        orders.append(order)
+        xs.append(leaf.lc.x[order]); ys.append(leaf.lc.y[order]); yes.append(leaf.lc.ye[order])
+        ws.append(leaf.lc.w[order])
         offs.append(offs[-1] + leaf.lc.n_data)
     fixed_invalid = any((not p.isVar) and (not p.isValid) for p in params)
     cat = lambda a: np.ascontiguousarray(np.concatenate(a).astype(np.float64)) if a else np.zeros(0)
@@ -87,7 +120,8 @@ def compile_tree(model, nsub=1):
         prior_p2=np.asarray([p.prior.p2 for p in var], np.float64),
         prior_norm=np.asarray([p.prior.normalise for p in var], np.float64),
         nsub=int(nsub), roche_priors=isinstance(model, LCModel),
-        fixed_invalid=fixed_invalid, leaf_labels=[l.label for l in leaves])
+        fixed_invalid=fixed_invalid, leaf_labels=[l.label for l in leaves],
+        gp=gp, gp_gather=gp_gather, gp_base=gp_base, gp_ecl=gp_ecl, order=orders)
 
 
 class LnProbEvaluator:
@@ -108,16 +142,35 @@ class LnProbEvaluator:
             ye=t(tree.ye, f64), w=t(tree.w, f64),
             prior_type=t(tree.prior_type, i32), prior_p1=t(tree.prior_p1, f64),
             prior_p2=t(tree.prior_p2, f64), prior_norm=t(tree.prior_norm, f64))
+        if tree.gp:
+            self._buf.update(gp_gather=t(tree.gp_gather.reshape(-1), i32),
+                             gp_base=t(self._gp_base(tree), f64),
+                             gp_ecl=t(tree.gp_ecl.reshape(-1), i32))
         b = self._buf
-        p = lambda k: ctypes.c_void_p(b[k].data_ptr())
+        p = lambda k: ctypes.c_void_p(b[k].data_ptr()) if k in b else None
         self.ctree = _native.LfgTree(
             tree.E, tree.ndim, tree.nsub, tree.max_n, p('gather'), p('npars'), p('consts'),
             p('off'), p('x'), p('y'), p('ye'), p('w'), p('prior_type'), p('prior_p1'),
-            p('prior_p2'), p('prior_norm'), int(tree.roche_priors))
+            p('prior_p2'), p('prior_norm'), int(tree.roche_priors), int(tree.gp),
+            p('gp_gather'), p('gp_base'), p('gp_ecl'))
         self._ws = None
         self._ws_walkers = 0
         if max_walkers:
             self._ensure(max_walkers)
+
+    def _gp_base(self, tree):
+        """[E, 4] q, dphi, rwd, dist_cp of the changepoint cache; a cache the
+        host never filled gets its dist_cp from the device (findi + wdphases,
+        CVModel.py:561-570)."""
+        from . import roche
+        base = np.array(tree.gp_base, dtype=np.float64)
+        todo = ~np.isfinite(base[:, 3])
+        if todo.any():
+            q, dphi, rwd = base[todo, 0], base[todo, 1], base[todo, 2]
+            inc = roche.findi(q, dphi)
+            p3, p4 = roche.wdphases(q, inc, rwd, 10)
+            base[todo, 3] = (dphi + (p4 - p3)) / 2.0
+        return base.reshape(-1)
 
     def _ensure(self, W):
         import torch

@@ -86,6 +86,9 @@ struct SetupArgs {
     int* status;
     double* prior;
     int* bstatus;  // stream lanes' status
+    int gp;        // GP likelihood: per-pair hyper-parameters and changepoints
+    const int* gp_gather;
+    const double* gp_base;
 };
 
 __device__ inline double gather_par(const SetupArgs& A, int w, int g)
@@ -249,6 +252,28 @@ __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
     G[G_WDF] = p[0]; G[G_DF] = p[1]; G[G_SF] = p[2]; G[G_RSF] = p[3];
     const double sce = s * cos(PI * p[5]);
     G[G_RCAL] = sqrt(1.0 - sce * sce);
+    if (A.gp) {
+        // SimpleGPEclipse.create_GP / calcChangepoints (CVModel.py:529-648):
+        // amplitudes exp(ln_amp), metric exp(ln_tau); the changepoint
+        // distance from the cache unless q, dphi or rwd moved > 120 %
+        const int* gg = A.gp_gather + e * 3;
+        const double ain = exp(gather_par(A, w, gg[0])), aout = exp(gather_par(A, w, gg[1]));
+        const double tau = exp(gather_par(A, w, gg[2]));
+        const double* B = A.gp_base + e * 4;
+        const double q = p[4], dphi = p[5], rwd = p[8];
+        double dcp = B[3];
+        bool ok = isfinite(dcp);
+        if (fabs(B[1] - dphi) / dphi > 1.2 || fabs(B[0] - q) / q > 1.2 || fabs(B[2] - rwd) / rwd > 1.2) {
+            double ph3, ph4;
+            ok = wdphases(R, inc, rwd, 10, ph3, ph4) == ST_OK;  // inc = roche.findi(q, dphi)
+            dcp = (dphi + (ph4 - ph3)) / 2.0;
+        }
+        G[G_GP_AIN] = ain;
+        G[G_GP_AOUT] = aout;
+        G[G_GP_LAM] = sqrt(3.0 / tau);
+        G[G_GP_DCP] = dcp;
+        G[G_GP_OK] = (ok && tau > 0.0 && isfinite(ain) && isfinite(aout)) ? 1.0 : 0.0;
+    }
 }
 
 // ------------------------------------------------------------- k_elements
@@ -503,6 +528,7 @@ struct LikeArgs {
     double* comps;  // nullable, [4][pairs][N]
     double* lle;    // nullable, [pairs]
     int npairs;
+    const int* gp_ecl;  // GP mode: [E][2] first and last changepoint eclipse numbers
 };
 
 // ---- sweeps over phase-sorted tiles of points (MODEL_SPEC 6 restated) ----
@@ -812,9 +838,13 @@ __device__ inline void direct_spot_donor(const double2* __restrict__ ABs, const 
 #define LIKE_STAMP(i)
 #endif
 
-template <bool CHI>
+// MODE 0: flux (and components) only; 1: fused chi^2 -> ln_like; 2: GP
+// ln_like of the residuals (a Kalman filter over each tile's sorted points,
+// run by wave 0 while the other waves wait at the tile barrier)
+template <int MODE>
 __global__ __launch_bounds__(LIKE_THREADS) void k_lnlike(LikeArgs L)
 {
+    constexpr bool CHI = MODE != 0, GP = MODE == 2;
 #ifdef LFG_PROFILE_LIKE
     const unsigned long long tstart = __builtin_amdgcn_s_memtime();
 #endif
@@ -925,6 +955,7 @@ __global__ __launch_bounds__(LIKE_THREADS) void k_lnlike(LikeArgs L)
     const double nb0 = G[G_NB0], nb1 = G[G_NB1], nb2 = G[G_NB2];
     const int S = L.nsub;
     double chi = 0.0;
+    GPFilter gpf;  // GP mode, wave 0
     for (int t0 = 0; t0 < n; t0 += LIKE_TILE) {
         const int m = min(LIKE_TILE, n - t0);
         LIKE_STAMP(0);
@@ -1044,14 +1075,35 @@ __global__ __launch_bounds__(LIKE_THREADS) void k_lnlike(LikeArgs L)
                 L.comps[(size_t(2) * L.npairs + pair) * n + pi] = fb;
                 L.comps[(size_t(3) * L.npairs + pair) * n + pi] = fr;
             }
-            if (CHI) {
+            if (CHI && !GP) {
                 const double r = (py - f) / pye;
                 chi += isnan(f) ? INFINITY : r * r;
             }
         }
+        if (GP) {
+            // residuals y - flux of the tile in LDS (the sweep buffers are free
+            // after the last pass); wave 0 carries the filter across tiles
+            if (own) {
+                TB.lo[tid] = px;
+                TB.hi[tid] = pye;
+                TB.iw[tid] = py - (wdF * (1.0 - fw) + dF * (1.0 - fd) + sF * sbs / S + rsF * srs / S);
+                TB.cell[tid] = gp_block(px, L.gp_ecl[2 * e], L.gp_ecl[2 * e + 1], G[G_GP_DCP], phi0);
+            }
+            __syncthreads();
+            if (wv == 0) {
+                if (t0 == 0) gpf.init(G[G_GP_AIN], G[G_GP_AOUT], 3.0 / (G[G_GP_LAM] * G[G_GP_LAM]));
+                for (int p = 0; p < m; ++p) gpf.step(TB.lo[p], TB.hi[p], TB.iw[p], TB.cell[p]);
+            }
+            __syncthreads();
+        }
         LIKE_STAMP(5);
     }
-    if (CHI) {
+    if (GP) {
+        if (tid == 0) {
+            const bool okp = G[G_GP_OK] != 0.0;
+            L.lle[pair] = (okp && n > 0) ? gpf.lnlike() : (okp ? 0.0 : -INFINITY);
+        }
+    } else if (CHI) {
         chi = wave_sum(chi);
         if (lane == 0) red[0][wv] = chi;
         __syncthreads();
@@ -1158,6 +1210,58 @@ __global__ void k_accept(double* __restrict__ pos, double* __restrict__ lnp, int
     }
 }
 
+// ------------------------------------------------------ k_gp, k_wdphases
+__device__ __forceinline__ double readlane_f64(double v, int j)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane(int(b), j), hi = __builtin_amdgcn_readlane(int(b >> 32), j);
+    return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
+}
+
+// one wave per residual vector: lanes load 64 points at a time, every lane
+// runs the (wave-uniform) filter over them through readlane broadcasts
+__global__ __launch_bounds__(64) void k_gp(const double* __restrict__ x, const double* __restrict__ ye,
+                                           const double* __restrict__ res, int N, const double* __restrict__ hyp,
+                                           const double* __restrict__ blocks, int nb, double* __restrict__ lnlike)
+{
+    const int w = blockIdx.x, lane = threadIdx.x;
+    const double* r = res + size_t(w) * N;
+    const double* bk = blocks + size_t(w) * nb * 2;
+    GPFilter F;
+    F.init(hyp[3 * w], hyp[3 * w + 1], hyp[3 * w + 2]);
+    for (int c0 = 0; c0 < N; c0 += 64) {
+        const int p = c0 + lane;
+        double xv = 0.0, yv = 1.0, rv = 0.0;
+        int bv = -1;
+        if (p < N) {
+            xv = x[p];
+            yv = ye[p];
+            rv = r[p];
+            for (int k = 0; k < nb; ++k)
+                if (xv >= bk[2 * k] && xv <= bk[2 * k + 1]) bv = k;
+        }
+        const int m = min(64, N - c0);
+        for (int j = 0; j < m; ++j)
+            F.step(readlane_f64(xv, j), readlane_f64(yv, j), readlane_f64(rv, j), __builtin_amdgcn_readlane(bv, j));
+    }
+    if (lane == 0) lnlike[w] = F.lnlike();
+}
+
+__global__ void k_wdphases(const double* __restrict__ q, const double* __restrict__ inc,
+                           const double* __restrict__ r1, int n, int ntheta, double* __restrict__ ph3,
+                           double* __restrict__ ph4, int* __restrict__ status)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Roche R;
+    double a = NAN, b = NAN;
+    int st = roche_init(R, q[i]);
+    if (st == ST_OK) st = wdphases(R, inc[i], r1[i], ntheta, a, b);
+    ph3[i] = (st == ST_OK) ? a : NAN;
+    ph4[i] = (st == ST_OK) ? b : NAN;
+    status[i] = st;
+}
+
 // ---------------------------------------------------------------- k_roche
 __global__ void k_roche(int op, const double* __restrict__ a, const double* __restrict__ b, int n,
                         double* __restrict__ out, int* __restrict__ status)
@@ -1227,13 +1331,13 @@ int lfg_flux(const double* pars, int W, int P, const double* x, const double* w,
     if (!wsp || ws_bytes < ws.total) return LFG_E_WORKSPACE;
     hipStream_t st = static_cast<hipStream_t>(stream);
     SetupArgs S{pars, W, P, 1, P, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
-                ws.geo, ws.status, ws.prior, ws.bstatus};
+                ws.geo, ws.status, ws.prior, ws.bstatus, 0, nullptr, nullptr};
     int rc = run_front(S, ws, st, nullptr);
     if (rc) return rc;
     if (N > 0) {
         LikeArgs L{ws.geo, ws.status, ws.ab, ws.donor, ws.wts, 1, nullptr, N, x, nullptr, nullptr, w,
-                   nsub, flux, comps, nullptr, W};
-        hipLaunchKernelGGL(k_lnlike<false>, dim3(W), dim3(LIKE_THREADS), 0, st, L);
+                   nsub, flux, comps, nullptr, W, nullptr};
+        hipLaunchKernelGGL(k_lnlike<0>, dim3(W), dim3(LIKE_THREADS), 0, st, L);
         if ((rc = launch_ok())) return rc;
     }
     if (status && hipMemcpyAsync(status, ws.status, sizeof(int) * W, hipMemcpyDeviceToDevice, st) != hipSuccess)
@@ -1252,14 +1356,16 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
         if (ev && ev[i]) (void)hipEventRecord(static_cast<hipEvent_t>(ev[i]), st);
     };
     SetupArgs S{walkers, W, T->ndim, T->E, 18, T->gather, T->npars, T->consts, T->prior_type, T->prior_p1,
-                T->prior_p2, T->prior_norm, T->roche_priors, ws.geo, ws.status, ws.prior, ws.bstatus};
+                T->prior_p2, T->prior_norm, T->roche_priors, ws.geo, ws.status, ws.prior, ws.bstatus, T->gp,
+                T->gp_gather, T->gp_base};
     const int npairs = W * T->E;
     int rc = run_front(S, ws, st, ev);
     if (rc) return rc;
     double* lle = lnlike_e ? lnlike_e : ws.lle;
     LikeArgs L{ws.geo, ws.status, ws.ab, ws.donor, ws.wts, T->E, T->off, T->max_n, T->x, T->y, T->ye,
-               T->w, T->nsub, nullptr, nullptr, lle, npairs};
-    hipLaunchKernelGGL(k_lnlike<true>, dim3(npairs), dim3(LIKE_THREADS), 0, st, L);
+               T->w, T->nsub, nullptr, nullptr, lle, npairs, T->gp ? T->gp_ecl : nullptr};
+    if (T->gp) hipLaunchKernelGGL(k_lnlike<2>, dim3(npairs), dim3(LIKE_THREADS), 0, st, L);
+    else hipLaunchKernelGGL(k_lnlike<1>, dim3(npairs), dim3(LIKE_THREADS), 0, st, L);
     if ((rc = launch_ok())) return rc;
     mark(3);
     hipLaunchKernelGGL(k_combine, dim3((W + 255) / 256), dim3(256), 0, st, W, T->E, ws.prior, ws.geo, lle, lnp);
@@ -1362,7 +1468,7 @@ int lfg_elements(const double* pars, int W, int P, double* a, double* b, double*
     if (!wsp || ws_bytes < ws.total) return LFG_E_WORKSPACE;
     hipStream_t st = static_cast<hipStream_t>(stream);
     SetupArgs S{pars, W, P, 1, P, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
-                ws.geo, ws.status, ws.prior, ws.bstatus};
+                ws.geo, ws.status, ws.prior, ws.bstatus, 0, nullptr, nullptr};
     int rc = run_front(S, ws, st, nullptr);
     if (rc) return rc;
     if (a || b || wgt || donor) {
@@ -1385,6 +1491,26 @@ int lfg_roche(int op, const double* a, const double* b, int n, double* out, int*
     if (n == 0) return LFG_OK;
     hipLaunchKernelGGL(k_roche, dim3((n + 63) / 64), dim3(64), 0, static_cast<hipStream_t>(stream), op, a, b, n,
                        out, status);
+    return launch_ok();
+}
+
+int lfg_wdphases(const double* q, const double* inc, const double* r1, int n, int ntheta, double* phi3,
+                 double* phi4, int* status, void* stream)
+{
+    if (n < 0 || ntheta < 1 || (n > 0 && (!q || !inc || !r1 || !phi3 || !phi4 || !status))) return LFG_E_ARGS;
+    if (n == 0) return LFG_OK;
+    hipLaunchKernelGGL(k_wdphases, dim3((n + 63) / 64), dim3(64), 0, static_cast<hipStream_t>(stream), q, inc, r1,
+                       n, ntheta, phi3, phi4, status);
+    return launch_ok();
+}
+
+int lfg_gp_lnlike(const double* x, const double* ye, const double* res, int W, int N, const double* hyp,
+                  const double* blocks, int nb, double* lnlike, void* stream)
+{
+    if (W <= 0 || N < 0 || nb < 0 || !hyp || !lnlike || (N > 0 && (!x || !ye || !res)) || (nb > 0 && !blocks))
+        return LFG_E_ARGS;
+    hipLaunchKernelGGL(k_gp, dim3(W), dim3(64), 0, static_cast<hipStream_t>(stream), x, ye, res, N, hyp, blocks, nb,
+                       lnlike);
     return launch_ok();
 }
 

@@ -57,7 +57,8 @@ enum Geo {
     G_BSX, G_BSY, G_BSVX, G_BSVY, G_L, G_UPK, G_UMAX, G_LNPK,
     G_EXP1, G_EXP2, G_CAZ, G_SAZ, G_NB0, G_NB1, G_NB2, G_BDEN,
     G_FIS, G_PHI0, G_WDF, G_DF, G_SF, G_RSF, G_RPRIOR, G_RCAL,
-    G_RPRIOR_BS,  // bright-spot part of the eclipse Roche prior (k_bspot)
+    G_RPRIOR_BS,  // bright-spot part of the eclipse Roche prior (stream lanes)
+    G_GP_AIN, G_GP_AOUT, G_GP_LAM, G_GP_DCP, G_GP_OK,  // GP likelihood (MODEL_SPEC 10)
     G_COUNT
 };
 static_assert(G_COUNT <= 48, "LFG_NGEO");
@@ -728,6 +729,144 @@ __device__ inline double bs_umax(double a, double b, double lnpk)
         if (fabs(dv) <= ROOT_LAST * v) break;  // quadratic: the error left is ~1e-18 v
     }
     return exp(log(v) / b);
+}
+
+// MODEL_SPEC 10.2: trm.roche.wdphases(q, iangle, r1, ntheta) (CVModel.py:564):
+// third and fourth contact phases of a sphere of radius r1 at the WD, from
+// ntheta points on the limb circle perpendicular to the line of sight at the
+// WD-centre egress phase; the nested solver (as the oracle) for each point
+__device__ inline int wdphases(const Roche& R, double inc_deg, double r1, int ntheta, double& ph3, double& ph4)
+{
+    if (!(r1 > 0.0) || ntheta < 1) return ST_BAD_GEOMETRY;
+    double dphi;
+    int st = findphi_fast(R, inc_deg, dphi);
+    if (st != ST_OK) return st;
+    double s, c, sth, cth;
+    sincos(inc_deg * DEG, &s, &c);
+    sincos(PI * dphi, &sth, &cth);
+    const double Reff = eggleton(R.q);
+    double lo = INFINITY, hi = -INFINITY;
+    for (int k = 0; k < ntheta; ++k) {
+        double sp, cp;
+        sincos(TWO_PI * k / ntheta, &sp, &cp);
+        double a, b;
+        if (element_interval(R, r1 * (cp * sth - sp * c * cth), r1 * (cp * cth + sp * c * sth), r1 * (sp * s), s, c,
+                             Reff, a, b)) {
+            lo = fmin(lo, b);
+            hi = fmax(hi, b);
+        }
+    }
+    if (!(lo <= hi)) return ST_BAD_DPHI;
+    ph3 = lo;
+    ph4 = hi;
+    return ST_OK;
+}
+
+// MODEL_SPEC 10.4: the GP log-likelihood of CVModel.py:636-691 as a 4-state
+// Kalman filter over phase-sorted points (tests/gp_kalman.py restates it in
+// numpy).  State (g, g', h, h'): the global Matern-3/2 process (variance
+// ampin) and the process of the current changepoint block (ampout), which
+// starts stationary at the block's first point; both share
+//   Phi(d) = e^{-u} [[1 + u, d], [-lam^2 d, 1 - u]],  u = lam d,
+//   lam = sqrt(3 / tau) (george's metric tau), Pinf = a diag(1, lam^2).
+// Covariances are carried as D = P - Pinf, so prediction is D <- Phi D Phi^T.
+struct GPFilter {
+    double lam, ain, aout;
+    double m0, m1, m2, m3;
+    double d00, d01, d11, d22, d23, d33, d02, d03, d12, d13;  // g-g, h-h, g-h blocks of D
+    double xp, ll;
+    int bp, n;
+    bool bad;
+
+    __device__ void init(double ampin, double ampout, double tau)
+    {
+        lam = sqrt(3.0 / tau);
+        ain = ampin;
+        aout = ampout;
+        m0 = m1 = m2 = m3 = 0.0;
+        d00 = d01 = d11 = d22 = d23 = d33 = d02 = d03 = d12 = d13 = 0.0;
+        xp = 0.0;
+        ll = 0.0;
+        bp = -1;
+        n = 0;
+        bad = !(tau > 0.0) || !(ampin >= 0.0) || !(ampout >= 0.0);
+    }
+
+    // one point: phase x (sorted), error ye, residual r, changepoint block blk (-1: none)
+    __device__ void step(double x, double ye, double r, int blk)
+    {
+        if (n > 0) {
+            const double d = x - xp;
+            const double u = lam * d, e = exp(-u);
+            const double f00 = e * (1.0 + u), f01 = e * d, f10 = -e * lam * u, f11 = e * (1.0 - u);
+            double t0 = f00 * m0 + f01 * m1;
+            m1 = f10 * m0 + f11 * m1;
+            m0 = t0;
+            t0 = f00 * m2 + f01 * m3;
+            m3 = f10 * m2 + f11 * m3;
+            m2 = t0;
+            sym(f00, f01, f10, f11, d00, d01, d11);
+            sym(f00, f01, f10, f11, d22, d23, d33);
+            const double t00 = f00 * d02 + f01 * d12, t01 = f00 * d03 + f01 * d13;
+            const double t10 = f10 * d02 + f11 * d12, t11 = f10 * d03 + f11 * d13;
+            d02 = t00 * f00 + t01 * f01;
+            d03 = t00 * f10 + t01 * f11;
+            d12 = t10 * f00 + t11 * f01;
+            d13 = t10 * f10 + t11 * f11;
+            bad = bad || !(d >= 0.0);
+        }
+        xp = x;
+        ++n;
+        if (blk >= 0 && blk != bp) {  // a new block: its process starts stationary, independent
+            m2 = m3 = 0.0;
+            d22 = d23 = d33 = d02 = d03 = d12 = d13 = 0.0;
+        }
+        bp = blk;
+        const double a = (blk >= 0) ? 1.0 : 0.0;
+        const double k0 = (d00 + ain) + a * d02, k1 = d01 + a * d12;
+        const double k2 = d02 + a * (d22 + aout), k3 = d03 + a * d23;
+        const double S = fma(a, k2, k0) + ye * ye;
+        const double v = r - fma(a, m2, m0);
+        const double iS = 1.0 / S;
+        bad = bad || !(S > 0.0) || !isfinite(v);
+        ll += v * v * iS + log(S);
+        const double g = v * iS;
+        m0 = fma(k0, g, m0);
+        m1 = fma(k1, g, m1);
+        m2 = fma(k2, g, m2);
+        m3 = fma(k3, g, m3);
+        d00 -= k0 * k0 * iS; d01 -= k0 * k1 * iS; d11 -= k1 * k1 * iS;
+        d22 -= k2 * k2 * iS; d23 -= k2 * k3 * iS; d33 -= k3 * k3 * iS;
+        d02 -= k0 * k2 * iS; d03 -= k0 * k3 * iS; d12 -= k1 * k2 * iS; d13 -= k1 * k3 * iS;
+    }
+
+    __device__ double lnlike() const
+    {
+        const double v = -0.5 * (ll + n * 1.8378770664093454836);  // log(2 pi)
+        return (bad || !isfinite(v)) ? -INFINITY : v;
+    }
+
+    __device__ static void sym(double f00, double f01, double f10, double f11, double& a, double& b, double& c)
+    {
+        const double t00 = f00 * a + f01 * b, t01 = f00 * b + f01 * c;
+        const double t10 = f10 * a + f11 * b, t11 = f10 * b + f11 * c;
+        a = t00 * f00 + t01 * f01;
+        b = t00 * f10 + t01 * f11;
+        c = t10 * f10 + t11 * f11;
+    }
+};
+
+// CVModel.py:582-599: changepoint block k of eclipse number ec is
+// [(ec - 1) + dcp + phi0, (ec - dcp) + phi0], closed as george tests blocks;
+// returns the block index of x in [e0, e1], or -1
+__device__ __forceinline__ int gp_block(double x, int e0, int e1, double dcp, double phi0)
+{
+    int blk = -1;
+    for (int ec = e0; ec <= e1; ++ec) {
+        const double lo = (double(ec - 1) + dcp) + phi0, hi = (double(ec) - dcp) + phi0;
+        if (x >= lo && x <= hi) blk = ec - e0;
+    }
+    return blk;
 }
 
 // Prior.ln_prob, model.py:83-113 (gauss through log(pdf), as scipy does)

@@ -8,15 +8,15 @@ GPU lfit.CV, so the tree can be driven one walker at a time exactly like the
 reference; lfit_python_amd.batch compiles the same tree for batched GPU
 evaluation of whole ensembles.
 
-The Gaussian-process likelihood (GPLCModel and the *GPEclipse leaves,
-CVModel.py:494-711) is out of scope for this round:
-the GP node classes keep the reference's parameter layout so that input files
-with useGP = 1 build and route correctly, but their ln_like raises.
+The Gaussian-process leaves (SimpleGPEclipse / ComplexGPEclipse,
+CVModel.py:517-711) keep the reference's changepoint cache and kernel
+construction; their likelihood runs on the GPU (lfit_python_amd.gp).
 """
 import os
 
 import numpy as np
 
+from . import gp as georgelike
 from . import lfit, roche
 from .tree import Node, Param, extract_par_and_key
 
@@ -194,18 +194,62 @@ class GPLCModel(LCModel):
     node_par_names = LCModel.node_par_names + ('ln_ampin_gp', 'ln_ampout_gp', 'ln_tau_gp')
 
 
-class _GPLeaf:
+class SimpleGPEclipse(SimpleEclipse):
+    """SimpleEclipse whose likelihood is a GP on its residuals (CVModel.py:517-696)."""
+
+    # changepoint cache (CVModel.py:522-527): filled by the first evaluation
+    _olddphi = 9e99
+    _oldq = 9e99
+    _oldrwd = 9e99
+    _dist_cp = 9e99
+
+    def calcChangepoints(self):
+        """[[egress, ingress], ...] of the inter-eclipse blocks (CVModel.py:529-601)."""
+        d = self.ancestor_param_dict
+        dphi, q, rwd, phi0 = d['dphi'], d['q'], d['rwd'], d['phi0']
+        dphi_change = np.fabs(self._olddphi - dphi.currVal) / dphi.currVal
+        q_change = np.fabs(self._oldq - q.currVal) / q.currVal
+        rwd_change = np.fabs(self._oldrwd - rwd.currVal) / rwd.currVal
+        if (dphi_change > 1.2) or (q_change > 1.2) or (rwd_change > 1.2):
+            inc = roche.findi(q.currVal, dphi.currVal)
+            phi3, phi4 = roche.wdphases(q.currVal, inc, rwd.currVal, ntheta=10)
+            dist_cp = (dphi.currVal + (phi4 - phi3)) / 2.
+            self._dist_cp = dist_cp
+            self._oldq = q.currVal
+            self._olddphi = dphi.currVal
+            self._oldrwd = rwd.currVal
+        else:
+            dist_cp = self._dist_cp
+        min_ecl = int(np.floor(self.lc.x.min()))
+        max_ecl = int(np.ceil(self.lc.x.max()))
+        eclipses = [e for e in range(min_ecl, max_ecl + 1)
+                    if np.logical_and(e > self.lc.x.min(), e < 1 + self.lc.x.max())]
+        return [[(e - 1) + dist_cp + phi0.currVal, e - dist_cp + phi0.currVal] for e in eclipses]
+
+    def create_GP(self):
+        """george-style GP of CVModel.py:603-648 (lfit_python_amd.gp)."""
+        d = self.ancestor_param_dict
+        ampin_gp = np.exp(d['ln_ampin_gp'].currVal)
+        ampout_gp = np.exp(d['ln_ampout_gp'].currVal)
+        tau_gp = np.exp(d['ln_tau_gp'].currVal)
+        changepoints = self.calcChangepoints()
+        kernel = ampin_gp * georgelike.kernels.Matern32Kernel(tau_gp)
+        for gap in changepoints:
+            kernel += ampout_gp * georgelike.kernels.Matern32Kernel(tau_gp, block=gap)
+        return georgelike.GP(kernel, solver=georgelike.HODLRSolver)
+
     def ln_like(self):
-        raise NotImplementedError("the Gaussian-process likelihood (CVModel.py:494-711) "
-                                  "is out of scope for this round; use useGP = 0")
+        residuals = self.lc.y - self.calcFlux()
+        if np.any(np.isinf(residuals)) or np.any(np.isnan(residuals)):
+            return -np.inf
+        gp = self.create_GP()
+        gp.compute(self.lc.x, self.lc.ye)
+        return gp.log_likelihood(residuals, quiet=True)
 
 
-class SimpleGPEclipse(_GPLeaf, SimpleEclipse):
-    pass
-
-
-class ComplexGPEclipse(_GPLeaf, ComplexEclipse):
-    pass
+class ComplexGPEclipse(SimpleGPEclipse):
+    node_par_names = ComplexEclipse.node_par_names
+    cv_parnames = ComplexEclipse.cv_parnames
 
 
 def construct_model(input_file, debug=False, nodata=False, nsub=1):

@@ -4,6 +4,7 @@
     findphi(q, inc)     CVModel.py:460, testCV.py:25
     findi(q, dphi)      CVModel.py:561, calcPhysicalParams.py:194
     bspot(q, rad)       CVModel.py:288  -> (x, y, vx, vy)
+    wdphases(q, inc, r1, ntheta=10)  CVModel.py:564 -> (phi3, phi4)
 
 Geometry follows MODEL_SPEC.md section 4 (separation a = 1, WD at the
 origin, donor centre at (1, 0, 0)).  Scalars in, scalars out, like trm.roche;
@@ -71,3 +72,30 @@ def bspot(q, rad):
             raise RocheError("bspot failed: the stream does not reach r = %g" % float(rad))
         return tuple(float(t) for t in v[0])
     return v
+
+
+def wdphases(q, inc, r1, ntheta=10):
+    """Third and fourth contact phases of a sphere of radius r1 (units of the
+    separation) at the white dwarf (trm.roche.wdphases; MODEL_SPEC 10.2)."""
+    import torch
+    _native.require_gpu()
+    L = _native.lib()
+    q_np = np.atleast_1d(np.asarray(q, dtype=np.float64))
+    shape = np.broadcast(q_np, np.asarray(inc), np.asarray(r1)).shape
+    dev = torch.device("cuda", torch.cuda.current_device())
+    t = lambda a: torch.as_tensor(np.array(np.broadcast_to(np.asarray(a, dtype=np.float64), shape)).reshape(-1),
+                                  device=dev)
+    qt, it, rt = t(q), t(inc), t(r1)
+    n = qt.shape[0]
+    p3 = torch.empty(n, dtype=torch.float64, device=dev)
+    p4 = torch.empty_like(p3)
+    st = torch.empty(n, dtype=torch.int32, device=dev)
+    vp = lambda a: ctypes.c_void_p(a.data_ptr())
+    _native.check(L.lfg_wdphases(vp(qt), vp(it), vp(rt), n, int(ntheta), vp(p3), vp(p4), vp(st),
+                                 _native.stream_ptr(dev)), "lfg_wdphases")
+    p3, p4, st = p3.cpu().numpy(), p4.cpu().numpy(), st.cpu().numpy()
+    if np.ndim(q) == 0 and np.ndim(inc) == 0 and np.ndim(r1) == 0:
+        if st[0] != 0:
+            raise RocheError("wdphases failed: %s" % _native.STATUS_TEXT.get(int(st[0]), st[0]))
+        return float(p3[0]), float(p4[0])
+    return p3, p4

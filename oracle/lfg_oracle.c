@@ -455,6 +455,40 @@ int lfo_point_interval(double q, double inc_deg, const double P[3], double* a,
     return element_interval(&R, P, sin(i), cos(i), eggleton(q), a, b);
 }
 
+/* trm.roche.wdphases(q, iangle, r1, ntheta) (CVModel.py:564; MODEL_SPEC 10.2):
+ * third and fourth contact phases of a sphere of radius r1 (units of a) at
+ * the WD.  ntheta points on the limb circle perpendicular to the line of
+ * sight at the WD-centre egress phase findphi(q, i)/2; phi3 / phi4 = the
+ * earliest / latest egress phase of those points. */
+int lfo_wdphases(double q, double inc_deg, double r1, int ntheta, double* phi3, double* phi4)
+{
+    Roche R;
+    int st = roche_init(&R, q);
+    if (st) return st;
+    if (!(r1 > 0.0) || ntheta < 1) return LFO_BAD_GEOMETRY;
+    double dphi;
+    st = findphi_R(&R, inc_deg, &dphi);
+    if (st) return st;
+    double i = inc_deg * DEG, s = sin(i), c = cos(i);
+    double th = PI * dphi, st_ = sin(th), ct_ = cos(th);
+    double u1[3] = {st_, ct_, 0.0}, u2[3] = {-c * ct_, c * st_, s};
+    double lo = INFINITY, hi = -INFINITY;
+    for (int k = 0; k < ntheta; ++k) {
+        double psi = TWO_PI * k / ntheta, cp = cos(psi), sp = sin(psi);
+        double P[3] = {r1 * (cp * u1[0] + sp * u2[0]), r1 * (cp * u1[1] + sp * u2[1]),
+                       r1 * (cp * u1[2] + sp * u2[2])};
+        double a, b;
+        if (element_interval(&R, P, s, c, eggleton(q), &a, &b)) {
+            if (b < lo) lo = b;
+            if (b > hi) hi = b;
+        }
+    }
+    if (!(lo <= hi)) return LFO_BAD_DPHI;
+    *phi3 = lo;
+    *phi4 = hi;
+    return LFO_OK;
+}
+
 /* ------------------------------------------------------- the CV model (5) */
 typedef struct {
     Roche R;
@@ -777,6 +811,97 @@ static double eclipse_roche_prior(const double* p)
     return 0.0;
 }
 
+/* ----------------------------------------- GP likelihood (MODEL_SPEC 10) */
+/* george Matern32Kernel(metric = tau): (1 + sqrt(3 d^2 / tau)) exp(-sqrt(3 d^2 / tau)) */
+static double matern32(double d, double tau)
+{
+    double u = sqrt(3.0 * d * d / tau);
+    return (1.0 + u) * exp(-u);
+}
+
+/* george.GP(ampin M32(tau) + sum_k ampout M32(tau, block = blk[k])).compute(x, ye)
+ * .log_likelihood(r): the exact dense likelihood (Cholesky), blocks closed
+ * [lo, hi] in x as george tests them.  Not positive definite -> -inf. */
+double lfo_gp_lnlike(const double* x, const double* r, const double* ye, int n, double ampin, double ampout,
+                     double tau, const double* blk, int nb)
+{
+    if (n <= 0) return 0.0;
+    double* K = (double*)malloc(sizeof(double) * (size_t)n * n);
+    int* in = (int*)malloc(sizeof(int) * (size_t)n);
+    for (int i = 0; i < n; ++i) {
+        in[i] = -1;
+        for (int k = 0; k < nb; ++k)
+            if (x[i] >= blk[2 * k] && x[i] <= blk[2 * k + 1]) in[i] = k;
+    }
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j <= i; ++j) {
+            double m = matern32(x[i] - x[j], tau);
+            double v = ampin * m;
+            if (in[i] >= 0 && in[i] == in[j]) v += ampout * m;
+            if (i == j) v += ye[i] * ye[i];
+            K[(size_t)i * n + j] = v;
+        }
+    /* in-place Cholesky, lower triangle */
+    double logdet = 0.0;
+    for (int j = 0; j < n; ++j) {
+        double d = K[(size_t)j * n + j];
+        for (int k = 0; k < j; ++k) d -= K[(size_t)j * n + k] * K[(size_t)j * n + k];
+        if (!(d > 0.0)) { free(K); free(in); return -INFINITY; }
+        d = sqrt(d);
+        K[(size_t)j * n + j] = d;
+        logdet += 2.0 * log(d);
+        for (int i = j + 1; i < n; ++i) {
+            double v = K[(size_t)i * n + j];
+            for (int k = 0; k < j; ++k) v -= K[(size_t)i * n + k] * K[(size_t)j * n + k];
+            K[(size_t)i * n + j] = v / d;
+        }
+    }
+    /* r^T K^-1 r = |L^-1 r|^2 */
+    double* z = (double*)malloc(sizeof(double) * (size_t)n);
+    double q = 0.0;
+    for (int i = 0; i < n; ++i) {
+        double v = r[i];
+        for (int k = 0; k < i; ++k) v -= K[(size_t)i * n + k] * z[k];
+        z[i] = v / K[(size_t)i * n + i];
+        q += z[i] * z[i];
+    }
+    free(z);
+    free(K);
+    free(in);
+    double ll = -0.5 * (q + logdet + n * log(2.0 * PI));
+    return isfinite(ll) ? ll : -INFINITY;
+}
+
+/* SimpleGPEclipse.calcChangepoints (CVModel.py:529-601): the distance from
+ * mid-eclipse to the changepoints, recomputed from (q, dphi, rwd) when any
+ * of them moved by more than 120 % from the cached base values (the cache
+ * holds the tree's start values, MODEL_SPEC 10.3). */
+static int gp_dist_cp(double q, double dphi, double rwd, const double* base, double base_dcp, double* dcp)
+{
+    if (fabs(base[1] - dphi) / dphi > 1.2 || fabs(base[0] - q) / q > 1.2 || fabs(base[2] - rwd) / rwd > 1.2) {
+        double inc, p3, p4;
+        int st = lfo_findi(q, dphi, &inc);
+        if (st) return st;
+        st = lfo_wdphases(q, inc, rwd, 10, &p3, &p4);
+        if (st) return st;
+        *dcp = (dphi + (p4 - p3)) / 2.0;
+    } else {
+        *dcp = base_dcp;
+    }
+    return LFO_OK;
+}
+
+int lfo_gp_base_dcp(double q, double dphi, double rwd, double* dcp)
+{
+    double inc, p3, p4;
+    int st = lfo_findi(q, dphi, &inc);
+    if (st) return st;
+    st = lfo_wdphases(q, inc, rwd, 10, &p3, &p4);
+    if (st) return st;
+    *dcp = (dphi + (p4 - p3)) / 2.0;
+    return LFO_OK;
+}
+
 int lfo_lnprob_batch(const double* walkers, int W, int ndim,
                      int E, const int* gather, const int* npars,
                      const double* consts,
@@ -785,6 +910,23 @@ int lfo_lnprob_batch(const double* walkers, int W, int ndim,
                      const int* prior_type, const double* prior_p1,
                      const double* prior_p2, const double* prior_norm,
                      double* lnp, double* lnlike_e, int nthreads)
+{
+    return lfo_lnprob_batch_gp(walkers, W, ndim, E, gather, npars, consts, off, x, y, ye, w, nsub, prior_type,
+                               prior_p1, prior_p2, prior_norm, NULL, NULL, NULL, lnp, lnlike_e, nthreads);
+}
+
+/* gp_gather [E*3] (ln_ampin_gp, ln_ampout_gp, ln_tau_gp: walker column or
+ * -1-const), gp_base [E*3] (q, dphi, rwd of the changepoint cache), gp_ecl
+ * [E*2] (first, last eclipse number); all NULL: chi^2 likelihood */
+int lfo_lnprob_batch_gp(const double* walkers, int W, int ndim,
+                        int E, const int* gather, const int* npars,
+                        const double* consts,
+                        const int* off, const double* x, const double* y,
+                        const double* ye, const double* w, int nsub,
+                        const int* prior_type, const double* prior_p1,
+                        const double* prior_p2, const double* prior_norm,
+                        const int* gp_gather, const double* gp_base, const int* gp_ecl,
+                        double* lnp, double* lnlike_e, int nthreads)
 {
     int used = 1;
 #ifdef _OPENMP
@@ -831,17 +973,46 @@ int lfo_lnprob_batch(const double* walkers, int W, int ndim,
                 double* f = (double*)malloc(sizeof(double) * (n > 0 ? n : 1));
                 int st = lfo_flux(pars, npars[e], x + off[e], w + off[e], n, nsub,
                                   f, NULL, NULL, NULL, NULL);
-                double chi = 0.0;
-                if (st != LFO_OK) chi = INFINITY;
-                else {
-                    for (int p = 0; p < n; ++p) {
-                        if (isnan(f[p])) { chi = INFINITY; break; }
-                        double r = (y[off[e] + p] - f[p]) / ye[off[e] + p];
-                        chi += r * r;
+                if (gp_gather) {
+                    /* SimpleGPEclipse.ln_like (CVModel.py:650-696) */
+                    le = -INFINITY;
+                    int good = (st == LFO_OK);
+                    for (int p = 0; p < n && good; ++p) {
+                        f[p] = y[off[e] + p] - f[p];  /* residuals */
+                        if (!isfinite(f[p])) good = 0;
                     }
+                    double dcp, base_dcp;
+                    const double* B = gp_base + 3 * e;
+                    if (good && lfo_gp_base_dcp(B[0], B[1], B[2], &base_dcp) == LFO_OK &&
+                        gp_dist_cp(pars[4], pars[5], pars[8], B, base_dcp, &dcp) == LFO_OK) {
+                        double hyp[3];
+                        for (int k = 0; k < 3; ++k) {
+                            int g = gp_gather[3 * e + k];
+                            hyp[k] = exp(g >= 0 ? v[g] : consts[-1 - g]);
+                        }
+                        int nb = gp_ecl[2 * e + 1] - gp_ecl[2 * e] + 1;
+                        double* blk = (double*)malloc(sizeof(double) * 2 * (nb > 0 ? nb : 1));
+                        for (int k = 0; k < nb; ++k) {
+                            int ec = gp_ecl[2 * e] + k;
+                            blk[2 * k] = ((double)(ec - 1) + dcp) + pars[13];
+                            blk[2 * k + 1] = ((double)ec - dcp) + pars[13];
+                        }
+                        le = lfo_gp_lnlike(x + off[e], f, ye + off[e], n, hyp[0], hyp[1], hyp[2], blk, nb);
+                        free(blk);
+                    }
+                } else {
+                    double chi = 0.0;
+                    if (st != LFO_OK) chi = INFINITY;
+                    else {
+                        for (int p = 0; p < n; ++p) {
+                            if (isnan(f[p])) { chi = INFINITY; break; }
+                            double r = (y[off[e] + p] - f[p]) / ye[off[e] + p];
+                            chi += r * r;
+                        }
+                    }
+                    le = -0.5 * chi;
                 }
                 free(f);
-                le = -0.5 * chi;
             }
             if (lnlike_e) lnlike_e[(size_t)iw * E + e] = le;
             ll += le;

@@ -36,6 +36,11 @@ int    lfo_bspot(double q, double rad, double out4[4]);
 int    lfo_point_interval(double q, double inc_deg, const double P[3],
                           double* a, double* b);
 
+/* trm.roche.wdphases(q, iangle, r1, ntheta) (CVModel.py:564): third and
+ * fourth contact phases of a sphere of radius r1 at the WD (MODEL_SPEC 10.2) */
+int    lfo_wdphases(double q, double inc_deg, double r1, int ntheta,
+                    double* phi3, double* phi4);
+
 /* lfit.CV.calcFlux restatement: pars[14|18] (CV order, README.md:24-43). */
 int lfo_flux(const double* pars, int npars, const double* x, const double* w,
              int n, int nsub, double* flux, double* ywd, double* yd,
@@ -73,6 +78,29 @@ int lfo_lnprob_batch(const double* walkers, int W, int ndim,
                      const int* prior_type, const double* prior_p1,
                      const double* prior_p2, const double* prior_norm,
                      double* lnp, double* lnlike_e, int nthreads);
+
+/* GP likelihood (CVModel.py:603-696; MODEL_SPEC 10): exact dense george
+ * log-likelihood of residuals r for ampin*M32(tau) + ampout*M32(tau) on each
+ * closed block [blk[2k], blk[2k+1]] of x, plus ye^2 on the diagonal */
+double lfo_gp_lnlike(const double* x, const double* r, const double* ye, int n,
+                     double ampin, double ampout, double tau,
+                     const double* blk, int nb);
+/* changepoint distance (dphi + phi4 - phi3) / 2 of CVModel.py:560-570 */
+int lfo_gp_base_dcp(double q, double dphi, double rwd, double* dcp);
+/* lfo_lnprob_batch with the GP likelihood of GPLCModel trees:
+ * gp_gather [E*3] ln_ampin_gp, ln_ampout_gp, ln_tau_gp (column or -1-const),
+ * gp_base [E*3] q, dphi, rwd of the changepoint cache, gp_ecl [E*2] first and
+ * last eclipse number of the changepoint list; NULL gp_gather = chi^2 */
+int lfo_lnprob_batch_gp(const double* walkers, int W, int ndim,
+                        int E, const int* gather, const int* npars,
+                        const double* consts,
+                        const int* off, const double* x, const double* y,
+                        const double* ye, const double* w, int nsub,
+                        const int* prior_type, const double* prior_p1,
+                        const double* prior_p2, const double* prior_norm,
+                        const int* gp_gather, const double* gp_base,
+                        const int* gp_ecl, double* lnp, double* lnlike_e,
+                        int nthreads);
 
 #ifdef __cplusplus
 }

@@ -61,6 +61,15 @@ class Oracle:
             _dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _ip, _ip, _dp,
             _ip, _dp, _dp, _dp, _dp, ctypes.c_int, _ip, _dp, _dp, _dp,
             _dp, _dp, ctypes.c_int]
+        lib.lfo_lnprob_batch_gp.argtypes = [
+            _dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _ip, _ip, _dp,
+            _ip, _dp, _dp, _dp, _dp, ctypes.c_int, _ip, _dp, _dp, _dp,
+            _ip, _dp, _ip, _dp, _dp, ctypes.c_int]
+        lib.lfo_wdphases.argtypes = [ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_int, _dp, _dp]
+        lib.lfo_gp_lnlike.restype = ctypes.c_double
+        lib.lfo_gp_lnlike.argtypes = [_dp, _dp, _dp, ctypes.c_int, ctypes.c_double, ctypes.c_double,
+                                      ctypes.c_double, _dp, ctypes.c_int]
+        lib.lfo_gp_base_dcp.argtypes = [ctypes.c_double, ctypes.c_double, ctypes.c_double, _dp]
         self.lib = lib
 
     # roche -----------------------------------------------------------------
@@ -87,6 +96,29 @@ class Oracle:
         if st:
             raise ValueError("bspot failed (status %d)" % st)
         return tuple(out)
+
+    def wdphases(self, q, inc, r1, ntheta=10):
+        p3, p4 = ctypes.c_double(), ctypes.c_double()
+        st = self.lib.lfo_wdphases(float(q), float(inc), float(r1), int(ntheta), ctypes.byref(p3), ctypes.byref(p4))
+        if st:
+            raise ValueError("wdphases failed (status %d)" % st)
+        return p3.value, p4.value
+
+    # GP --------------------------------------------------------------------
+    def gp_lnlike(self, x, r, ye, ampin, ampout, tau, blocks):
+        x, xp = _f(x)
+        r, rp = _f(r)
+        ye, yp = _f(ye)
+        b, bp = _f(np.asarray(blocks, dtype=np.float64).reshape(-1, 2) if len(blocks) else np.zeros((1, 2)))
+        return self.lib.lfo_gp_lnlike(xp, rp, yp, x.shape[0], float(ampin), float(ampout), float(tau), bp,
+                                      len(blocks))
+
+    def gp_base_dcp(self, q, dphi, rwd):
+        out = ctypes.c_double()
+        st = self.lib.lfo_gp_base_dcp(float(q), float(dphi), float(rwd), ctypes.byref(out))
+        if st:
+            raise ValueError("changepoints failed (status %d)" % st)
+        return out.value
 
     # CV --------------------------------------------------------------------
     def flux(self, pars, x, w=None, nsub=1, components=False):
@@ -135,11 +167,15 @@ class Oracle:
 
         lnp = np.empty(W)
         lle = np.empty((W, tree.E))
-        used = self.lib.lfo_lnprob_batch(
+        gp = getattr(tree, "gp", False)
+        used = self.lib.lfo_lnprob_batch_gp(
             wp, W, ndim, tree.E, I(tree.gather.reshape(-1)), I(tree.npars),
             F(tree.consts if len(tree.consts) else np.zeros(1)),
             I(tree.offsets), F(tree.x), F(tree.y), F(tree.ye), F(tree.w),
             int(nsub), I(tree.prior_type), F(tree.prior_p1), F(tree.prior_p2),
-            F(tree.prior_norm), lnp.ctypes.data_as(_dp),
-            lle.ctypes.data_as(_dp), int(nthreads))
+            F(tree.prior_norm),
+            I(tree.gp_gather.reshape(-1)) if gp else None,
+            F(tree.gp_base[:, :3].reshape(-1)) if gp else None,
+            I(tree.gp_ecl.reshape(-1)) if gp else None,
+            lnp.ctypes.data_as(_dp), lle.ctypes.data_as(_dp), int(nthreads))
         return lnp, lle, used

@@ -78,10 +78,97 @@ def test_routing_matches_reference():
     assert leaves[0].cv_parnames.index('tilt') < leaves[0].cv_parnames.index('yaw')
 
 
-def test_gp_tree_routes_but_gp_likelihood_is_out_of_scope():
+def test_gp_tree_compiles():
+    """The shipped example (useGP = 1) compiles: GP hyper-parameters routed
+    from the core node, phase-sorted data, the changepoint eclipse range."""
     m = cvmodel.construct_model(INPUT)
-    with pytest.raises(NotImplementedError):
-        batch.compile_tree(m)
+    t = batch.compile_tree(m)
+    assert t.gp and t.E == 6 and t.ndim == 87
+    names = m.dynasty_par_names
+    for e in range(t.E):
+        assert [names[g] for g in t.gp_gather[e]] == ['ln_ampin_gp_core', 'ln_ampout_gp_core', 'ln_tau_gp_core']
+        x = t.x[t.offsets[e]:t.offsets[e + 1]]
+        assert np.all(np.diff(x) >= 0)
+        assert tuple(t.gp_ecl[e]) == (0, 1)  # phi_start = -0.2, phi_end = 0.3 (CVModel.py:582-590)
+    np.testing.assert_array_equal(t.gp_base[:, :3], [[0.1037, 0.0392, 0.0187]] * 6)
+
+
+def _gp_blocks(oracle, t, e, v, base_dcp):
+    """blocks of eclipse e for walker v, as the oracle / kernels form them"""
+    p = [v[g] if g >= 0 else t.consts[-1 - g] for g in t.gather[e]]
+    q, dphi, rwd, phi0 = p[4], p[5], p[8], p[13]
+    B = t.gp_base[e]
+    if abs(B[1] - dphi) / dphi > 1.2 or abs(B[0] - q) / q > 1.2 or abs(B[2] - rwd) / rwd > 1.2:
+        dcp = oracle.gp_base_dcp(q, dphi, rwd)
+    else:
+        dcp = base_dcp
+    return [[(ec - 1) + dcp + phi0, ec - dcp + phi0] for ec in range(t.gp_ecl[e, 0], t.gp_ecl[e, 1] + 1)]
+
+
+def test_gp_changepoints_and_kernel_match_reference(oracle):
+    """SimpleGPEclipse.calcChangepoints / create_GP of the reference
+    (tests/golden/gp_structure.json) against the compiled tree + oracle
+    changepoint distance, including the > 120 % recomputation (walkers 5, 6)."""
+    g = json.load(open(os.path.join(GOLD, "gp_structure.json")))
+    d = np.load(os.path.join(GOLD, "lnprob_gp.npz"))
+    m = cvmodel.construct_model(INPUT)
+    t = batch.compile_tree(m)
+    base_dcp = oracle.gp_base_dcp(*t.gp_base[0, :3])
+    seen_recompute = False
+    for rec in g["walkers"]:
+        v = d["walkers"][rec["walker"]]
+        for e, ecl in enumerate(rec["eclipses"]):
+            assert ecl["label"] == t.leaf_labels[e]
+            cps = _gp_blocks(oracle, t, e, v, base_dcp)
+            np.testing.assert_allclose(cps, ecl["changepoints"], rtol=0, atol=1e-11)
+            amps = np.exp(v[t.gp_gather[e]])
+            terms = ecl["kernel"]
+            assert len(terms) == 1 + len(cps)
+            np.testing.assert_allclose(terms[0][:2], [amps[0], amps[2]], rtol=1e-14)
+            assert terms[0][2] is None
+            for term, cp in zip(terms[1:], cps):
+                np.testing.assert_allclose(term[:2], [amps[1], amps[2]], rtol=1e-14)
+                np.testing.assert_allclose(term[2], cp, rtol=0, atol=1e-11)
+        seen_recompute |= rec["walker"] in (5, 6)
+    assert seen_recompute
+
+
+def test_gp_kalman_matches_dense_oracle(oracle):
+    """The O(N) state-space likelihood the kernels run (tests/gp_kalman.py)
+    equals the dense Cholesky likelihood: ties, empty and edge blocks."""
+    from tests.gp_kalman import gp_lnlike_kalman
+    rng = np.random.default_rng(7)
+    for trial in range(6):
+        n = int(rng.integers(2, 120))
+        x = np.sort(rng.uniform(-0.2, 0.3, n))
+        if trial == 1:
+            x[3:6] = x[3]
+        r = 0.004 * rng.standard_normal(n)
+        ye = rng.uniform(0.002, 0.008, n)
+        a1, a2, tau = np.exp(rng.uniform(-12, -7)), np.exp(rng.uniform(-12, -7)), np.exp(rng.uniform(-6.9, -2))
+        blocks = [(-0.98, -0.03), (0.02, 0.97)]
+        if trial == 2:
+            blocks = []
+        if trial == 3:
+            blocks = [(x[0], x[n // 3]), (x[n // 2], x[-1])]   # closed at data points
+        if trial == 4:
+            blocks = [(0.5, 0.4)]                               # empty (dist_cp > 1/2)
+        dense = oracle.gp_lnlike(x, r, ye, a1, a2, tau, blocks)
+        kal = gp_lnlike_kalman(x, r, ye, a1, a2, tau, blocks)
+        assert abs(dense - kal) <= 1e-10 * max(1.0, abs(dense)), (trial, dense, kal)
+
+
+def test_oracle_gp_lnprob_matches_reference(oracle):
+    """The oracle's GP ln_prob (dense GP, changepoint cache rule) against the
+    reference GPLCModel tree on the same walkers (tests/golden/lnprob_gp.npz)."""
+    d = np.load(os.path.join(GOLD, "lnprob_gp.npz"))
+    m = cvmodel.construct_model(INPUT)
+    assert m.dynasty_par_names == list(d["names"])
+    t = batch.compile_tree(m)
+    lnp, lle, _ = oracle.lnprob_batch(d["walkers"], t)
+    _same(lnp, d["ln_prob"], rtol=1e-10)
+    fin = np.isfinite(d["ln_prior"])
+    _same(lle.sum(1)[fin], d["ln_like"][fin], rtol=1e-10)
 
 
 def _tree_from_golden(tag):

@@ -145,3 +145,68 @@ def test_graph_replay_matches_eager():
             assert S._graph is not None
     for a, b in zip(out[0], out[1]):
         np.testing.assert_array_equal(a, b)
+
+
+# ---------------------------------------------------------------- GP trees
+def test_wdphases_matches_oracle(oracle):
+    from lfit_python_amd import roche
+    for q, dphi, r1 in ((0.1037, 0.0392, 0.0187), (0.2, 0.05, 0.01), (0.06, 0.03, 0.03)):
+        inc = oracle.findi(q, dphi)
+        got = roche.wdphases(q, inc, r1, 10)
+        ref = oracle.wdphases(q, inc, r1, 10)
+        np.testing.assert_allclose(got, ref, rtol=0, atol=1e-11)
+        assert got[0] < dphi / 2 < got[1]
+
+
+def test_gp_kernel_matches_dense_oracle(oracle):
+    """lfg_gp_lnlike (Kalman filter, one wave per set) against the dense
+    Cholesky oracle; bar 1e-9 relative (both exact, FP64 rounding apart)."""
+    from lfit_python_amd import gp
+    rng = np.random.default_rng(3)
+    n, W = 300, 24
+    x = rng.permutation(np.linspace(-0.2, 0.3, n))   # unsorted input: the wrapper sorts
+    ye = rng.uniform(0.003, 0.006, n)
+    res = 0.004 * rng.standard_normal((W, n))
+    hyp = np.stack([np.exp(rng.uniform(-11, -8, W)), np.exp(rng.uniform(-11, -8, W)),
+                    np.exp(rng.uniform(-6.9, -2, W))], axis=1)
+    d = rng.uniform(0.01, 0.05, W)
+    blocks = np.stack([np.stack([-1 + d, -d], 1), np.stack([d, 1 - d], 1)], axis=1)
+    got = gp.log_likelihood_batch(x, ye, res, hyp, blocks)
+    for i in range(W):
+        ref = oracle.gp_lnlike(x, res[i], ye, *hyp[i], blocks[i])
+        assert abs(got[i] - ref) <= 1e-9 * abs(ref), (i, got[i], ref)
+
+
+def test_gp_tree_matches_reference():
+    """Batched ln_prob of the shipped GP example (87 parameters, 6 eclipses)
+    against the reference tree's own ln_prob (tests/golden/lnprob_gp.npz)."""
+    import torch
+    from lfit_python_amd import batch, cvmodel
+    d = np.load(os.path.join(GOLD, "lnprob_gp.npz"))
+    m = cvmodel.construct_model(os.path.join(GOLD, "ref_test_data", "mcmc_input.dat"))
+    t = batch.compile_tree(m)
+    ev = batch.LnProbEvaluator(t)
+    W = len(d["walkers"])
+    lle = torch.empty((W, t.E), dtype=torch.float64, device="cuda")
+    got = ev(torch.as_tensor(d["walkers"], device="cuda"), lnlike_e=lle).cpu().numpy()
+    _same(got, d["ln_prob"], LNP_RTOL)
+    fin = np.isfinite(d["ln_prior"])
+    _same(lle.cpu().numpy().sum(1)[fin], d["ln_like"][fin], LNP_RTOL)
+
+
+def test_gp_leaf_scalar_path():
+    """The one-walker host path (cvmodel GP leaves with the reference's
+    changepoint cache, lfit_python_amd.gp) against the golden ln_prob."""
+    import copy
+    from lfit_python_amd import cvmodel
+    d = np.load(os.path.join(GOLD, "lnprob_gp.npz"))
+    m = cvmodel.construct_model(os.path.join(GOLD, "ref_test_data", "mcmc_input.dat"))
+    m.ln_like()  # fills the changepoint caches at the start values, as mcmcfit.py:154 does
+    for i in (0, 1, 5, 6):
+        mc = copy.deepcopy(m)
+        mc.dynasty_par_vals = list(d["walkers"][i])
+        got = mc.ln_prob()
+        ref = d["ln_prob"][i]
+        assert np.isfinite(got) == np.isfinite(ref)
+        if np.isfinite(ref):
+            assert abs(got - ref) <= LNP_RTOL * abs(ref), (i, got, ref)

@@ -41,15 +41,17 @@ def test_tree_struct_layout_matches_ctypes(tmp_path):
 #include <stddef.h>
 #include "lfg.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu\n", sizeof(lfg_tree), offsetof(lfg_tree, gather),
-         offsetof(lfg_tree, x), offsetof(lfg_tree, prior_norm), offsetof(lfg_tree, roche_priors));
+  printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(lfg_tree), offsetof(lfg_tree, gather),
+         offsetof(lfg_tree, x), offsetof(lfg_tree, prior_norm), offsetof(lfg_tree, roche_priors),
+         offsetof(lfg_tree, gp_gather), offsetof(lfg_tree, gp_ecl));
   return 0;
 }''')
     exe = tmp_path / "layout"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(prog)], check=True)
     got = list(map(int, subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()))
     T = _native.LfgTree
-    assert got == [ctypes.sizeof(T), T.gather.offset, T.x.offset, T.prior_norm.offset, T.roche_priors.offset]
+    assert got == [ctypes.sizeof(T), T.gather.offset, T.x.offset, T.prior_norm.offset, T.roche_priors.offset,
+                   T.gp_gather.offset, T.gp_ecl.offset]
 
 
 def test_constants_agree_with_header():
@@ -73,6 +75,9 @@ def test_argument_errors_without_gpu():
     assert L.lfg_lnprob(None, 4, None, None, None, None, 0, None) == -1
     assert L.lfg_stretch_propose(None, 15, 4, 0, 2.0, 1, 0, None, None, None) == -1
     assert L.lfg_roche(7, None, None, 1, None, None, None) == -1
+    assert L.lfg_wdphases(None, None, None, 4, 10, None, None, None, None) == -1
+    assert L.lfg_wdphases(None, None, None, 0, 10, None, None, None, None) == 0  # nothing to do
+    assert L.lfg_gp_lnlike(None, None, None, 0, 10, None, None, 0, None, None) == -1
     assert L.lfg_version().startswith(b"lfg")
 
 

@@ -4,10 +4,13 @@
 Runs ONLY in the build container (it imports /root/reference/model.py and
 CVModel.py; nothing of the reference travels).  The reference's third-party
 imports are replaced by stand-ins:
-  george      unused by the non-GP path -> empty module
+  george      kernels / GP -> a recorder of the kernel the reference builds
+              (terms, amplitudes, metric, blocks) whose log_likelihood is the
+              exact dense GP likelihood (numpy Cholesky): george's HODLR
+              solver approximates exactly this
   configobj   ConfigObj(path) -> key = value reader
   lfit        CV(pars).calcFlux(pars, x, w) -> this repo's CPU oracle
-  trm.roche   xl1 / findphi / findi / bspot -> this repo's CPU oracle
+  trm.roche   xl1 / findphi / findi / bspot / wdphases -> this repo's CPU oracle
 so the fixtures pin the reference's parameter routing, yaw/tilt swap, Prior
 quirks, Lightcurve loading/trim, Roche-prior logic and chi^2 / ln_like /
 ln_prob composition; the flux arithmetic inside them is the oracle's
@@ -20,7 +23,16 @@ Outputs (JSON / npz, data only):
   tests/golden/lnprob_tree.npz       ln_prior / ln_like / ln_prob per walker
                                      (6-eclipse complex tree, useGP = 0)
   tests/golden/lnprob_simple.npz     same for a 1-eclipse simple-BS tree
+  tests/golden/lnprob_gp.npz         the shipped example as is (useGP = 1):
+                                     ln_prior / ln_like / ln_prob per walker,
+                                     each walker on a fresh copy of the model
+                                     whose changepoint cache was set by one
+                                     ln_like at the start values (what each
+                                     emcee pool task receives)
+  tests/golden/gp_structure.json     changepoints and kernel terms the
+                                     reference builds for a few walkers
 """
+import copy
 import json
 import os
 import sys
@@ -40,11 +52,66 @@ from oracle.oracle import Oracle  # noqa: E402
 ORC = Oracle()
 
 
+LAST_GP = {}
+
+
+class _Kernel:
+    """george kernel stand-in: a sum of amp * Matern32(metric) terms, each
+    optionally restricted to a block of x (george 0.3: closed [min, max])."""
+
+    def __init__(self, terms):
+        self.terms = terms
+
+    def __rmul__(self, a):
+        return _Kernel([(float(a) * amp, metric, blk) for amp, metric, blk in self.terms])
+
+    __mul__ = __rmul__
+
+    def __add__(self, other):
+        return _Kernel(self.terms + other.terms)
+
+
+def _matern32(metric, block=None):
+    blk = None if block is None else tuple(float(v) for v in np.atleast_2d(block)[0])
+    return _Kernel([(1.0, float(metric), blk)])
+
+
+class _GP:
+    def __init__(self, kernel, solver=None):
+        self.kernel = kernel
+        LAST_GP["kernel"] = kernel.terms
+
+    def compute(self, x, yerr):
+        self.x = np.asarray(x, dtype=np.float64)
+        self.yerr = np.asarray(yerr, dtype=np.float64)
+
+    def log_likelihood(self, r, quiet=False):
+        x = self.x
+        d = x[:, None] - x[None, :]
+        K = np.diag(self.yerr ** 2)
+        for amp, metric, blk in self.kernel.terms:
+            u = np.sqrt(3.0 * d * d / metric)
+            k = amp * (1.0 + u) * np.exp(-u)
+            if blk is not None:
+                inb = (x >= blk[0]) & (x <= blk[1])
+                k = k * (inb[:, None] & inb[None, :])
+            K = K + k
+        try:
+            L = np.linalg.cholesky(K)
+        except np.linalg.LinAlgError:
+            if quiet:
+                return -np.inf
+            raise
+        z = np.linalg.solve(L, np.asarray(r, dtype=np.float64))
+        ll = -0.5 * (z @ z + 2.0 * np.sum(np.log(np.diag(L))) + len(x) * np.log(2.0 * np.pi))
+        return ll if np.isfinite(ll) else -np.inf
+
+
 def install_standins():
     george = types.ModuleType("george")
-    george.kernels = types.SimpleNamespace(Matern32Kernel=None)
-    george.GP = None
-    george.HODLRSolver = None
+    george.kernels = types.SimpleNamespace(Matern32Kernel=_matern32)
+    george.GP = _GP
+    george.HODLRSolver = object()
     sys.modules["george"] = george
 
     cfg = types.ModuleType("configobj")
@@ -86,6 +153,7 @@ def install_standins():
     roche.findphi = ORC.findphi
     roche.findi = ORC.findi
     roche.bspot = ORC.bspot
+    roche.wdphases = ORC.wdphases
     trm.roche = roche
     sys.modules["trm"] = trm
     sys.modules["trm.roche"] = roche
@@ -183,6 +251,47 @@ def main():
                                 walkers=walk, ln_prior=np.array(lp), ln_like=np.array(ll),
                                 ln_prob=np.array(lprob), input=np.array("\n".join(lines)))
             print(tag, "ndim", len(names), "finite ln_prob", int(np.isfinite(lprob).sum()), "of", nw)
+    # ---- the GP example tree as shipped (useGP = 1)
+    os.chdir(os.path.join(REF, "test_data"))
+    try:
+        m = refcv.construct_model("mcmc_input.dat")
+    finally:
+        os.chdir(cwd)
+    names = m.dynasty_par_names
+    p0 = np.asarray(m.dynasty_par_vals)
+    m.ln_like()  # the sanity evaluation of mcmcfit.py:154: fills the changepoint caches
+    nw = 40
+    walk = p0 * (1.0 + 0.02 * rng.standard_normal((nw, p0.size)))
+    walk[nw // 2:] = p0 * (1.0 + 0.3 * rng.standard_normal((nw - nw // 2, p0.size)))
+    iq, idp, irw = names.index("q_core"), names.index("dphi_core"), names.index("rwd_core")
+    walk[4, irw] = p0[irw] * 0.4     # > 120 % changes: the changepoints are recomputed
+    walk[5, iq] = p0[iq] * 0.4
+    walk[6, idp] = p0[idp] * 0.42
+    lp, ll, lprob, structs = [], [], [], []
+    for i, v in enumerate(walk):
+        mc = copy.deepcopy(m)  # what a pool task unpickles
+        mc.dynasty_par_vals = list(v)
+        pri = mc.ln_prior()
+        lp.append(pri)
+        ll.append(copy.deepcopy(mc).ln_like() if np.isfinite(pri) else np.nan)
+        lprob.append(mc.ln_prob())
+        if i < 8 and np.isfinite(pri):
+            leaves = sorted(mc.search_node_type("Eclipse"), key=lambda n: int(n.label))
+            rec = []
+            for leaf in leaves:
+                try:
+                    cps = [[float(a), float(b)] for a, b in leaf.calcChangepoints()]
+                    leaf.create_GP()
+                    terms = [[a, mt, list(bk) if bk else None] for a, mt, bk in LAST_GP["kernel"]]
+                except Exception as exc:  # noqa: BLE001 - record what the reference raises
+                    cps, terms = repr(exc), None
+                rec.append({"label": leaf.label, "changepoints": cps, "kernel": terms})
+            structs.append({"walker": i, "eclipses": rec})
+    np.savez_compressed(os.path.join(OUT, "lnprob_gp.npz"), names=np.array(names), walkers=walk,
+                        ln_prior=np.array(lp), ln_like=np.array(ll), ln_prob=np.array(lprob))
+    json.dump({"source": "reference CVModel.py SimpleGPEclipse with the george stand-in above",
+               "walkers": structs}, open(os.path.join(OUT, "gp_structure.json"), "w"), indent=1)
+    print("gp ndim", len(names), "finite ln_prob", int(np.isfinite(lprob).sum()), "of", nw)
     print("wrote", sorted(os.listdir(OUT)))
 
 
