@@ -117,6 +117,16 @@ int lfg_lnprob(const double* walkers, int W, const lfg_tree* tree,
                void* stream);
 
 /*
+ * ln_prior alone of a walker ensemble through a compiled tree: Node.ln_prior
+ * of the tree root (model.py:426-474) with the LCModel and eclipse Roche
+ * priors (CVModel.py:193-324, 440-491), as mcmcfit.ln_prior
+ * (mcmcfit.py:30-34) feeds the walker initialisation (mcmc_utils.py:46-72).
+ *   walkers [dev] W x ndim;  lnprior [dev] W
+ */
+int lfg_lnprior(const double* walkers, int W, const lfg_tree* tree,
+                double* lnprior, void* ws, size_t ws_bytes, void* stream);
+
+/*
  * White-box access to the element tables of MODEL_SPEC.md section 5 for W
  * parameter sets (tests): a, b, wgt [dev] W x LFG_NEL eclipse intervals
  * (phase) and weights; donor [dev] W x LFG_NDONOR x 3; geo [dev] W x LFG_NGEO;

@@ -55,7 +55,7 @@ class LfgTree(ctypes.Structure):
     ]
 
 
-EXPORTS = ("lfg_workspace_size", "lfg_flux", "lfg_lnprob", "lfg_lnprob_timed",
+EXPORTS = ("lfg_workspace_size", "lfg_flux", "lfg_lnprob", "lfg_lnprior", "lfg_lnprob_timed",
            "lfg_elements", "lfg_roche", "lfg_stretch_propose", "lfg_stretch_accept",
            "lfg_stretch_propose_dev", "lfg_stretch_accept_dev", "lfg_event_create", "lfg_event_destroy",
            "lfg_event_elapsed_ms", "lfg_wdphases", "lfg_gp_lnlike", "lfg_version")
@@ -101,6 +101,8 @@ def lib():
         L.lfg_flux.argtypes = [vp, ip, ip, vp, vp, ip, ip, vp, vp, vp, vp, sz, vp]
         L.lfg_lnprob.restype = ip
         L.lfg_lnprob.argtypes = [vp, ip, ctypes.POINTER(LfgTree), vp, vp, vp, sz, vp]
+        L.lfg_lnprior.restype = ip
+        L.lfg_lnprior.argtypes = [vp, ip, ctypes.POINTER(LfgTree), vp, vp, sz, vp]
         L.lfg_elements.restype = ip
         L.lfg_elements.argtypes = [vp, ip, ip, vp, vp, vp, vp, vp, vp, vp, sz, vp]
         L.lfg_roche.restype = ip

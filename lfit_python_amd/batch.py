@@ -201,6 +201,24 @@ class LnProbEvaluator:
         return out
 
 
+    def ln_prior(self, walkers, out=None):
+        """ln_prior alone (mcmcfit.ln_prior, mcmcfit.py:30-34) of walkers [W, ndim]."""
+        import torch
+        if walkers.dtype != torch.float64 or walkers.device != self.device or not walkers.is_contiguous():
+            walkers = walkers.to(device=self.device, dtype=torch.float64).contiguous()
+        W = walkers.shape[0]
+        self._ensure(W)
+        if out is None:
+            out = torch.empty(W, dtype=torch.float64, device=self.device)
+        rc = self.L.lfg_lnprior(ctypes.c_void_p(walkers.data_ptr()), W, ctypes.byref(self.ctree),
+                                ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(self._ws.data_ptr()),
+                                self._ws.numel(), _native.stream_ptr(self.device))
+        _native.check(rc, "lfg_lnprior")
+        if self.tree.fixed_invalid:
+            out.fill_(-np.inf)
+        return out
+
+
 def ln_prob_batch(model, walkers, nsub=1):
     """Convenience: compile `model` and evaluate walkers [W, ndim] (numpy)."""
     import torch

@@ -1126,6 +1126,10 @@ __global__ void k_combine(int W, int E, const double* __restrict__ prior, const 
         const double* G = geo + (size_t(w) * E + e) * LFG_NGEO;
         lp += G[G_RPRIOR] + G[G_RPRIOR_BS];
     }
+    if (!lle) {  // ln_prior only (lfg_lnprior)
+        lnp[w] = isfinite(lp) ? lp : -INFINITY;
+        return;
+    }
     if (!isfinite(lp)) {
         for (int e = 0; e < E; ++e) lle[size_t(w) * E + e] = -INFINITY;
         lnp[w] = -INFINITY;
@@ -1372,6 +1376,25 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
     rc = launch_ok();
     mark(4);
     return rc;
+}
+
+int lfg_lnprior(const double* walkers, int W, const lfg_tree* T, double* lnprior, void* wsp, size_t ws_bytes,
+                void* stream)
+{
+    if (W <= 0 || !T || T->E <= 0 || T->ndim <= 0 || !walkers || !lnprior) return LFG_E_ARGS;
+    Ws ws = carve(wsp, W, T->E);
+    if (!wsp || ws_bytes < ws.total) return LFG_E_WORKSPACE;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    SetupArgs S{walkers, W, T->ndim, T->E, 18, T->gather, T->npars, T->consts, T->prior_type, T->prior_p1,
+                T->prior_p2, T->prior_norm, T->roche_priors, ws.geo, ws.status, ws.prior, ws.bstatus, 0,
+                nullptr, nullptr};
+    const int nlanes = 2 * W * T->E + W;
+    hipLaunchKernelGGL(k_setup, dim3((nlanes + SETUP_BLOCK - 1) / SETUP_BLOCK), dim3(SETUP_BLOCK), 0, st, S);
+    int rc = launch_ok();
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_combine, dim3((W + 255) / 256), dim3(256), 0, st, W, T->E, ws.prior, ws.geo, nullptr,
+                       lnprior);
+    return launch_ok();
 }
 
 int lfg_lnprob(const double* walkers, int W, const lfg_tree* T, double* lnp, double* lnlike_e, void* wsp,

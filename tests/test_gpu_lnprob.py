@@ -210,3 +210,19 @@ def test_gp_leaf_scalar_path():
         assert np.isfinite(got) == np.isfinite(ref)
         if np.isfinite(ref):
             assert abs(got - ref) <= LNP_RTOL * abs(ref), (i, got, ref)
+
+
+@pytest.mark.parametrize("tag", ["tree", "simple", "gp"])
+def test_lnprior_matches_reference(tag):
+    """lfg_lnprior (mcmcfit.ln_prior, used for the walker ball) against the
+    reference tree's own ln_prior on the golden walkers."""
+    import torch
+    from lfit_python_amd import batch, cvmodel
+    if tag == "gp":
+        d = np.load(os.path.join(GOLD, "lnprob_gp.npz"))
+        m = cvmodel.construct_model(os.path.join(GOLD, "ref_test_data", "mcmc_input.dat"))
+    else:
+        d, m = _golden_tree(tag)
+    ev = batch.LnProbEvaluator(batch.compile_tree(m))
+    got = ev.ln_prior(torch.as_tensor(d["walkers"], device="cuda")).cpu().numpy()
+    _same(got, d["ln_prior"], 1e-10)
