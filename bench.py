@@ -4,8 +4,10 @@ emcee loop, on BASELINE.json's metric config (single eclipse, complex bright
 spot, 300-point phase grid; config 2 = 1024 walkers per GPU).
 
 A step is one emcee iteration of the whole ensemble: two half-steps of
-propose -> batched ln_prob (lfg_lnprob: k_setup, k_bspot, k_elements,
-k_lnlike, k_combine) -> all_gather -> accept.  value = walkers x steps /
+propose -> batched ln_prob of the proposals (k_setup, k_elements, k_lnlike)
+-> accept.  On one GPU the acceptance is fused into k_lnlike
+(lfg_stretch_lnprob_accept); with N ranks each evaluates its shard
+(lfg_lnprob), all_gathers ln_prob, and every rank accepts.  value = walkers x steps /
 time, max over ranks, inputs resident in HBM.  Per-GPU work is fixed (weak
 scaling): --walkers per GPU, total = walkers x N.
 
@@ -35,9 +37,9 @@ HBM_PEAK_GBS = 8000.0
 FP64_PEAK_TFLOPS = 78.6
 PMC_FILE = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
 
-NEV = 5  # LFG_NEV (include/lfg.h)
+NEV = 4  # LFG_NEV (include/lfg.h)
 # (name as rocprofv3 prints it, start event, end event)
-KERNELS = [("k_setup", 0, 1), ("k_elements", 1, 2), ("k_lnlike<true>", 2, 3), ("k_combine", 3, 4)]
+KERNELS = [("k_setup", 0, 1), ("k_elements", 1, 2), ("k_lnlike<1>", 2, 3)]
 
 # Algorithmic HBM bytes per (walker, eclipse) pair of each kernel (DESIGN.md
 # section 3): what the kernel must read and write, counted once.
@@ -47,8 +49,7 @@ WT_N = 124                                     # weight doubles per pair
 PER_PAIR = {
     "k_setup": 18 * 8 + GEO_SETUP * 8 + 4 + 3 * 8 + GEO_BSPOT * 8 + 4,   # setup + stream lanes
     "k_elements": GEO_READ * 8 + 8 + NEL * 16 + U_DON * DON_STRIDE * 8 + WT_N * 8,
-    "k_lnlike<true>": GEO_READ * 8 + 4 + NEL * 16 + U_DON * DON_STRIDE * 8 + WT_N * 8 + 8,
-    "k_combine": 0,
+    "k_lnlike<1>": GEO_READ * 8 + 4 + NEL * 16 + U_DON * DON_STRIDE * 8 + WT_N * 8 + 8,
 }
 
 
@@ -64,6 +65,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--seed", type=int, default=20261015)
+    ap.add_argument("--time-every", type=int, default=4,
+                    help="record the dominant kernel's event pair on every k-th ln_prob call of the timed region")
     return ap.parse_args()
 
 
@@ -71,10 +74,9 @@ def algo_bytes(kernel, pairs, walkers, ndim, E, npts):
     b = PER_PAIR[kernel] * pairs
     if kernel == "k_setup":
         b += walkers * (ndim * 8 + 8)          # per-walker prior lane
-    if kernel == "k_lnlike<true>":
+    if kernel == "k_lnlike<1>":
         b += E * npts * 4 * 8                   # x, y, ye, w once per launch
-    if kernel == "k_combine":
-        b += walkers * (8 * 2 + E * 8 * 3)      # prior, lnp; per eclipse 2 Roche priors + ln_like
+        b += walkers * (8 * 2 + E * 8 * 2)      # fused combine: prior, lnp; 2 Roche priors per eclipse
     return b
 
 
@@ -125,6 +127,12 @@ def main():
     # HIP events around kernels of lfg_lnprob calls (include/lfg.h LFG_NEV)
     events = []
     want = [True] * NEV  # which events to record
+    every = [1]          # record on every k-th call
+    ncall = [0]
+
+    def sampled():
+        ncall[0] += 1
+        return (ncall[0] - 1) % every[0] == 0
 
     def make_evs():
         evs = (ctypes.c_void_p * NEV)()
@@ -138,13 +146,29 @@ def main():
     def timed_eval(x, out=None):
         if out is None:
             out = torch.empty(x.shape[0], dtype=torch.float64, device=dev)
-        evs = make_evs()
-        events.append((evs, x.shape[0]))
+        evs = None
+        if sampled():
+            evs = make_evs()
+            events.append((evs, x.shape[0]))
         rc = L.lfg_lnprob_timed(ctypes.c_void_p(x.data_ptr()), x.shape[0], ctypes.byref(ev.ctree),
                                 ctypes.c_void_p(out.data_ptr()), None, ctypes.c_void_p(ev._ws.data_ptr()),
                                 ev._ws.numel(), _native.stream_ptr(dev), evs)
         _native.check(rc, "lfg_lnprob_timed")
         return out
+
+    def timed_accept(q, pos, lnp, half, zfac, seed, step, naccept, lnp_new=None):
+        """the single-process path: lfg_stretch_lnprob_accept with the events"""
+        evs = None
+        if sampled():
+            evs = make_evs()
+            events.append((evs, q.shape[0]))
+        ev.lnprob_accept(q, pos, lnp, half, zfac, seed, step, naccept, lnp_new=lnp_new, events=evs)
+
+    def set_timing(on):
+        if world == 1:
+            S.accept_timer = timed_accept if on else None
+        else:
+            S.timer = timed_eval if on else None
 
     def kernel_ms(kernels):
         """mean ms per launch of each (name, a, b) over the recorded calls; frees the events"""
@@ -164,10 +188,10 @@ def main():
     ev._ensure(W)
     for i in range(args.warmup):
         if i == args.warmup - 1:
-            S.timer = timed_eval  # calibration: every kernel
+            set_timing(True)  # calibration: every kernel
         S.step()
     torch.cuda.synchronize()
-    S.timer = None
+    set_timing(False)
     dom = 2  # k_lnlike unless calibrated
     calib = {}
     if events:
@@ -177,7 +201,9 @@ def main():
     events.clear()
     kname, ea, eb = KERNELS[dom]
     want[:] = [i in (ea, eb) for i in range(NEV)]
-    S.timer = timed_eval
+    every[0] = max(1, args.time_every)
+    ncall[0] = 0
+    set_timing(True)
 
     if dist:
         dist.barrier()
@@ -190,7 +216,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    S.timer = None
+    set_timing(False)
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

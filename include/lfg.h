@@ -150,10 +150,10 @@ int lfg_roche(int op, const double* a, const double* b, int n, double* out,
 /*
  * Same as lfg_lnprob, recording LFG_NEV caller-created hipEvent_t events on
  * `stream` around each kernel (bench timing): ev[0] before k_setup, ev[1]
- * after k_setup, ev[2] after k_elements, ev[3] after k_lnlike, ev[4] after
- * k_combine.  NULL entries are skipped.
+ * after k_setup, ev[2] after k_elements, ev[3] after k_lnlike (which also
+ * forms ln_prob).  NULL entries are skipped.
  */
-#define LFG_NEV 5
+#define LFG_NEV 4
 int lfg_lnprob_timed(const double* walkers, int W, const lfg_tree* tree,
                      double* lnp, double* lnlike_e, void* ws, size_t ws_bytes,
                      void* stream, void* const* ev);
@@ -178,6 +178,22 @@ int lfg_stretch_accept(double* pos, double* lnp, int W, int ndim, int half,
                        const double* q, const double* zfac,
                        const double* lnp_new, unsigned long long seed,
                        unsigned long long step, int* naccept, void* stream);
+
+/*
+ * One half-step of the stretch move after the proposal: the batched ln_prob
+ * of the proposals q (lfg_lnprob on W/2 walkers) with the Metropolis step of
+ * lfg_stretch_accept fused into the kernel that forms each ln_prob (same
+ * draws, same result; one launch fewer per half-step).  pos, lnp, naccept
+ * as lfg_stretch_accept; lnp_new [dev] nullable W/2; ev: LFG_NEV events or
+ * NULL.  Single process only: with walker shards over ranks, use lfg_lnprob,
+ * gather, then lfg_stretch_accept.
+ */
+int lfg_stretch_lnprob_accept(double* pos, double* lnp, int W, int half,
+                              const double* q, const double* zfac,
+                              const lfg_tree* tree, unsigned long long seed,
+                              unsigned long long step, int* naccept,
+                              double* lnp_new, void* ws, size_t ws_bytes,
+                              void* stream, void* const* ev);
 
 /*
  * The same two moves with the step counter read from device memory

@@ -201,6 +201,18 @@ class LnProbEvaluator:
         return out
 
 
+    def lnprob_accept(self, q, pos, lnp, half, zfac, seed, step, naccept, lnp_new=None, events=None):
+        """ln_prob of the proposals q [W/2, ndim] with the stretch move's
+        Metropolis step fused in (lfg_stretch_lnprob_accept): updates pos,
+        lnp and naccept of half `half` in place."""
+        W = pos.shape[0]
+        self._ensure(W // 2)
+        vp = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
+        rc = self.L.lfg_stretch_lnprob_accept(vp(pos), vp(lnp), W, half, vp(q), vp(zfac), ctypes.byref(self.ctree),
+                                              seed, step, vp(naccept), vp(lnp_new), vp(self._ws), self._ws.numel(),
+                                              _native.stream_ptr(self.device), events)
+        _native.check(rc, "lfg_stretch_lnprob_accept")
+
     def ln_prior(self, walkers, out=None):
         """ln_prior alone (mcmcfit.ln_prior, mcmcfit.py:30-34) of walkers [W, ndim]."""
         import torch

@@ -11,7 +11,7 @@
 //   k_lnlike    one workgroup per (walker, eclipse): element tables staged in
 //               LDS, lanes stride the phase axis (coalesced), exposure
 //               integration, fused chi^2 with a wavefront/LDS reduction
-//   k_combine   one lane per walker: ln_prob = ln_prior + sum_e ln_like_e
+//               and, for the walker's last eclipse, ln_prob = ln_prior + sum_e ln_like_e
 // Replaces, per walker, mcmcfit.ln_prob (mcmcfit.py:37-41) -> Node.ln_prob
 // (model.py:476-498) -> lfit.CV.calcFlux (CVModel.py:138).
 #include <hip/hip_runtime.h>
@@ -46,6 +46,7 @@ struct Ws {
     double* wts;    // [pairs][WT_N] ring / spot weights
     double* prior;
     double* lle;
+    int* done;      // [W] eclipses finished per walker (k_lnlike's fused combine, E > 1)
     size_t total;
 };
 
@@ -66,6 +67,7 @@ Ws carve(void* base, int W, int E)
     ws.wts = reinterpret_cast<double*>(take(pairs * WT_N * sizeof(double)));
     ws.prior = reinterpret_cast<double*>(take(size_t(W) * sizeof(double)));
     ws.lle = reinterpret_cast<double*>(take(pairs * sizeof(double)));
+    ws.done = reinterpret_cast<int*>(take(size_t(W) * sizeof(int)));
     ws.total = off;
     return ws;
 }
@@ -89,6 +91,7 @@ struct SetupArgs {
     int gp;        // GP likelihood: per-pair hyper-parameters and changepoints
     const int* gp_gather;
     const double* gp_base;
+    int* done;     // nullable: per-walker eclipse counters of k_lnlike, zeroed here
 };
 
 __device__ inline double gather_par(const SetupArgs& A, int w, int g)
@@ -165,6 +168,7 @@ __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
                 lp += prior_lnprob(A.prior_type[d], A.prior_p1[d], A.prior_p2[d], A.prior_norm[d], v[d]);
         }
         A.prior[w] = lp;
+        if (A.done) A.done[w] = 0;
         return;
     }
 
@@ -529,7 +533,84 @@ struct LikeArgs {
     double* lle;    // nullable, [pairs]
     int npairs;
     const int* gp_ecl;  // GP mode: [E][2] first and last changepoint eclipse numbers
+    // fused k_combine (MODE 1, 2): ln_prob = ln_prior + sum_e ln_like_e
+    const double* prior;  // [W] Prior.ln_prob sums + LCModel prior (k_setup)
+    double* lnp;          // nullable, [W]
+    int* done;            // [W] counters zeroed by k_setup (E > 1)
+    bool combine;         // form ln_prob at all
+    // fused stretch-move acceptance (lfg_stretch_lnprob_accept; pos nullptr:
+    // off): walker w of this batch is the proposal for ensemble walker
+    // half * W + w, with W = the batch size = half the ensemble
+    double* pos;
+    double* lnp_ens;
+    const double* qprop;
+    const double* zfac;
+    int ndim, half;
+    unsigned long long seed, step;
+    int* naccept;
 };
+
+__device__ inline uint4 draw(unsigned long long seed, unsigned long long step, int half, int purpose, int i);
+__device__ inline double u53(unsigned a, unsigned b);
+
+// ln_prob of walker w once all its eclipses' ln_like are in lle
+// (Node.ln_prob, model.py:476-498; what k_combine does), then the
+// Metropolis step of the stretch move for it when fused (k_accept's rule)
+__device__ inline void combine_walker(const LikeArgs& L, int w)
+{
+    double lp = L.prior[w];
+    for (int e = 0; e < L.E; ++e) {
+        const double* G = L.geo + (size_t(w) * L.E + e) * LFG_NGEO;
+        lp += G[G_RPRIOR] + G[G_RPRIOR_BS];
+    }
+    double v;
+    if (!isfinite(lp)) {
+        for (int e = 0; e < L.E; ++e) L.lle[size_t(w) * L.E + e] = -INFINITY;
+        v = -INFINITY;
+    } else {
+        double ll = 0.0;
+        for (int e = 0; e < L.E; ++e) ll += L.lle[size_t(w) * L.E + e];
+        v = lp + ll;
+    }
+    if (L.lnp) L.lnp[w] = v;
+    if (L.pos) {
+        const int wg = L.half * L.npairs / L.E + w;  // ensemble index (npairs / E = batch walkers)
+        const uint4 r = draw(L.seed, L.step, L.half, 1, w);
+        const double lu = log(u53(r.x, r.y));
+        if (lu < L.zfac[w] + v - L.lnp_ens[wg]) {
+            double* p = L.pos + size_t(wg) * L.ndim;
+            const double* qi = L.qprop + size_t(w) * L.ndim;
+            for (int d = 0; d < L.ndim; ++d) p[d] = qi[d];
+            L.lnp_ens[wg] = v;
+            if (L.naccept) L.naccept[wg] += 1;
+        }
+    }
+}
+
+// called by thread 0 after it wrote lle[pair]: the walker's last finished
+// eclipse forms its ln_prob (E = 1: at once; E > 1: a device-scope counter,
+// with fences so that the other blocks' lle are visible across XCD L2s)
+// end of k_lnlike (all threads; lle[pair] written by thread 0): with one
+// eclipse per walker and fused acceptance, thread 0 decides with the
+// prefetched draw and the copy of the accepted proposal is spread over the
+// first ndim lanes; otherwise thread 0 runs combine_after
+__device__ inline void finish_walker(const LikeArgs& L, int pair, int tid, bool acc1, double aq, double alu,
+                                     double azf, double alo, int* sflag);
+
+__device__ inline void combine_after(const LikeArgs& L, int pair)
+{
+    if (!L.combine) return;
+    const int w = pair / L.E;
+    if (L.E == 1) {
+        combine_walker(L, w);
+        return;
+    }
+    __threadfence();
+    if (atomicAdd(L.done + w, 1) == L.E - 1) {
+        __threadfence();
+        combine_walker(L, w);
+    }
+}
 
 // ---- sweeps over phase-sorted tiles of points (MODEL_SPEC 6 restated) ----
 // Every eclipse / visibility term is a sum over elements of w_k g_k(p), where
@@ -838,6 +919,37 @@ __device__ inline void direct_spot_donor(const double2* __restrict__ ABs, const 
 #define LIKE_STAMP(i)
 #endif
 
+__device__ inline void finish_walker(const LikeArgs& L, int pair, int tid, bool acc1, double aq, double alu,
+                                     double azf, double alo, int* sflag)
+{
+    if (!acc1) {
+        if (tid == 0) combine_after(L, pair);
+        return;
+    }
+    __syncthreads();  // sflag is free; lle[pair] is this block's own write
+    const int wg = L.half * L.npairs + pair;
+    if (tid == 0) {
+        const double* G = L.geo + size_t(pair) * LFG_NGEO;
+        const double lp = L.prior[pair] + G[G_RPRIOR] + G[G_RPRIOR_BS];
+        double v;
+        if (!isfinite(lp)) {
+            L.lle[pair] = -INFINITY;
+            v = -INFINITY;
+        } else {
+            v = lp + L.lle[pair];
+        }
+        if (L.lnp) L.lnp[pair] = v;
+        const bool a = alu < azf + v - alo;
+        if (a) {
+            L.lnp_ens[wg] = v;
+            if (L.naccept) L.naccept[wg] += 1;
+        }
+        sflag[0] = a ? 1 : 0;
+    }
+    __syncthreads();
+    if (sflag[0] && tid < L.ndim) L.pos[size_t(wg) * L.ndim + tid] = aq;
+}
+
 // MODE 0: flux (and components) only; 1: fused chi^2 -> ln_like; 2: GP
 // ln_like of the residuals (a Kalman filter over each tile's sorted points,
 // run by wave 0 while the other waves wait at the tile barrier)
@@ -869,6 +981,21 @@ __global__ __launch_bounds__(LIKE_THREADS) void k_lnlike(LikeArgs L)
     const double2* AB = L.AB + size_t(pair) * NEL;
     const double* DONp = L.DON + size_t(pair) * U_DON * DON_STRIDE;
 
+    // fused acceptance with one eclipse per walker: the proposal's coordinates
+    // (one per lane), the uniform draw and the old ln_prob are fetched here,
+    // off the tail of the block (combine_walker does it for E > 1)
+    const bool acc1 = CHI && L.pos && L.E == 1;
+    double aq = 0.0, alu = 0.0, azf = 0.0, alo = 0.0;
+    if (acc1) {
+        const int wg = L.half * L.npairs + pair;
+        if (tid < L.ndim) aq = L.qprop[size_t(pair) * L.ndim + tid];
+        if (tid == 0) {
+            const uint4 r = draw(L.seed, L.step, L.half, 1, pair);
+            alu = log(u53(r.x, r.y));
+            azf = L.zfac[pair];
+            alo = L.lnp_ens[wg];
+        }
+    }
     // every global load of the prologue is issued before anything waits on
     // one (the status included): a single memory round trip
     const int st = L.status[pair];
@@ -922,7 +1049,10 @@ __global__ __launch_bounds__(LIKE_THREADS) void k_lnlike(LikeArgs L)
             if (L.comps)
                 for (int m = 0; m < 4; ++m) L.comps[(size_t(m) * L.npairs + pair) * n + p] = NAN;
         }
-        if (CHI && tid == 0) L.lle[pair] = -INFINITY;
+        if (CHI) {
+            if (tid == 0) L.lle[pair] = -INFINITY;
+            finish_walker(L, pair, tid, acc1, aq, alu, azf, alo, sflag);
+        }
         return;
     }
     double tb = 0.0, dn = 0.0, vs = 0.0;
@@ -1103,6 +1233,7 @@ __global__ __launch_bounds__(LIKE_THREADS) void k_lnlike(LikeArgs L)
             const bool okp = G[G_GP_OK] != 0.0;
             L.lle[pair] = (okp && n > 0) ? gpf.lnlike() : (okp ? 0.0 : -INFINITY);
         }
+        finish_walker(L, pair, tid, acc1, aq, alu, azf, alo, sflag);
     } else if (CHI) {
         chi = wave_sum(chi);
         if (lane == 0) red[0][wv] = chi;
@@ -1112,6 +1243,7 @@ __global__ __launch_bounds__(LIKE_THREADS) void k_lnlike(LikeArgs L)
             for (int i = 0; i < nw; ++i) tot += red[0][i];
             L.lle[pair] = -0.5 * tot;
         }
+        finish_walker(L, pair, tid, acc1, aq, alu, azf, alo, sflag);
     }
 }
 
@@ -1335,12 +1467,13 @@ int lfg_flux(const double* pars, int W, int P, const double* x, const double* w,
     if (!wsp || ws_bytes < ws.total) return LFG_E_WORKSPACE;
     hipStream_t st = static_cast<hipStream_t>(stream);
     SetupArgs S{pars, W, P, 1, P, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
-                ws.geo, ws.status, ws.prior, ws.bstatus, 0, nullptr, nullptr};
+                ws.geo, ws.status, ws.prior, ws.bstatus, 0, nullptr, nullptr, nullptr};
     int rc = run_front(S, ws, st, nullptr);
     if (rc) return rc;
     if (N > 0) {
         LikeArgs L{ws.geo, ws.status, ws.ab, ws.donor, ws.wts, 1, nullptr, N, x, nullptr, nullptr, w,
-                   nsub, flux, comps, nullptr, W, nullptr};
+                   nsub, flux, comps, nullptr, W, nullptr, nullptr, nullptr, nullptr, false, nullptr,
+                   nullptr, nullptr, nullptr, 0, 0, 0ull, 0ull, nullptr};
         hipLaunchKernelGGL(k_lnlike<0>, dim3(W), dim3(LIKE_THREADS), 0, st, L);
         if ((rc = launch_ok())) return rc;
     }
@@ -1349,10 +1482,19 @@ int lfg_flux(const double* pars, int W, int P, const double* x, const double* w,
     return LFG_OK;
 }
 
+struct Accept {  // fused stretch-move acceptance of lfg_stretch_lnprob_accept
+    double* pos;
+    double* lnp;
+    const double* zfac;
+    int half;
+    unsigned long long seed, step;
+    int* naccept;
+};
+
 static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* lnp, double* lnlike_e, void* wsp,
-                       size_t ws_bytes, void* stream, void* const* ev)
+                       size_t ws_bytes, void* stream, void* const* ev, const Accept* acc = nullptr)
 {
-    if (W <= 0 || !T || T->E <= 0 || T->ndim <= 0 || T->nsub < 1 || !walkers || !lnp) return LFG_E_ARGS;
+    if (W <= 0 || !T || T->E <= 0 || T->ndim <= 0 || T->nsub < 1 || !walkers || (!lnp && !acc)) return LFG_E_ARGS;
     Ws ws = carve(wsp, W, T->E);
     if (!wsp || ws_bytes < ws.total) return LFG_E_WORKSPACE;
     hipStream_t st = static_cast<hipStream_t>(stream);
@@ -1361,21 +1503,21 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
     };
     SetupArgs S{walkers, W, T->ndim, T->E, 18, T->gather, T->npars, T->consts, T->prior_type, T->prior_p1,
                 T->prior_p2, T->prior_norm, T->roche_priors, ws.geo, ws.status, ws.prior, ws.bstatus, T->gp,
-                T->gp_gather, T->gp_base};
+                T->gp_gather, T->gp_base, ws.done};
     const int npairs = W * T->E;
     int rc = run_front(S, ws, st, ev);
     if (rc) return rc;
     double* lle = lnlike_e ? lnlike_e : ws.lle;
     LikeArgs L{ws.geo, ws.status, ws.ab, ws.donor, ws.wts, T->E, T->off, T->max_n, T->x, T->y, T->ye,
-               T->w, T->nsub, nullptr, nullptr, lle, npairs, T->gp ? T->gp_ecl : nullptr};
+               T->w, T->nsub, nullptr, nullptr, lle, npairs, T->gp ? T->gp_ecl : nullptr, ws.prior, lnp, ws.done,
+               true, acc ? acc->pos : nullptr, acc ? acc->lnp : nullptr, walkers, acc ? acc->zfac : nullptr,
+               T->ndim, acc ? acc->half : 0, acc ? acc->seed : 0ull, acc ? acc->step : 0ull,
+               acc ? acc->naccept : nullptr};
     if (T->gp) hipLaunchKernelGGL(k_lnlike<2>, dim3(npairs), dim3(LIKE_THREADS), 0, st, L);
     else hipLaunchKernelGGL(k_lnlike<1>, dim3(npairs), dim3(LIKE_THREADS), 0, st, L);
     if ((rc = launch_ok())) return rc;
     mark(3);
-    hipLaunchKernelGGL(k_combine, dim3((W + 255) / 256), dim3(256), 0, st, W, T->E, ws.prior, ws.geo, lle, lnp);
-    rc = launch_ok();
-    mark(4);
-    return rc;
+    return LFG_OK;
 }
 
 int lfg_lnprior(const double* walkers, int W, const lfg_tree* T, double* lnprior, void* wsp, size_t ws_bytes,
@@ -1387,7 +1529,7 @@ int lfg_lnprior(const double* walkers, int W, const lfg_tree* T, double* lnprior
     hipStream_t st = static_cast<hipStream_t>(stream);
     SetupArgs S{walkers, W, T->ndim, T->E, 18, T->gather, T->npars, T->consts, T->prior_type, T->prior_p1,
                 T->prior_p2, T->prior_norm, T->roche_priors, ws.geo, ws.status, ws.prior, ws.bstatus, 0,
-                nullptr, nullptr};
+                nullptr, nullptr, nullptr};
     const int nlanes = 2 * W * T->E + W;
     hipLaunchKernelGGL(k_setup, dim3((nlanes + SETUP_BLOCK - 1) / SETUP_BLOCK), dim3(SETUP_BLOCK), 0, st, S);
     int rc = launch_ok();
@@ -1407,6 +1549,15 @@ int lfg_lnprob_timed(const double* walkers, int W, const lfg_tree* T, double* ln
                      size_t ws_bytes, void* stream, void* const* ev)
 {
     return lnprob_impl(walkers, W, T, lnp, lnlike_e, wsp, ws_bytes, stream, ev);
+}
+
+int lfg_stretch_lnprob_accept(double* pos, double* lnp, int W, int half, const double* q, const double* zfac,
+                              const lfg_tree* T, unsigned long long seed, unsigned long long step, int* naccept,
+                              double* lnp_new, void* wsp, size_t ws_bytes, void* stream, void* const* ev)
+{
+    if (W < 4 || (W & 1) || (half != 0 && half != 1) || !pos || !lnp || !q || !zfac || !T) return LFG_E_ARGS;
+    const Accept acc{pos, lnp, zfac, half, seed, step, naccept};
+    return lnprob_impl(q, W / 2, T, lnp_new, nullptr, wsp, ws_bytes, stream, ev, &acc);
 }
 
 static int propose_impl(const double* pos, int W, int ndim, int half, double a, unsigned long long seed,
@@ -1491,7 +1642,7 @@ int lfg_elements(const double* pars, int W, int P, double* a, double* b, double*
     if (!wsp || ws_bytes < ws.total) return LFG_E_WORKSPACE;
     hipStream_t st = static_cast<hipStream_t>(stream);
     SetupArgs S{pars, W, P, 1, P, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
-                ws.geo, ws.status, ws.prior, ws.bstatus, 0, nullptr, nullptr};
+                ws.geo, ws.status, ws.prior, ws.bstatus, 0, nullptr, nullptr, nullptr};
     int rc = run_front(S, ws, st, nullptr);
     if (rc) return rc;
     if (a || b || wgt || donor) {

@@ -122,6 +122,35 @@ def test_device_mcmc_runs():
     np.testing.assert_allclose(again, S.lnprob_chain[-1].cpu().numpy(), rtol=1e-12)
 
 
+def test_fused_lnprob_accept_matches_separate_kernels():
+    """lfg_stretch_lnprob_accept (the default single-process path) gives the
+    chain of lfg_lnprob + lfg_stretch_accept, bit for bit, across reset()."""
+    import torch
+    from lfit_python_amd import batch, sampler, synthetic
+    out = []
+    for cfg in ("c2", "c3"):
+        if cfg == "c2":
+            m = synthetic.config_single(300, flux_fn=_flux_fn)
+        else:
+            m = synthetic.config_tree(2, 200, flux_fn=_flux_fn)   # E = 6: the last-eclipse counter path
+        t = batch.compile_tree(m)
+        ev = batch.LnProbEvaluator(t)
+        p0 = np.array(m.dynasty_par_vals)
+        W = 64 if cfg == "c2" else 2 * len(p0) + 2
+        init = sampler.initialise_walkers(p0, sampler.comp_scatter(m.dynasty_par_names, 0.1), W,
+                                          lambda p: ev(torch.as_tensor(p, device="cuda")).cpu().numpy())
+        res = []
+        for fuse in (False, True):
+            S = sampler.EnsembleSampler(W, t.ndim, ev, seed=21)
+            S.fuse = fuse
+            S.run_mcmc(init, 4)
+            S.reset()
+            S.run_mcmc(None, 3)
+            res.append((S.chain.cpu().numpy(), S.lnprob_chain.cpu().numpy(), S.naccept.cpu().numpy()))
+        for a, b in zip(res[0], res[1]):
+            np.testing.assert_array_equal(a, b)
+
+
 def test_graph_replay_matches_eager():
     """HIP-graph replay of whole iterations (device step counter) gives the
     bit-identical chain of the eager path, including across reset()."""
