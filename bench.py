@@ -5,9 +5,10 @@ spot, 300-point phase grid; config 2 = 1024 walkers per GPU).
 
 A step is one emcee iteration of the whole ensemble: two half-steps of
 propose -> batched ln_prob of the proposals (k_setup, k_elements, k_lnlike)
--> accept.  On one GPU the acceptance is fused into k_lnlike
-(lfg_stretch_lnprob_accept); with N ranks each evaluates its shard
-(lfg_lnprob), all_gathers ln_prob, and every rank accepts.  value = walkers x steps /
+-> accept.  On one GPU a half-step is those three kernels alone
+(lfg_stretch_step_half: the proposal formed in k_setup, the acceptance in
+k_lnlike); with N ranks each proposes, evaluates its shard (lfg_lnprob),
+all_gathers ln_prob, and every rank accepts.  value = walkers x steps /
 time, max over ranks, inputs resident in HBM.  Per-GPU work is fixed (weak
 scaling): --walkers per GPU, total = walkers x N.
 
@@ -156,17 +157,17 @@ def main():
         _native.check(rc, "lfg_lnprob_timed")
         return out
 
-    def timed_accept(q, pos, lnp, half, zfac, seed, step, naccept, lnp_new=None):
-        """the single-process path: lfg_stretch_lnprob_accept with the events"""
+    def timed_half(pos, lnp, half, a, seed, step, q, zfac, naccept, lnp_new=None):
+        """the single-process path: lfg_stretch_step_half with the events"""
         evs = None
         if sampled():
             evs = make_evs()
             events.append((evs, q.shape[0]))
-        ev.lnprob_accept(q, pos, lnp, half, zfac, seed, step, naccept, lnp_new=lnp_new, events=evs)
+        ev.step_half(pos, lnp, half, a, seed, step, q, zfac, naccept, lnp_new=lnp_new, events=evs)
 
     def set_timing(on):
         if world == 1:
-            S.accept_timer = timed_accept if on else None
+            S.half_timer = timed_half if on else None
         else:
             S.timer = timed_eval if on else None
 

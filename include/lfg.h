@@ -196,6 +196,20 @@ int lfg_stretch_lnprob_accept(double* pos, double* lnp, int W, int half,
                               void* stream, void* const* ev);
 
 /*
+ * A whole half-step of the stretch move in three kernels: the proposals of
+ * half `half` are formed inside k_setup (k_propose's arithmetic and draws;
+ * written to q / zfac), their ln_prob evaluated, and the Metropolis step
+ * fused as in lfg_stretch_lnprob_accept.  Same chain as lfg_stretch_propose
+ * + lfg_lnprob + lfg_stretch_accept.  q [dev] W/2 x ndim, zfac [dev] W/2
+ * (outputs); the rest as lfg_stretch_lnprob_accept.  Single process only.
+ */
+int lfg_stretch_step_half(double* pos, double* lnp, int W, int half, double a,
+                          unsigned long long seed, unsigned long long step,
+                          double* q, double* zfac, const lfg_tree* tree,
+                          int* naccept, double* lnp_new, void* ws,
+                          size_t ws_bytes, void* stream, void* const* ev);
+
+/*
  * The same two moves with the step counter read from device memory
  * (step_dev [dev] 1 x uint64), so that one emcee iteration can be captured
  * in a HIP graph and replayed; the caller advances *step_dev after half 1.

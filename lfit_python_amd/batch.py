@@ -213,6 +213,17 @@ class LnProbEvaluator:
                                               _native.stream_ptr(self.device), events)
         _native.check(rc, "lfg_stretch_lnprob_accept")
 
+    def step_half(self, pos, lnp, half, a, seed, step, q, zfac, naccept, lnp_new=None, events=None):
+        """A whole stretch-move half-step (lfg_stretch_step_half): propose half
+        `half` into q / zfac, evaluate, accept; pos, lnp, naccept in place."""
+        W = pos.shape[0]
+        self._ensure(W // 2)
+        vp = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
+        rc = self.L.lfg_stretch_step_half(vp(pos), vp(lnp), W, half, a, seed, step, vp(q), vp(zfac),
+                                          ctypes.byref(self.ctree), vp(naccept), vp(lnp_new), vp(self._ws),
+                                          self._ws.numel(), _native.stream_ptr(self.device), events)
+        _native.check(rc, "lfg_stretch_step_half")
+
     def ln_prior(self, walkers, out=None):
         """ln_prior alone (mcmcfit.ln_prior, mcmcfit.py:30-34) of walkers [W, ndim]."""
         import torch

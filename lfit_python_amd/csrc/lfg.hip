@@ -72,6 +72,10 @@ Ws carve(void* base, int W, int E)
     return ws;
 }
 
+// Philox draws of the stretch move (defined with k_propose below)
+__device__ inline uint4 draw(unsigned long long seed, unsigned long long step, int half, int purpose, int i);
+__device__ inline double u53(unsigned a, unsigned b);
+
 // ---------------------------------------------------------------- k_setup
 struct SetupArgs {
     const double* walkers;
@@ -92,11 +96,41 @@ struct SetupArgs {
     const int* gp_gather;
     const double* gp_base;
     int* done;     // nullable: per-walker eclipse counters of k_lnlike, zeroed here
+    // inline stretch-move proposal (lfg_stretch_step_half; pos nullptr: off):
+    // walker w of the batch is the proposal for ensemble walker half * W + w,
+    // formed from pos as k_propose does; the walker lanes store it in qout
+    const double* pos;
+    double a;
+    unsigned long long seed, step;
+    int half;
+    double* qout;
+    double* zfout;
 };
 
-__device__ inline double gather_par(const SetupArgs& A, int w, int g)
+// where a lane reads walker w's parameters: the walker row, or the
+// stretch-move proposal s + z (c_j - s) ... written as k_propose writes it
+struct Prop {
+    const double* s;
+    const double* cj;
+    double z;
+};
+
+__device__ inline Prop make_prop(const SetupArgs& A, int w)
 {
-    return g >= 0 ? A.walkers[size_t(w) * A.ndim + g] : A.consts[-1 - g];
+    if (!A.pos) return Prop{A.walkers + size_t(w) * A.ndim, nullptr, 0.0};
+    const int ns = A.W;  // the batch is half the ensemble
+    const uint4 r = draw(A.seed, A.step, A.half, 0, w);
+    const double u = u53(r.x, r.y);
+    const double zr = (A.a - 1.0) * u + 1.0;
+    const int j = int(__umulhi(r.z, unsigned(ns)));
+    return Prop{A.pos + size_t(A.half * ns + w) * A.ndim, A.pos + size_t((1 - A.half) * ns + j) * A.ndim,
+                zr * zr / A.a};
+}
+
+__device__ __forceinline__ double gather_par(const SetupArgs& A, const Prop& P, int g)
+{
+    if (g < 0) return A.consts[-1 - g];
+    return P.cj ? fma(P.s[g] - P.cj[g], P.z, P.cj[g]) : P.s[g];
 }
 
 // ------------------------------------------------------- stream lanes of k_setup
@@ -109,9 +143,10 @@ __device__ inline void bspot_lane(const SetupArgs& A, int t)
 {
     const int* gat = A.gather ? A.gather : kIdentityGather;
     const int w = t / A.E, e = t - w * A.E;
-    const double q = gather_par(A, w, gat[e * 18 + 4]);
-    const double rdisc = gather_par(A, w, gat[e * 18 + 6]);
-    const double az = gather_par(A, w, gat[e * 18 + 10]);
+    const Prop P = make_prop(A, w);
+    const double q = gather_par(A, P, gat[e * 18 + 4]);
+    const double rdisc = gather_par(A, P, gat[e * 18 + 6]);
+    const double az = gather_par(A, P, gat[e * 18 + 10]);
     double* G = A.geo + size_t(t) * LFG_NGEO;
 #ifdef LFG_PROFILE_SETUP
     const unsigned long long tp0 = __builtin_amdgcn_s_memtime();
@@ -153,19 +188,25 @@ __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
         // per-walker lane: LCModel.ln_prior dphi check (CVModel.py:452-473)
         // and Node.ln_prior over the variable parameters (model.py:439-449)
         const int w = t - npairs;
+        const Prop P = make_prop(A, w);
+        if (A.pos) {  // store the proposal: k_lnlike copies an accepted one into pos
+            double* qo = A.qout + size_t(w) * A.ndim;
+            for (int d = 0; d < A.ndim; ++d) qo[d] = gather_par(A, P, d);
+            A.zfout[w] = (A.ndim - 1.0) * log(P.z);
+        }
         double lp = 0.0;
         if (A.roche_priors) {
-            const double q = gather_par(A, w, gat[4]);
-            const double dphi = gather_par(A, w, gat[5]);
+            const double q = gather_par(A, P, gat[4]);
+            const double dphi = gather_par(A, P, gat[5]);
             Roche R;
             double maxphi;
             if (roche_init(R, q) != ST_OK || findphi_fast(R, 90.0, maxphi) != ST_OK) lp = -INFINITY;
             else if (dphi > maxphi - DPHI_TOL) lp = -INFINITY;
         }
         if (A.prior_type) {
-            const double* v = A.walkers + size_t(w) * A.ndim;
             for (int d = 0; d < A.ndim && isfinite(lp); ++d)
-                lp += prior_lnprob(A.prior_type[d], A.prior_p1[d], A.prior_p2[d], A.prior_norm[d], v[d]);
+                lp += prior_lnprob(A.prior_type[d], A.prior_p1[d], A.prior_p2[d], A.prior_norm[d],
+                                   gather_par(A, P, d));
         }
         A.prior[w] = lp;
         if (A.done) A.done[w] = 0;
@@ -173,11 +214,12 @@ __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
     }
 
     const int w = t / A.E, e = t - (t / A.E) * A.E;
+    const Prop P = make_prop(A, w);
     const int np = A.npars ? A.npars[e] : A.P;
     double p[18];
     bool finite = (np == 14 || np == 18);
     for (int k = 0; k < 18; ++k) {
-        p[k] = (k < np) ? gather_par(A, w, gat[e * 18 + k]) : 0.0;
+        p[k] = (k < np) ? gather_par(A, P, gat[e * 18 + k]) : 0.0;
         finite = finite && isfinite(p[k]);
     }
     if (np == 14) { p[14] = 2.0; p[15] = 1.0; p[16] = 90.0; p[17] = 0.0; }  // MODEL_SPEC 5.3
@@ -261,8 +303,8 @@ __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
         // amplitudes exp(ln_amp), metric exp(ln_tau); the changepoint
         // distance from the cache unless q, dphi or rwd moved > 120 %
         const int* gg = A.gp_gather + e * 3;
-        const double ain = exp(gather_par(A, w, gg[0])), aout = exp(gather_par(A, w, gg[1]));
-        const double tau = exp(gather_par(A, w, gg[2]));
+        const double ain = exp(gather_par(A, P, gg[0])), aout = exp(gather_par(A, P, gg[1]));
+        const double tau = exp(gather_par(A, P, gg[2]));
         const double* B = A.gp_base + e * 4;
         const double q = p[4], dphi = p[5], rwd = p[8];
         double dcp = B[3];
@@ -550,8 +592,7 @@ struct LikeArgs {
     int* naccept;
 };
 
-__device__ inline uint4 draw(unsigned long long seed, unsigned long long step, int half, int purpose, int i);
-__device__ inline double u53(unsigned a, unsigned b);
+
 
 // ln_prob of walker w once all its eclipses' ln_like are in lle
 // (Node.ln_prob, model.py:476-498; what k_combine does), then the
@@ -1319,7 +1360,7 @@ __global__ void k_propose(const double* __restrict__ pos, int W, int ndim, int h
     const double* s = pos + size_t(half * ns + i) * ndim;
     const double* cj = pos + size_t((1 - half) * ns + j) * ndim;
     double* out = q + size_t(i) * ndim;
-    for (int d = 0; d < ndim; ++d) out[d] = cj[d] - (cj[d] - s[d]) * z;
+    for (int d = 0; d < ndim; ++d) out[d] = fma(s[d] - cj[d], z, cj[d]);  // c_j + z (s - c_j), as make_prop
     zfac[i] = (ndim - 1.0) * log(z);
 }
 
@@ -1491,8 +1532,16 @@ struct Accept {  // fused stretch-move acceptance of lfg_stretch_lnprob_accept
     int* naccept;
 };
 
+struct Propose {  // inline proposal of lfg_stretch_step_half
+    const double* pos;
+    double a;
+    double* q;
+    double* zfac;
+};
+
 static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* lnp, double* lnlike_e, void* wsp,
-                       size_t ws_bytes, void* stream, void* const* ev, const Accept* acc = nullptr)
+                       size_t ws_bytes, void* stream, void* const* ev, const Accept* acc = nullptr,
+                       const Propose* prop = nullptr)
 {
     if (W <= 0 || !T || T->E <= 0 || T->ndim <= 0 || T->nsub < 1 || !walkers || (!lnp && !acc)) return LFG_E_ARGS;
     Ws ws = carve(wsp, W, T->E);
@@ -1504,6 +1553,15 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
     SetupArgs S{walkers, W, T->ndim, T->E, 18, T->gather, T->npars, T->consts, T->prior_type, T->prior_p1,
                 T->prior_p2, T->prior_norm, T->roche_priors, ws.geo, ws.status, ws.prior, ws.bstatus, T->gp,
                 T->gp_gather, T->gp_base, ws.done};
+    if (prop) {
+        S.pos = prop->pos;
+        S.a = prop->a;
+        S.seed = acc->seed;
+        S.step = acc->step;
+        S.half = acc->half;
+        S.qout = prop->q;
+        S.zfout = prop->zfac;
+    }
     const int npairs = W * T->E;
     int rc = run_front(S, ws, st, ev);
     if (rc) return rc;
@@ -1549,6 +1607,17 @@ int lfg_lnprob_timed(const double* walkers, int W, const lfg_tree* T, double* ln
                      size_t ws_bytes, void* stream, void* const* ev)
 {
     return lnprob_impl(walkers, W, T, lnp, lnlike_e, wsp, ws_bytes, stream, ev);
+}
+
+int lfg_stretch_step_half(double* pos, double* lnp, int W, int half, double a, unsigned long long seed,
+                          unsigned long long step, double* q, double* zfac, const lfg_tree* T, int* naccept,
+                          double* lnp_new, void* wsp, size_t ws_bytes, void* stream, void* const* ev)
+{
+    if (W < 4 || (W & 1) || (half != 0 && half != 1) || !(a > 1.0) || !pos || !lnp || !q || !zfac || !T)
+        return LFG_E_ARGS;
+    const Accept acc{pos, lnp, zfac, half, seed, step, naccept};
+    const Propose prop{pos, a, q, zfac};
+    return lnprob_impl(q, W / 2, T, lnp_new, nullptr, wsp, ws_bytes, stream, ev, &acc, &prop);
 }
 
 int lfg_stretch_lnprob_accept(double* pos, double* lnp, int W, int half, const double* q, const double* zfac,

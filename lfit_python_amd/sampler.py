@@ -111,11 +111,11 @@ class EnsembleSampler:
         self.chain = None
         self.lnprob_chain = None
         self.timer = None  # optional callable(walkers) -> lnp used instead of self.ev
-        # one process, HIP moves, an evaluator with the fused entry: ln_prob and
-        # acceptance in one launch sequence (lfg_stretch_lnprob_accept); the
-        # optional accept_timer replaces evaluator.lnprob_accept (bench timing)
-        self.fuse = hasattr(evaluator, "lnprob_accept") and isinstance(self.ops, HipStretchOps)
-        self.accept_timer = None
+        # one process, HIP moves, an evaluator with the fused entry: proposal,
+        # ln_prob and acceptance in one launch sequence (lfg_stretch_step_half);
+        # the optional half_timer replaces evaluator.step_half (bench timing)
+        self.fuse = hasattr(evaluator, "step_half") and isinstance(self.ops, HipStretchOps)
+        self.half_timer = None
         # HIP-graph replay of whole iterations (single rank, HIP ops): the first
         # step() after enabling runs eagerly, the next captures, later ones replay
         self.use_graph = False
@@ -210,12 +210,12 @@ class EnsembleSampler:
             return
         self._warm = True
         for half in (0, 1):
-            self.ops.propose(self.pos, half, self.a, self.seed, self.iteration, self.q, self.zfac)
             if self.world == 1 and self.fuse and self.timer is None:
-                f = self.accept_timer or self.ev.lnprob_accept
-                f(self.q, self.pos, self.lnp, half, self.zfac, self.seed, self.iteration, self.naccept,
+                f = self.half_timer or self.ev.step_half
+                f(self.pos, self.lnp, half, self.a, self.seed, self.iteration, self.q, self.zfac, self.naccept,
                   lnp_new=self.lnp_new)
                 continue
+            self.ops.propose(self.pos, half, self.a, self.seed, self.iteration, self.q, self.zfac)
             if self.world == 1:
                 self._eval(self.q, self.lnp_new)
             else:

@@ -122,9 +122,11 @@ def test_device_mcmc_runs():
     np.testing.assert_allclose(again, S.lnprob_chain[-1].cpu().numpy(), rtol=1e-12)
 
 
-def test_fused_lnprob_accept_matches_separate_kernels():
-    """lfg_stretch_lnprob_accept (the default single-process path) gives the
-    chain of lfg_lnprob + lfg_stretch_accept, bit for bit, across reset()."""
+def test_fused_half_step_matches_separate_kernels():
+    """lfg_stretch_step_half (the default single-process path: proposal in
+    k_setup, acceptance in k_lnlike) gives the chain of lfg_stretch_propose +
+    lfg_lnprob + lfg_stretch_accept, bit for bit, across reset(); and so does
+    lfg_stretch_lnprob_accept."""
     import torch
     from lfit_python_amd import batch, sampler, synthetic
     out = []
@@ -140,15 +142,21 @@ def test_fused_lnprob_accept_matches_separate_kernels():
         init = sampler.initialise_walkers(p0, sampler.comp_scatter(m.dynasty_par_names, 0.1), W,
                                           lambda p: ev(torch.as_tensor(p, device="cuda")).cpu().numpy())
         res = []
-        for fuse in (False, True):
+        for mode in ("separate", "step_half", "lnprob_accept"):
             S = sampler.EnsembleSampler(W, t.ndim, ev, seed=21)
-            S.fuse = fuse
+            S.fuse = mode != "separate"
+            if mode == "lnprob_accept":
+                def half(pos, lnp, h, a, seed, step, q, zfac, naccept, lnp_new=None, S=S, ev=ev):
+                    S.ops.propose(pos, h, a, seed, step, q, zfac)
+                    ev.lnprob_accept(q, pos, lnp, h, zfac, seed, step, naccept, lnp_new=lnp_new)
+                S.half_timer = half
             S.run_mcmc(init, 4)
             S.reset()
             S.run_mcmc(None, 3)
             res.append((S.chain.cpu().numpy(), S.lnprob_chain.cpu().numpy(), S.naccept.cpu().numpy()))
-        for a, b in zip(res[0], res[1]):
-            np.testing.assert_array_equal(a, b)
+        for other in res[1:]:
+            for a, b in zip(res[0], other):
+                np.testing.assert_array_equal(a, b)
 
 
 def test_graph_replay_matches_eager():
