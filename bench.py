@@ -59,16 +59,26 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--walkers", type=int, default=1024, help="walkers per GPU")
-    ap.add_argument("--npts", type=int, default=300)
-    ap.add_argument("--nsub", type=int, default=1)
+    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 5),
+                    help="BASELINE.json config: 2 (the metric's, default), 3 (3-band x 4-eclipse tree, "
+                         "2048 walkers), 5 (10000 points x 5 sub-samples, 4096 walkers)")
+    ap.add_argument("--walkers", type=int, default=None, help="walkers per GPU (default: the config's)")
+    ap.add_argument("--npts", type=int, default=None)
+    ap.add_argument("--nsub", type=int, default=None)
+    ap.add_argument("--shard-path", action="store_true",
+                    help="run the multi-rank half-step (lfg_stretch_step_shard + accept_regen) on one rank")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--seed", type=int, default=20261015)
     ap.add_argument("--time-every", type=int, default=4,
                     help="record the dominant kernel's event pair on every k-th ln_prob call of the timed region")
-    return ap.parse_args()
+    args = ap.parse_args()
+    dflt = {2: (1024, 300, 1), 3: (2048, 300, 1), 5: (4096, 10000, 5)}[args.config]
+    args.walkers = args.walkers or dflt[0]
+    args.npts = args.npts or dflt[1]
+    args.nsub = args.nsub or dflt[2]
+    return args
 
 
 def algo_bytes(kernel, pairs, walkers, ndim, E, npts):
@@ -114,7 +124,10 @@ def main():
         assert int(st[0].item()) == 0
         return f[0].cpu().numpy()
 
-    model = synthetic.config_single(npts=args.npts, flux_fn=flux_fn, nsub=args.nsub)
+    if args.config == 3:
+        model = synthetic.config_tree(4, args.npts, flux_fn=flux_fn, nsub=args.nsub)
+    else:
+        model = synthetic.config_single(npts=args.npts, flux_fn=flux_fn, nsub=args.nsub)
     tree = batch.compile_tree(model, nsub=args.nsub)
     ev = batch.LnProbEvaluator(tree, device=dev, max_walkers=args.walkers * world)
     W = args.walkers * world
@@ -123,6 +136,7 @@ def main():
     init = sampler.initialise_walkers(
         p0, scat, W, lambda p: ev(torch.as_tensor(p, device=dev)).cpu().numpy(), seed=args.seed)
     S = sampler.EnsembleSampler(W, tree.ndim, ev, seed=args.seed)
+    S.force_shard = args.shard_path
     S.set_state(init)
 
     # HIP events around kernels of lfg_lnprob calls (include/lfg.h LFG_NEV)
@@ -144,19 +158,6 @@ def main():
                 evs[i] = h.value
         return evs
 
-    def timed_eval(x, out=None):
-        if out is None:
-            out = torch.empty(x.shape[0], dtype=torch.float64, device=dev)
-        evs = None
-        if sampled():
-            evs = make_evs()
-            events.append((evs, x.shape[0]))
-        rc = L.lfg_lnprob_timed(ctypes.c_void_p(x.data_ptr()), x.shape[0], ctypes.byref(ev.ctree),
-                                ctypes.c_void_p(out.data_ptr()), None, ctypes.c_void_p(ev._ws.data_ptr()),
-                                ev._ws.numel(), _native.stream_ptr(dev), evs)
-        _native.check(rc, "lfg_lnprob_timed")
-        return out
-
     def timed_half(pos, lnp, half, a, seed, step, q, zfac, naccept, lnp_new=None):
         """the single-process path: lfg_stretch_step_half with the events"""
         evs = None
@@ -165,11 +166,19 @@ def main():
             events.append((evs, q.shape[0]))
         ev.step_half(pos, lnp, half, a, seed, step, q, zfac, naccept, lnp_new=lnp_new, events=evs)
 
+    def timed_shard(pos, half, a, seed, step, lo, q, zfac, lnp_sh):
+        """the multi-rank path: this rank's lfg_stretch_step_shard with the events"""
+        evs = None
+        if sampled():
+            evs = make_evs()
+            events.append((evs, lnp_sh.shape[0]))
+        ev.step_shard(pos, half, a, seed, step, lo, q, zfac, lnp_sh, events=evs)
+
     def set_timing(on):
-        if world == 1:
+        if world == 1 and not args.shard_path:
             S.half_timer = timed_half if on else None
         else:
-            S.timer = timed_eval if on else None
+            S.shard_timer = timed_shard if on else None
 
     def kernel_ms(kernels):
         """mean ms per launch of each (name, a, b) over the recorded calls; frees the events"""
@@ -267,9 +276,10 @@ def main():
             "dtype": "f64",
             "data": "synthetic light curve (model at mcmc_input.dat eclipse-0 truth + N(0, 0.004)); "
                     "walkers from the comp_scat ball of mcmcfit.py",
-            "config": {"workload": "config 2: single eclipse, complex 18-par bright spot, "
+            "config": {"workload": "config %d: %s, complex 18-par bright spot, "
                                    "%d phase pts, nsub %d, %d walkers/GPU, emcee stretch move"
-                                   % (args.npts, args.nsub, args.walkers),
+                                   % (args.config, "3-band x 4-eclipse tree" if args.config == 3
+                                      else "single eclipse", args.npts, args.nsub, args.walkers),
                        "walkers_total": W, "eclipses": E, "ndim": tree.ndim,
                        "parallelism": "walker shards x%d, replicated Philox RNG, "
                                       "all_gather of ln_prob per half-step" % world,

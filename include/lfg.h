@@ -210,6 +210,29 @@ int lfg_stretch_step_half(double* pos, double* lnp, int W, int half, double a,
                           size_t ws_bytes, void* stream, void* const* ev);
 
 /*
+ * The half-step of one rank when the walkers of each half are sharded over
+ * ranks (the replacement of the reference's pool.map over walkers,
+ * mcmcfit.py:273-288).  lfg_stretch_step_shard forms the proposals of
+ * walkers lo .. lo+n-1 of half `half` inside k_setup (same draws as
+ * lfg_stretch_propose's lanes lo .. lo+n-1) and writes their ln_prob to
+ * lnp_new [dev] n; q [dev] n x ndim and zfac [dev] n receive the proposals.
+ * After the caller has gathered every rank's lnp_new into the W/2 vector,
+ * lfg_stretch_accept_regen applies the Metropolis step to the whole half,
+ * re-forming each proposal from its draws (bit-identical to k_propose), so
+ * no rank needs another rank's q.  Three kernels + collective + one kernel
+ * per half-step; the chain equals lfg_stretch_step_half's.
+ */
+int lfg_stretch_step_shard(const double* pos, int W, int half, double a,
+                           unsigned long long seed, unsigned long long step,
+                           int lo, int n, double* q, double* zfac,
+                           const lfg_tree* tree, double* lnp_new, void* ws,
+                           size_t ws_bytes, void* stream, void* const* ev);
+int lfg_stretch_accept_regen(double* pos, double* lnp, int W, int ndim,
+                             int half, double a, unsigned long long seed,
+                             unsigned long long step, const double* lnp_new,
+                             int* naccept, void* stream);
+
+/*
  * The same two moves with the step counter read from device memory
  * (step_dev [dev] 1 x uint64), so that one emcee iteration can be captured
  * in a HIP graph and replayed; the caller advances *step_dev after half 1.

@@ -224,6 +224,18 @@ class LnProbEvaluator:
                                           self._ws.numel(), _native.stream_ptr(self.device), events)
         _native.check(rc, "lfg_stretch_step_half")
 
+    def step_shard(self, pos, half, a, seed, step, lo, q, zfac, lnp_new, events=None):
+        """This rank's part of a sharded half-step (lfg_stretch_step_shard):
+        the proposals of walkers lo .. lo + n - 1 of half `half` (n =
+        lnp_new.numel()) into q / zfac and their ln_prob into lnp_new."""
+        W, n = pos.shape[0], lnp_new.shape[0]
+        self._ensure(n)
+        vp = lambda t: ctypes.c_void_p(t.data_ptr())
+        rc = self.L.lfg_stretch_step_shard(vp(pos), W, half, a, seed, step, lo, n, vp(q), vp(zfac),
+                                           ctypes.byref(self.ctree), vp(lnp_new), vp(self._ws), self._ws.numel(),
+                                           _native.stream_ptr(self.device), events)
+        _native.check(rc, "lfg_stretch_step_shard")
+
     def ln_prior(self, walkers, out=None):
         """ln_prior alone (mcmcfit.ln_prior, mcmcfit.py:30-34) of walkers [W, ndim]."""
         import torch

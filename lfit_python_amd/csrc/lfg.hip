@@ -27,6 +27,9 @@ namespace {
 
 constexpr int SETUP_BLOCK = 64;
 constexpr int ELEM_BLOCK = 256;
+#ifndef ELEM_MINW
+#define ELEM_MINW 1  // minimum waves per SIMD of k_elements
+#endif
 // per-pair weight block written by k_elements: disc ring weights, the disc
 // total 2 pi [P(rdisc) - P(rin)], spot element weights
 constexpr int WT_DISC = 0, WT_TD = NDISC_R, WT_BS = 24, WT_N = WT_BS + NBS;
@@ -105,6 +108,9 @@ struct SetupArgs {
     int half;
     double* qout;
     double* zfout;
+    // the batch is walkers lo .. lo + W - 1 of the ns-walker half (ns = W,
+    // lo = 0 on one process; a rank's shard with lfg_stretch_step_shard)
+    int lo, ns;
 };
 
 // where a lane reads walker w's parameters: the walker row, or the
@@ -118,12 +124,12 @@ struct Prop {
 __device__ inline Prop make_prop(const SetupArgs& A, int w)
 {
     if (!A.pos) return Prop{A.walkers + size_t(w) * A.ndim, nullptr, 0.0};
-    const int ns = A.W;  // the batch is half the ensemble
-    const uint4 r = draw(A.seed, A.step, A.half, 0, w);
+    const int ns = A.ns, i = A.lo + w;  // walker i of the half, as k_propose's lane i
+    const uint4 r = draw(A.seed, A.step, A.half, 0, i);
     const double u = u53(r.x, r.y);
     const double zr = (A.a - 1.0) * u + 1.0;
     const int j = int(__umulhi(r.z, unsigned(ns)));
-    return Prop{A.pos + size_t(A.half * ns + w) * A.ndim, A.pos + size_t((1 - A.half) * ns + j) * A.ndim,
+    return Prop{A.pos + size_t(A.half * ns + i) * A.ndim, A.pos + size_t((1 - A.half) * ns + j) * A.ndim,
                 zr * zr / A.a};
 }
 
@@ -214,6 +220,9 @@ __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
     }
 
     const int w = t / A.E, e = t - (t / A.E) * A.E;
+#ifdef LFG_PROFILE_SETUP
+    const unsigned long long tlane = __builtin_amdgcn_s_memtime();
+#endif
     const Prop P = make_prop(A, w);
     const int np = A.npars ? A.npars[e] : A.P;
     double p[18];
@@ -258,7 +267,7 @@ __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
         const unsigned long long tb = __builtin_amdgcn_s_memtime();
         const double um = bs_umax(p[14], p[15], p[14] * log(pow(p[14] / p[15], 1.0 / p[15])) - p[14] / p[15]);
         const unsigned long long tc2 = __builtin_amdgcn_s_memtime();
-        G[42] = double(tp1 - tp0);
+        G[42] = double(tp0 - tlane);
         G[44] = double(tp3 - tp2);
         G[45] = double(tb - ta);
         G[46] = double(tc2 - tb) + 0.0 * um;
@@ -320,6 +329,9 @@ __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
         G[G_GP_DCP] = dcp;
         G[G_GP_OK] = (ok && tau > 0.0 && isfinite(ain) && isfinite(aout)) ? 1.0 : 0.0;
     }
+#ifdef LFG_PROFILE_SETUP
+    G[47] = double(__builtin_amdgcn_s_memtime() - tlane);
+#endif
 }
 
 // ------------------------------------------------------------- k_elements
@@ -370,7 +382,7 @@ __device__ inline double bs_weight(int j, const double* G)
     return exp(G[G_EXP1] * log(uk) - pow(uk, G[G_EXP2]) - G[G_LNPK]);
 }
 
-__global__ __launch_bounds__(ELEM_BLOCK) void k_elements(const double* __restrict__ geo, int* status, int npairs,
+__global__ __launch_bounds__(ELEM_BLOCK, ELEM_MINW) void k_elements(const double* __restrict__ geo, int* status, int npairs,
                                                          double2* __restrict__ AB, double* __restrict__ DON,
                                                          double* __restrict__ WT, const int* __restrict__ bstatus)
 {
@@ -635,8 +647,8 @@ __device__ inline void combine_walker(const LikeArgs& L, int w)
 // eclipse per walker and fused acceptance, thread 0 decides with the
 // prefetched draw and the copy of the accepted proposal is spread over the
 // first ndim lanes; otherwise thread 0 runs combine_after
-__device__ inline void finish_walker(const LikeArgs& L, int pair, int tid, bool acc1, double aq, double alu,
-                                     double azf, double alo, int* sflag);
+__device__ inline void finish_walker(const LikeArgs& L, int pair, int tid, bool acc1, double aq,
+                                     const double* sacc1, int* sflag);
 
 __device__ inline void combine_after(const LikeArgs& L, int pair)
 {
@@ -665,6 +677,9 @@ __device__ inline void combine_after(const LikeArgs& L, int pair)
 // w |[a,b] n [lo,hi]| / (hi - lo) directly.  Sums are 2^-61 fixed point in
 // int64 so LDS atomics add them exactly, independent of order.
 constexpr int LIKE_THREADS = 512;
+#ifndef LIKE_MINW
+#define LIKE_MINW 2  // minimum waves per SIMD (4: two blocks per CU, <= 128 VGPRs)
+#endif
 constexpr int LIKE_TILE = LIKE_THREADS;  // one point per thread per tile
 constexpr int LIKE_NC = 2 * LIKE_TILE;   // cells of the phase index
 constexpr double FX_SCALE = 2305843009213693952.0;  // 2^61
@@ -835,6 +850,17 @@ __device__ __forceinline__ void apply_runs(const Runs& R, double a, double b, do
 // (their runs start at different points: fewer same-address LDS atomics)
 __device__ __forceinline__ int sweep_item(int g) { return g < NWD + NDISC ? (g * 37) % (NWD + NDISC) : g; }
 
+// ring of WD/disc element k: WD ring r holds 4 r^2 <= k < 4 (r + 1)^2, disc
+// rings follow (NDISC_AZ elements each)
+__device__ __forceinline__ int sweep_ring(int k)
+{
+    if (k >= NWD) return NWD_RINGS + (k - NWD) / NDISC_AZ;
+    int r = int(sqrtf(float(k) * 0.25f));
+    r += (4 * (r + 1) * (r + 1) <= k) ? 1 : 0;
+    r -= (4 * r * r > k) ? 1 : 0;
+    return r;
+}
+
 __device__ __forceinline__ long long wave_scan_incl(long long v, int lane)
 {
     for (int off = 1; off < 64; off <<= 1) {
@@ -891,14 +917,17 @@ __device__ __forceinline__ int check_sorted(const TileBufs& T, int tid, bool own
 // spot element (lane < NBS) and donor tile (last NDONOR lanes) contributions
 // of one sub-bin pass into acc[0] (spot eclipse) and acc[1..3] (donor sum v)
 __device__ __forceinline__ void sweep_spot_donor(int tid, const PhaseIndex& XW, const TileBufs& TW,
-                                                 const PhaseIndex& XP, double2 abB, double wB,
-                                                 const double* dq, double ivs,
+                                                 const PhaseIndex& XP, const double2* sab, const double* sbw,
+                                                 double itb, const double* sdq, double ivs,
                                                  unsigned long long (*acc)[LIKE_TILE + 1])
 {
     if (tid < NBS) {
+        const double2 abB = sab[tid];
+        const double wB = sbw[tid] * itb;
         if (abB.x < abB.y) apply_runs(element_runs(abB.x, abB.y, XW, TW.hi), abB.x, abB.y, wB, XW, TW.hi, TW.iw, acc[0]);
     } else if (tid >= LIKE_THREADS - NDONOR) {
         const int mr = (tid - (LIKE_THREADS - NDONOR)) & 3;
+        const double* dq = sdq + ((tid - (LIKE_THREADS - NDONOR)) >> 2) * DON_STRIDE;
         const double vx = dq[0], vy = (mr & 1) ? -dq[1] : dq[1], vz = (mr & 2) ? -dq[2] : dq[2];
         const double cen = (mr & 1) ? -dq[3] : dq[3];
         const double hw = (mr & 2) ? 0.5 - dq[4] : dq[4];
@@ -960,8 +989,8 @@ __device__ inline void direct_spot_donor(const double2* __restrict__ ABs, const 
 #define LIKE_STAMP(i)
 #endif
 
-__device__ inline void finish_walker(const LikeArgs& L, int pair, int tid, bool acc1, double aq, double alu,
-                                     double azf, double alo, int* sflag)
+__device__ inline void finish_walker(const LikeArgs& L, int pair, int tid, bool acc1, double aq,
+                                     const double* sacc1, int* sflag)
 {
     if (!acc1) {
         if (tid == 0) combine_after(L, pair);
@@ -980,7 +1009,7 @@ __device__ inline void finish_walker(const LikeArgs& L, int pair, int tid, bool 
             v = lp + L.lle[pair];
         }
         if (L.lnp) L.lnp[pair] = v;
-        const bool a = alu < azf + v - alo;
+        const bool a = sacc1[0] < sacc1[1] + v - sacc1[2];
         if (a) {
             L.lnp_ens[wg] = v;
             if (L.naccept) L.naccept[wg] += 1;
@@ -995,14 +1024,24 @@ __device__ inline void finish_walker(const LikeArgs& L, int pair, int tid, bool 
 // ln_like of the residuals (a Kalman filter over each tile's sorted points,
 // run by wave 0 while the other waves wait at the tile barrier)
 template <int MODE>
-__global__ __launch_bounds__(LIKE_THREADS) void k_lnlike(LikeArgs L)
+__global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
 {
     constexpr bool CHI = MODE != 0, GP = MODE == 2;
 #ifdef LFG_PROFILE_LIKE
     const unsigned long long tstart = __builtin_amdgcn_s_memtime();
+    if (threadIdx.x == 0) {  // block start (100 MHz wall clock) and the CU it runs on
+        const_cast<double*>(L.geo)[size_t(blockIdx.x) * LFG_NGEO + 47] = double(__builtin_amdgcn_s_memrealtime());
+        unsigned hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        const_cast<double*>(L.geo)[size_t(blockIdx.x) * LFG_NGEO + 40] = double(hw);
+    }
 #endif
     __shared__ double swr[NWD_RINGS + NDISC_R];
+    __shared__ double swn[NWD_RINGS + NDISC_R];  // ring weights / component totals (the sweep's wn)
     __shared__ double sbw[NBS];
+    __shared__ double2 sab[NBS];                  // spot intervals
+    __shared__ double sdq[U_DON * DON_STRIDE];    // unique donor tiles
+    __shared__ double sacc1[3];                   // fused acceptance: ln u, zfac, old ln_prob
     __shared__ TileBufs TA, TB;      // WD/disc windows; spot windows of the current sub-bin
     __shared__ double sph[LIKE_TILE];  // sub-bin centre phases (donor)
     __shared__ int scp[LIKE_NC + 1];
@@ -1026,15 +1065,15 @@ __global__ __launch_bounds__(LIKE_THREADS) void k_lnlike(LikeArgs L)
     // (one per lane), the uniform draw and the old ln_prob are fetched here,
     // off the tail of the block (combine_walker does it for E > 1)
     const bool acc1 = CHI && L.pos && L.E == 1;
-    double aq = 0.0, alu = 0.0, azf = 0.0, alo = 0.0;
+    double aq = 0.0;
     if (acc1) {
         const int wg = L.half * L.npairs + pair;
         if (tid < L.ndim) aq = L.qprop[size_t(pair) * L.ndim + tid];
         if (tid == 0) {
             const uint4 r = draw(L.seed, L.step, L.half, 1, pair);
-            alu = log(u53(r.x, r.y));
-            azf = L.zfac[pair];
-            alo = L.lnp_ens[wg];
+            sacc1[0] = log(u53(r.x, r.y));
+            sacc1[1] = L.zfac[pair];
+            sacc1[2] = L.lnp_ens[wg];
         }
     }
     // every global load of the prologue is issued before anything waits on
@@ -1056,18 +1095,9 @@ __global__ __launch_bounds__(LIKE_THREADS) void k_lnlike(LikeArgs L)
     // tid (< NBS), donor tile (last NDONOR lanes)
     constexpr int NI = (NWD + NDISC + nt - 1) / nt;
     double2 abk[NI];
-    double wr[NI];
     for (int i = 0; i < NI; ++i) {
         const int k = sweep_item(tid + i * nt);
         abk[i] = (k < NWD + NDISC) ? AB[k] : make_double2(1.0, -1.0);
-        if (k < NWD) {
-            int r = int(sqrtf(float(k) * 0.25f));  // WD ring: 4 r^2 <= k < 4 (r + 1)^2
-            r += (4 * (r + 1) * (r + 1) <= k) ? 1 : 0;
-            r -= (4 * r * r > k) ? 1 : 0;
-            wr[i] = wd_ring_weight(r, ul);
-        } else {
-            wr[i] = (k < NWD + NDISC) ? Wt[WT_DISC + (k - NWD) / NDISC_AZ] : 0.0;
-        }
     }
     double2 abB = make_double2(1.0, -1.0);
     double wB = 0.0;
@@ -1092,7 +1122,7 @@ __global__ __launch_bounds__(LIKE_THREADS) void k_lnlike(LikeArgs L)
         }
         if (CHI) {
             if (tid == 0) L.lle[pair] = -INFINITY;
-            finish_walker(L, pair, tid, acc1, aq, alu, azf, alo, sflag);
+            finish_walker(L, pair, tid, acc1, aq, sacc1, sflag);
         }
         return;
     }
@@ -1108,6 +1138,9 @@ __global__ __launch_bounds__(LIKE_THREADS) void k_lnlike(LikeArgs L)
         vs = fabs(dq[0]) + fabs(dq[1]) + fabs(dq[2]);
     }
     if (tid >= NBS && tid < NBS + NWD_RINGS + NDISC_R) swr[tid - NBS] = wring;
+    if (tid < NBS) sab[tid] = abB;
+    else if (tid >= nt - NDONOR && ((tid - (nt - NDONOR)) & 3) == 0)
+        for (int i = 0; i < DON_STRIDE; ++i) sdq[((tid - (nt - NDONOR)) >> 2) * DON_STRIDE + i] = dq[i];
     tb = wave_sum(tb);
     dn = wave_sum(dn);
     vs = wave_sum(vs);
@@ -1117,9 +1150,8 @@ __global__ __launch_bounds__(LIKE_THREADS) void k_lnlike(LikeArgs L)
     for (int i = 0; i < nw; ++i) { tb += red[0][i]; dn += red[1][i]; vs += red[2][i]; }
     const double twd = TWO_PI * ((1.0 - ul) * 0.5 + ul / 3.0);  // 2 pi [F(1) - F(0)]
     const double iwd = 1.0 / twd, id = 1.0 / td, itb = 1.0 / tb, ivs = 1.0 / vs;
-    double wn[NI];
-    for (int i = 0; i < NI; ++i) wn[i] = wr[i] * ((sweep_item(tid + i * nt) < NWD) ? iwd : id);
-    wB *= itb;
+    if (tid >= NBS && tid < NBS + NWD_RINGS + NDISC_R)  // visible to the sweep after the pass barrier
+        swn[tid - NBS] = wring * ((tid - NBS < NWD_RINGS) ? iwd : id);
 
     const double wdF = G[G_WDF], dF = G[G_DF], sF = G[G_SF], rsF = G[G_RSF];
     const double phi0 = G[G_PHI0], fis = G[G_FIS], bden = G[G_BDEN];
@@ -1181,14 +1213,16 @@ __global__ __launch_bounds__(LIKE_THREADS) void k_lnlike(LikeArgs L)
                 count_le_back_multi<2 * NI>(TA.hi, qx, J, Jb);
 #pragma unroll
                 for (int i = 0; i < NI; ++i)
-                    if (abk[i].x < abk[i].y)
+                    if (abk[i].x < abk[i].y) {
+                        const int k = sweep_item(tid + i * nt);
                         apply_runs(Runs{Jb[2 * i], J[2 * i], Jb[2 * i + 1], J[2 * i + 1]}, abk[i].x, abk[i].y,
-                                   wn[i], X, TA.hi, TA.iw, sacc[(sweep_item(tid + i * nt) < NWD) ? 0 : 1]);
+                                   swn[sweep_ring(k)], X, TA.hi, TA.iw, sacc[(k < NWD) ? 0 : 1]);
+                    }
             }
             LIKE_STAMP(2);
             if (swB) {
                 const PhaseIndex XW = phase_index(TB.lo, TB.cell, m), XP = phase_index(sph, scp, m);
-                sweep_spot_donor(tid, XW, TB, XP, abB, wB, dq, ivs, sacc + 2);
+                sweep_spot_donor(tid, XW, TB, XP, sab, sbw, itb, sdq, ivs, sacc + 2);
             }
             __syncthreads();
             LIKE_STAMP(3);
@@ -1274,7 +1308,7 @@ __global__ __launch_bounds__(LIKE_THREADS) void k_lnlike(LikeArgs L)
             const bool okp = G[G_GP_OK] != 0.0;
             L.lle[pair] = (okp && n > 0) ? gpf.lnlike() : (okp ? 0.0 : -INFINITY);
         }
-        finish_walker(L, pair, tid, acc1, aq, alu, azf, alo, sflag);
+        finish_walker(L, pair, tid, acc1, aq, sacc1, sflag);
     } else if (CHI) {
         chi = wave_sum(chi);
         if (lane == 0) red[0][wv] = chi;
@@ -1284,7 +1318,7 @@ __global__ __launch_bounds__(LIKE_THREADS) void k_lnlike(LikeArgs L)
             for (int i = 0; i < nw; ++i) tot += red[0][i];
             L.lle[pair] = -0.5 * tot;
         }
-        finish_walker(L, pair, tid, acc1, aq, alu, azf, alo, sflag);
+        finish_walker(L, pair, tid, acc1, aq, sacc1, sflag);
     }
 }
 
@@ -1382,6 +1416,33 @@ __global__ void k_accept(double* __restrict__ pos, double* __restrict__ lnp, int
         double* p = pos + size_t(w) * ndim;
         const double* qi = q + size_t(i) * ndim;
         for (int d = 0; d < ndim; ++d) p[d] = qi[d];
+        lnp[w] = lnp_new[i];
+        if (naccept) naccept[w] += 1;
+    }
+}
+
+// k_accept with the proposal re-formed from the same draws (k_propose's
+// arithmetic): the sharded half-step keeps only its own shard of q, and the
+// partner half is unchanged until this half is accepted
+__global__ void k_accept_regen(double* __restrict__ pos, double* __restrict__ lnp, int W, int ndim, int half,
+                               double a, const double* __restrict__ lnp_new, unsigned long long seed,
+                               unsigned long long step, int* __restrict__ naccept)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int ns = W / 2;
+    if (i >= ns) return;
+    const int w = half * ns + i;
+    const uint4 r0 = draw(seed, step, half, 0, i);
+    const double zr = (a - 1.0) * u53(r0.x, r0.y) + 1.0;
+    const double z = zr * zr / a;
+    const uint4 r = draw(seed, step, half, 1, i);
+    const double lu = log(u53(r.x, r.y));
+    const double diff = (ndim - 1.0) * log(z) + lnp_new[i] - lnp[w];
+    if (lu < diff) {
+        const int j = int(__umulhi(r0.z, unsigned(ns)));
+        double* p = pos + size_t(w) * ndim;
+        const double* cj = pos + size_t((1 - half) * ns + j) * ndim;
+        for (int d = 0; d < ndim; ++d) p[d] = fma(p[d] - cj[d], z, cj[d]);
         lnp[w] = lnp_new[i];
         if (naccept) naccept[w] += 1;
     }
@@ -1532,11 +1593,14 @@ struct Accept {  // fused stretch-move acceptance of lfg_stretch_lnprob_accept
     int* naccept;
 };
 
-struct Propose {  // inline proposal of lfg_stretch_step_half
+struct Propose {  // inline proposal of lfg_stretch_step_half / _shard
     const double* pos;
     double a;
     double* q;
     double* zfac;
+    int half;
+    unsigned long long seed, step;
+    int lo, ns;  // the batch: walkers lo .. lo + W - 1 of the ns-walker half
 };
 
 static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* lnp, double* lnlike_e, void* wsp,
@@ -1556,11 +1620,13 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
     if (prop) {
         S.pos = prop->pos;
         S.a = prop->a;
-        S.seed = acc->seed;
-        S.step = acc->step;
-        S.half = acc->half;
+        S.seed = prop->seed;
+        S.step = prop->step;
+        S.half = prop->half;
         S.qout = prop->q;
         S.zfout = prop->zfac;
+        S.lo = prop->lo;
+        S.ns = prop->ns;
     }
     const int npairs = W * T->E;
     int rc = run_front(S, ws, st, ev);
@@ -1616,8 +1682,19 @@ int lfg_stretch_step_half(double* pos, double* lnp, int W, int half, double a, u
     if (W < 4 || (W & 1) || (half != 0 && half != 1) || !(a > 1.0) || !pos || !lnp || !q || !zfac || !T)
         return LFG_E_ARGS;
     const Accept acc{pos, lnp, zfac, half, seed, step, naccept};
-    const Propose prop{pos, a, q, zfac};
+    const Propose prop{pos, a, q, zfac, half, seed, step, 0, W / 2};
     return lnprob_impl(q, W / 2, T, lnp_new, nullptr, wsp, ws_bytes, stream, ev, &acc, &prop);
+}
+
+int lfg_stretch_step_shard(const double* pos, int W, int half, double a, unsigned long long seed,
+                           unsigned long long step, int lo, int n, double* q, double* zfac, const lfg_tree* T,
+                           double* lnp_new, void* wsp, size_t ws_bytes, void* stream, void* const* ev)
+{
+    if (W < 4 || (W & 1) || (half != 0 && half != 1) || !(a > 1.0) || !pos || !q || !zfac || !T || !lnp_new ||
+        n <= 0 || lo < 0 || lo + n > W / 2)
+        return LFG_E_ARGS;
+    const Propose prop{pos, a, q, zfac, half, seed, step, lo, W / 2};
+    return lnprob_impl(q, n, T, lnp_new, nullptr, wsp, ws_bytes, stream, ev, nullptr, &prop);
 }
 
 int lfg_stretch_lnprob_accept(double* pos, double* lnp, int W, int half, const double* q, const double* zfac,
@@ -1650,6 +1727,18 @@ static int accept_impl(double* pos, double* lnp, int W, int ndim, int half, cons
     const int ns = W / 2;
     hipLaunchKernelGGL(k_accept, dim3((ns + 63) / 64), dim3(64), 0, static_cast<hipStream_t>(stream), pos, lnp,
                        W, ndim, half, q, zfac, lnp_new, seed, step, stepp, naccept);
+    return launch_ok();
+}
+
+int lfg_stretch_accept_regen(double* pos, double* lnp, int W, int ndim, int half, double a,
+                             unsigned long long seed, unsigned long long step, const double* lnp_new, int* naccept,
+                             void* stream)
+{
+    if (W < 4 || (W & 1) || ndim <= 0 || (half != 0 && half != 1) || !(a > 1.0) || !pos || !lnp || !lnp_new)
+        return LFG_E_ARGS;
+    const int ns = W / 2;
+    hipLaunchKernelGGL(k_accept_regen, dim3((ns + 63) / 64), dim3(64), 0, static_cast<hipStream_t>(stream), pos,
+                       lnp, W, ndim, half, a, lnp_new, seed, step, naccept);
     return launch_ok();
 }
 

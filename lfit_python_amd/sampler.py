@@ -64,6 +64,12 @@ class HipStretchOps:
         _native.check(rc, "lfg_stretch_accept")
 
     # step counter in device memory (int64 tensor of one element): HIP-graph capturable
+    def accept_regen(self, pos, lnp, half, a, lnp_new, seed, step, naccept):
+        W, ndim = pos.shape
+        rc = self.L.lfg_stretch_accept_regen(self._vp(pos), self._vp(lnp), W, ndim, half, a, seed, step,
+                                             self._vp(lnp_new), self._vp(naccept), _native.stream_ptr(self.device))
+        _native.check(rc, "lfg_stretch_accept_regen")
+
     def propose_dev(self, pos, half, a, seed, step_dev, q, zfac):
         W, ndim = pos.shape
         rc = self.L.lfg_stretch_propose_dev(self._vp(pos), W, ndim, half, a, seed, self._vp(step_dev),
@@ -116,6 +122,14 @@ class EnsembleSampler:
         # the optional half_timer replaces evaluator.step_half (bench timing)
         self.fuse = hasattr(evaluator, "step_half") and isinstance(self.ops, HipStretchOps)
         self.half_timer = None
+        # sharded fused path (N ranks, or forced on one for tests): proposal and
+        # ln_prob of this rank's shard in three kernels (lfg_stretch_step_shard),
+        # all_gather of ln_prob, acceptance re-forming the proposals
+        # (lfg_stretch_accept_regen); shard_timer replaces evaluator.step_shard
+        self.fuse_shard = hasattr(evaluator, "step_shard") and isinstance(self.ops, HipStretchOps)
+        self.force_shard = False
+        self.shard_timer = None
+        self._q_sh = self._zf_sh = self._lnp_sh = None
         # HIP-graph replay of whole iterations (single rank, HIP ops): the first
         # step() after enabling runs eagerly, the next captures, later ones replay
         self.use_graph = False
@@ -210,10 +224,13 @@ class EnsembleSampler:
             return
         self._warm = True
         for half in (0, 1):
-            if self.world == 1 and self.fuse and self.timer is None:
+            if self.world == 1 and self.fuse and self.timer is None and not self.force_shard:
                 f = self.half_timer or self.ev.step_half
                 f(self.pos, self.lnp, half, self.a, self.seed, self.iteration, self.q, self.zfac, self.naccept,
                   lnp_new=self.lnp_new)
+                continue
+            if (self.world > 1 or self.force_shard) and self.fuse_shard and self.timer is None:
+                self._shard_half(half)
                 continue
             self.ops.propose(self.pos, half, self.a, self.seed, self.iteration, self.q, self.zfac)
             if self.world == 1:
@@ -225,6 +242,23 @@ class EnsembleSampler:
             self.ops.accept(self.pos, self.lnp, half, self.q, self.zfac, self.lnp_new, self.seed,
                             self.iteration, self.naccept)
         self.iteration += 1
+
+    def _shard_half(self, half):
+        import torch
+        if self._lnp_sh is None:
+            f64 = dict(dtype=torch.float64, device=self.dev)
+            self._q_sh = torch.empty((self.shard, self.ndim), **f64)
+            self._zf_sh = torch.empty(self.shard, **f64)
+            self._lnp_sh = torch.empty(self.shard, **f64)
+        f = self.shard_timer or self.ev.step_shard
+        f(self.pos, half, self.a, self.seed, self.iteration, self.rank * self.shard, self._q_sh, self._zf_sh,
+          self._lnp_sh)
+        if self.world > 1:
+            self._gather(self.lnp_new, self._lnp_sh)
+        else:
+            self.lnp_new.copy_(self._lnp_sh)
+        self.ops.accept_regen(self.pos, self.lnp, half, self.a, self.lnp_new, self.seed, self.iteration,
+                              self.naccept)
 
     def run_mcmc(self, p0, nsteps, store=True, lnp0=None):
         """emcee-style run; returns (pos, lnp) as numpy.  With store=True the

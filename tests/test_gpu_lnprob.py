@@ -125,8 +125,9 @@ def test_device_mcmc_runs():
 def test_fused_half_step_matches_separate_kernels():
     """lfg_stretch_step_half (the default single-process path: proposal in
     k_setup, acceptance in k_lnlike) gives the chain of lfg_stretch_propose +
-    lfg_lnprob + lfg_stretch_accept, bit for bit, across reset(); and so does
-    lfg_stretch_lnprob_accept."""
+    lfg_lnprob + lfg_stretch_accept, bit for bit, across reset(); and so do
+    lfg_stretch_lnprob_accept and the sharded path (lfg_stretch_step_shard on
+    one or two shards + lfg_stretch_accept_regen)."""
     import torch
     from lfit_python_amd import batch, sampler, synthetic
     out = []
@@ -142,9 +143,18 @@ def test_fused_half_step_matches_separate_kernels():
         init = sampler.initialise_walkers(p0, sampler.comp_scatter(m.dynasty_par_names, 0.1), W,
                                           lambda p: ev(torch.as_tensor(p, device="cuda")).cpu().numpy())
         res = []
-        for mode in ("separate", "step_half", "lnprob_accept"):
+        for mode in ("separate", "step_half", "lnprob_accept", "shard1", "shard2"):
             S = sampler.EnsembleSampler(W, t.ndim, ev, seed=21)
-            S.fuse = mode != "separate"
+            S.fuse = mode in ("step_half", "lnprob_accept")
+            S.force_shard = mode.startswith("shard")
+            if mode == "shard2":
+                # two ranks' shards of each half (lfg_stretch_step_shard with
+                # lo = 0 and lo = k) into one ln_prob vector, as the gather does
+                def shard(pos, h, a, seed, step, lo, q, zfac, lnp_sh, ev=ev):
+                    k = lnp_sh.shape[0] // 2
+                    for lo_, hi_ in ((0, k), (k, lnp_sh.shape[0])):
+                        ev.step_shard(pos, h, a, seed, step, lo_, q[lo_:hi_], zfac[lo_:hi_], lnp_sh[lo_:hi_])
+                S.shard_timer = shard
             if mode == "lnprob_accept":
                 def half(pos, lnp, h, a, seed, step, q, zfac, naccept, lnp_new=None, S=S, ev=ev):
                     S.ops.propose(pos, h, a, seed, step, q, zfac)

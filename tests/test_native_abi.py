@@ -75,6 +75,11 @@ def test_argument_errors_without_gpu():
     assert L.lfg_lnprob(None, 4, None, None, None, None, 0, None) == -1
     assert L.lfg_stretch_propose(None, 15, 4, 0, 2.0, 1, 0, None, None, None) == -1
     assert L.lfg_roche(7, None, None, 1, None, None, None) == -1
+    # a shard outside the half, an odd ensemble: refused before any launch
+    vp8 = ctypes.c_void_p(8)
+    assert L.lfg_stretch_step_shard(vp8, 64, 0, 2.0, 1, 0, 20, 16, vp8, vp8, None, vp8, vp8, 1 << 30, None,
+                                    None) == -1
+    assert L.lfg_stretch_accept_regen(vp8, vp8, 63, 4, 0, 2.0, 1, 0, vp8, None, None) == -1
     assert L.lfg_wdphases(None, None, None, 4, 10, None, None, None, None) == -1
     assert L.lfg_wdphases(None, None, None, 0, 10, None, None, None, None) == 0  # nothing to do
     assert L.lfg_gp_lnlike(None, None, None, 0, 10, None, None, 0, None, None) == -1

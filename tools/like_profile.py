@@ -10,18 +10,27 @@ from tests.helpers import random_pars, phase_grid
 L = _native.lib()
 dev = torch.device('cuda', 0)
 W = int(sys.argv[1]) if len(sys.argv) > 1 else 512
+NPTS = int(sys.argv[2]) if len(sys.argv) > 2 else 300
+NSUB = int(sys.argv[3]) if len(sys.argv) > 3 else 1
 pars = torch.as_tensor(random_pars(W, complex_bs=True, seed=1), device=dev).contiguous()
-x, w = phase_grid(300)
+x, w = phase_grid(NPTS)
 X = torch.as_tensor(x, device=dev); Wd = torch.as_tensor(w, device=dev)
 flux = torch.empty((W, len(x)), dtype=torch.float64, device=dev)
 st = torch.empty(W, dtype=torch.int32, device=dev)
 ws = torch.empty(L.lfg_workspace_size(W, 1), dtype=torch.uint8, device=dev)
 vp = lambda t: ctypes.c_void_p(t.data_ptr())
 for _ in range(3):
-    rc = L.lfg_flux(vp(pars), W, 18, vp(X), vp(Wd), len(x), 1, vp(flux), None, vp(st), vp(ws), ws.numel(),
+    rc = L.lfg_flux(vp(pars), W, 18, vp(X), vp(Wd), len(x), NSUB, vp(flux), None, vp(st), vp(ws), ws.numel(),
                     _native.stream_ptr())
     assert rc == 0
 torch.cuda.synchronize()
+import time
+t0 = time.perf_counter()
+for _ in range(5):
+    L.lfg_flux(vp(pars), W, 18, vp(X), vp(Wd), len(x), NSUB, vp(flux), None, vp(st), vp(ws), ws.numel(),
+               _native.stream_ptr())
+torch.cuda.synchronize()
+print('W %d npts %d nsub %d: %.1f us per lfg_flux' % (W, NPTS, NSUB, (time.perf_counter() - t0) / 5 * 1e6))
 g = ws[:W * 48 * 8].view(torch.float64).view(W, 48).cpu().numpy()
 ok = st.cpu().numpy() == 0
 names = ['staged', 'cells', 'sweepWD', 'sweepBD', 'scan', 'end']
@@ -30,3 +39,12 @@ for i, nm in enumerate(names):
     v = g[ok, 41 + i]
     print('%-8s cum mean %8.0f  max %8.0f   delta mean %8.0f' % (nm, v.mean(), v.max(), (v - prev).mean()))
     prev = v
+
+t = g[:, 47] - g[:, 47].min()
+print('block start (us, 100 MHz clock): %s' % np.percentile(t / 100.0, [0, 25, 50, 75, 90, 100]).round(2))
+hw = g[:, 40].astype(np.int64)
+cu = (hw >> 8) & 0xF
+sh = (hw >> 12) & 1
+se = (hw >> 13) & 0x7
+key = se * 32 + sh * 16 + cu
+print('distinct (se, sh, cu) slots in use: %d of %d blocks' % (len(np.unique(key)), len(key)))

@@ -25,7 +25,8 @@ ws = torch.empty(L.lfg_workspace_size(W, 1), dtype=torch.uint8, device=dev)
 vp = lambda t: ctypes.c_void_p(t.data_ptr())
 L.lfg_elements(vp(P), W, 18, None, None, None, None, vp(geo), vp(st), vp(ws), ws.numel(), _native.stream_ptr())
 g = geo.cpu().numpy()
-for k, name in zip(range(42, 47), ['roche_init', 'bspot', 'findi', 'findphi90', 'bs_umax']):
+for k, name in zip(range(42, 48), ['gather+roche_init', 'stream lane', 'findi', 'findphi90', 'bs_umax',
+                                   'setup lane']):
     v = g[:, k]
     print('%-10s cycles mean %9.0f  max %9.0f' % (name, v.mean(), v.max()))
 print('status', np.bincount(st.cpu().numpy()))
