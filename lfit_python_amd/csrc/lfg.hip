@@ -562,9 +562,27 @@ __global__ void k_expand(const double* __restrict__ geo, const int* __restrict__
 }
 
 // --------------------------------------------------------------- k_lnlike
+// Cross-lane moves by ds_bpermute with the lane address formed at each use:
+// __shfl_xor / __shfl_up hoist one address VGPR per offset out of every loop
+// and keep them live through k_lnlike (the volatile mbcnt is not hoisted).
+__device__ __forceinline__ int lane_id_here()
+{
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
+__device__ __forceinline__ long long bperm64(int addr, long long v)
+{
+    const int lo = __builtin_amdgcn_ds_bpermute(addr, static_cast<int>(v));
+    const int hi = __builtin_amdgcn_ds_bpermute(addr, static_cast<int>(v >> 32));
+    return (static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo);
+}
+
 __device__ __forceinline__ double wave_sum(double v)
 {
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    for (int off = 32; off > 0; off >>= 1)
+        v += __longlong_as_double(bperm64((lane_id_here() ^ off) << 2, __double_as_longlong(v)));
     return v;
 }
 
@@ -678,7 +696,7 @@ __device__ inline void combine_after(const LikeArgs& L, int pair)
 // int64 so LDS atomics add them exactly, independent of order.
 constexpr int LIKE_THREADS = 512;
 #ifndef LIKE_MINW
-#define LIKE_MINW 2  // minimum waves per SIMD (4: two blocks per CU, <= 128 VGPRs)
+#define LIKE_MINW 4  // minimum waves per SIMD: two 512-lane blocks per CU (<= 128 VGPRs; LDS < 80 KB)
 #endif
 constexpr int LIKE_TILE = LIKE_THREADS;  // one point per thread per tile
 constexpr int LIKE_NC = 2 * LIKE_TILE;   // cells of the phase index
@@ -864,7 +882,7 @@ __device__ __forceinline__ int sweep_ring(int k)
 __device__ __forceinline__ long long wave_scan_incl(long long v, int lane)
 {
     for (int off = 1; off < 64; off <<= 1) {
-        const long long u = __shfl_up(v, off, 64);
+        const long long u = bperm64((lane_id_here() - off) << 2, v);  // lanes below off: ignored
         if (lane >= off) v += u;
     }
     return v;
@@ -876,20 +894,37 @@ __device__ __forceinline__ void block_scan(unsigned long long (*acc)[LIKE_TILE +
                                            int tid, long long* out)
 {
     const int lane = tid & 63, wv = tid >> 6;
-    long long w[NA];
+    constexpr int NW = LIKE_THREADS / 64;
     for (int i = 0; i < NA; ++i) {
-        w[i] = wave_scan_incl(static_cast<long long>(acc[i][tid]), lane);
-        if (lane == 63) part[i][wv] = w[i];
+        out[i] = wave_scan_incl(static_cast<long long>(acc[i][tid]), lane);
+        if (lane == 63) part[i][wv] = out[i];
     }
     __syncthreads();
-    for (int i = 0; i < NA; ++i) {
-        long long b = 0;
-        for (int k = 0; k < wv; ++k) b += part[i][k];
-        out[i] = w[i] + b;
+    // exclusive prefix over the waves, one (array, wave) per thread, in
+    // place after a second barrier: each thread then reads one word per array
+    // (summing all earlier waves' totals in every thread holds NA x NW of
+    // them in registers at once)
+    long long pre = 0;
+    if (tid < NA * NW) {
+        const int i = tid / NW, k = tid - (tid / NW) * NW;
+        for (int q = 0; q < k; ++q) pre += part[i][q];
     }
+    __syncthreads();
+    if (tid < NA * NW) part[tid / NW][tid - (tid / NW) * NW] = pre;
+    __syncthreads();
+    for (int i = 0; i < NA; ++i) out[i] += part[i][wv];
 }
 
 __device__ __forceinline__ double wrap_phase(double ph) { return ph - floor(ph + 0.5); }
+
+// sincospi out of line: inlined into the tile loop, its polynomial constants
+// are hoisted into ~20 loop-invariant VGPRs
+__device__ __noinline__ double2 sincospi_ool(double x)
+{
+    double sn, cs;
+    sincospi(x, &sn, &cs);
+    return make_double2(sn, cs);
+}
 
 // tile buffers of one sweep pass: windows [lo, hi] with inverse widths, and
 // the sub-bin centre phases (donor), each with its cell index
@@ -959,13 +994,35 @@ __device__ __forceinline__ void sweep_spot_donor(int tid, const PhaseIndex& XW, 
     }
 }
 
-// direct (point-major) spot eclipse fraction and donor sum for one point
-__device__ inline void direct_spot_donor(const double2* __restrict__ ABs, const double* __restrict__ sbw,
-                                         const double* __restrict__ DONp, double ph, double h, double e0,
-                                         double e1, double c, double itb, double& eb, double& D)
+// direct (point-major) WD and disc eclipse fractions of one window: the
+// fallback for unsorted or mixed windows (out of line: it must not add to the
+// sweep's register budget)
+__device__ __noinline__ double2 direct_wd_disc(const double2* __restrict__ AB, const double* __restrict__ swr,
+                                               double phc, double wk, double twd, double td)
 {
-    eb = 0.0;
-    D = 0.0;
+    double ewd = 0.0, ed = 0.0;
+    const double lo = phc - wk, hi = phc + wk;
+    for (int ring = 0; ring < NWD_RINGS + NDISC_R; ++ring) {
+        const int k0 = ring < NWD_RINGS ? 4 * ring * ring : NWD + (ring - NWD_RINGS) * NDISC_AZ;
+        const int k1 = ring < NWD_RINGS ? 4 * (ring + 1) * (ring + 1) : k0 + NDISC_AZ;
+        double acc = 0.0;
+        for (int k = k0; k < k1; ++k) {
+            const double2 ab = AB[k];
+            acc += (wk > 0.0) ? fmax(fmin(ab.y, hi) - fmax(ab.x, lo), 0.0)
+                              : ((phc > ab.x && phc < ab.y) ? 1.0 : 0.0);
+        }
+        if (ring < NWD_RINGS) ewd = fma(swr[ring], acc, ewd); else ed = fma(swr[ring], acc, ed);
+    }
+    const double nrm = (wk > 0.0) ? 1.0 / (2.0 * wk) : 1.0;
+    return make_double2(ewd * nrm * (1.0 / twd), ed * nrm * (1.0 / td));
+}
+
+// direct (point-major) spot eclipse fraction and donor sum for one point
+__device__ __noinline__ double2 direct_spot_donor(const double2* __restrict__ ABs, const double* __restrict__ sbw,
+                                            const double* __restrict__ DONp, double ph, double h, double e0,
+                                            double e1, double c, double itb)
+{
+    double eb = 0.0, D = 0.0;
     const double l2 = ph - h, h2 = ph + h;
     for (int k = 0; k < NBS; ++k) {
         const double2 ab = ABs[k];
@@ -980,6 +1037,7 @@ __device__ inline void direct_spot_donor(const double2* __restrict__ ABs, const 
         const double A1 = fma(d5[0], e0, z), A2 = fma(d5[0], e0, -z);
         D += fmax(A1 + fmax(y, A1), 0.0) + fmax(A2 + fmax(y, A2), 0.0);
     }
+    return make_double2(eb, D);
 }
 
 #ifdef LFG_PROFILE_LIKE  // diagnostic build only: phase stamps (first tile) into spare geo slots 41..46
@@ -1042,6 +1100,8 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
     __shared__ double2 sab[NBS];                  // spot intervals
     __shared__ double sdq[U_DON * DON_STRIDE];    // unique donor tiles
     __shared__ double sacc1[3];                   // fused acceptance: ln u, zfac, old ln_prob
+    __shared__ double snorm[4];                   // 1 / spot total, 1 / donor |v| sum, donor norm, |v| sum
+    __shared__ double sgeo[LFG_NGEO];             // the pair's geometry record, read at use in the tile loop
     __shared__ TileBufs TA, TB;      // WD/disc windows; spot windows of the current sub-bin
     __shared__ double sph[LIKE_TILE];  // sub-bin centre phases (donor)
     __shared__ int scp[LIKE_NC + 1];
@@ -1081,14 +1141,10 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
     const int st = L.status[pair];
     const double s = G[G_S], c = G[G_C], ul = G[G_ULIMB];
     const double td = Wt[WT_TD];
-    double px = 0.0, pw = 0.0, py = 0.0, pye = 1.0;  // tile-0 point of this thread
+    double px = 0.0, pw = 0.0;  // tile-0 point of this thread (y, ye: read where chi^2 is formed)
     if (tid < n) {
         px = L.x[o0 + tid];
         pw = L.w ? L.w[o0 + tid] : 0.0;
-        if (CHI) {
-            py = L.y[o0 + tid];
-            pye = L.ye[o0 + tid];
-        }
     }
     // this thread's sweep items, held in registers for every tile: WD/disc
     // elements sweep_item(tid + i nt) with their ring weights, spot element
@@ -1109,6 +1165,9 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
         const int t = tid - (nt - NDONOR);
         for (int i = 0; i < DON_STRIDE; ++i) dq[i] = DONp[(t >> 2) * DON_STRIDE + i];
     }
+    double gv = 0.0;  // one geometry word per lane for sgeo
+    if (tid >= NBS + NWD_RINGS + NDISC_R && tid < NBS + NWD_RINGS + NDISC_R + G_COUNT)
+        gv = G[tid - (NBS + NWD_RINGS + NDISC_R)];
     double wring = 0.0;  // ring weights for the direct path
     if (tid >= NBS && tid < NBS + NWD_RINGS) wring = wd_ring_weight(tid - NBS, ul);
     else if (tid >= NBS + NWD_RINGS && tid < NBS + NWD_RINGS + NDISC_R)
@@ -1138,6 +1197,8 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
         vs = fabs(dq[0]) + fabs(dq[1]) + fabs(dq[2]);
     }
     if (tid >= NBS && tid < NBS + NWD_RINGS + NDISC_R) swr[tid - NBS] = wring;
+    if (tid >= NBS + NWD_RINGS + NDISC_R && tid < NBS + NWD_RINGS + NDISC_R + G_COUNT)
+        sgeo[tid - (NBS + NWD_RINGS + NDISC_R)] = gv;
     if (tid < NBS) sab[tid] = abB;
     else if (tid >= nt - NDONOR && ((tid - (nt - NDONOR)) & 3) == 0)
         for (int i = 0; i < DON_STRIDE; ++i) sdq[((tid - (nt - NDONOR)) >> 2) * DON_STRIDE + i] = dq[i];
@@ -1146,16 +1207,21 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
     vs = wave_sum(vs);
     if (lane == 0) { red[0][wv] = tb; red[1][wv] = dn; red[2][wv] = vs; }
     __syncthreads();
-    tb = dn = vs = 0.0;
-    for (int i = 0; i < nw; ++i) { tb += red[0][i]; dn += red[1][i]; vs += red[2][i]; }
+    if (tid == 0) {  // block-uniform normalisers live in LDS (read at use: no registers held)
+        tb = dn = vs = 0.0;
+        for (int i = 0; i < nw; ++i) { tb += red[0][i]; dn += red[1][i]; vs += red[2][i]; }
+        snorm[0] = 1.0 / tb;
+        snorm[1] = 1.0 / vs;
+        snorm[2] = dn;
+        snorm[3] = vs;
+    }
     const double twd = TWO_PI * ((1.0 - ul) * 0.5 + ul / 3.0);  // 2 pi [F(1) - F(0)]
-    const double iwd = 1.0 / twd, id = 1.0 / td, itb = 1.0 / tb, ivs = 1.0 / vs;
     if (tid >= NBS && tid < NBS + NWD_RINGS + NDISC_R)  // visible to the sweep after the pass barrier
-        swn[tid - NBS] = wring * ((tid - NBS < NWD_RINGS) ? iwd : id);
+        swn[tid - NBS] = wring * ((tid - NBS < NWD_RINGS) ? 1.0 / twd : 1.0 / td);
 
-    const double wdF = G[G_WDF], dF = G[G_DF], sF = G[G_SF], rsF = G[G_RSF];
-    const double phi0 = G[G_PHI0], fis = G[G_FIS], bden = G[G_BDEN];
-    const double nb0 = G[G_NB0], nb1 = G[G_NB1], nb2 = G[G_NB2];
+    // geometry constants of the tile loop come from sgeo at each use (vector
+    // loads of G would hold ~13 doubles in VGPRs through every pass)
+    const double* SG = sgeo;
     const int S = L.nsub;
     double chi = 0.0;
     GPFilter gpf;  // GP mode, wave 0
@@ -1167,13 +1233,9 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
         if (t0 > 0 && own) {
             px = L.x[p];
             pw = L.w ? L.w[p] : 0.0;
-            if (CHI) {
-                py = L.y[p];
-                pye = L.ye[p];
-            }
         }
         const double wk = own ? pw : 0.0;
-        const double ph0 = own ? px - phi0 : 0.0;
+        const double ph0 = own ? px - SG[G_PHI0] : 0.0;
         const double phc = wrap_phase(ph0);
         const double h = wk / S;
         double fw = 0.0, fd = 0.0, sbs = 0.0, srs = 0.0;
@@ -1222,7 +1284,7 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
             LIKE_STAMP(2);
             if (swB) {
                 const PhaseIndex XW = phase_index(TB.lo, TB.cell, m), XP = phase_index(sph, scp, m);
-                sweep_spot_donor(tid, XW, TB, XP, sab, sbw, itb, sdq, ivs, sacc + 2);
+                sweep_spot_donor(tid, XW, TB, XP, sab, sbw, snorm[0], sdq, snorm[1], sacc + 2);
             }
             __syncthreads();
             LIKE_STAMP(3);
@@ -1234,43 +1296,37 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
                     fw = double(r[0]) * FX_INV;
                     fd = double(r[1]) * FX_INV;
                 } else if (own) {  // unsorted / mixed widths: every element against this point
-                    double ewd = 0.0, ed = 0.0;
-                    const double lo = phc - wk, hi = phc + wk;
-                    for (int ring = 0; ring < NWD_RINGS + NDISC_R; ++ring) {
-                        const int k0 = ring < NWD_RINGS ? 4 * ring * ring : NWD + (ring - NWD_RINGS) * NDISC_AZ;
-                        const int k1 = ring < NWD_RINGS ? 4 * (ring + 1) * (ring + 1) : k0 + NDISC_AZ;
-                        double acc = 0.0;
-                        for (int k = k0; k < k1; ++k) {
-                            const double2 ab = AB[k];
-                            acc += (wk > 0.0) ? fmax(fmin(ab.y, hi) - fmax(ab.x, lo), 0.0)
-                                              : ((phc > ab.x && phc < ab.y) ? 1.0 : 0.0);
-                        }
-                        if (ring < NWD_RINGS) ewd = fma(swr[ring], acc, ewd); else ed = fma(swr[ring], acc, ed);
-                    }
-                    const double nrm = (wk > 0.0) ? 1.0 / (2.0 * wk) : 1.0;
-                    fw = ewd * nrm * iwd;
-                    fd = ed * nrm * id;
+                    const double ulg = SG[G_ULIMB];
+                    const double2 f2 = direct_wd_disc(AB, swr, phc, wk, TWO_PI * ((1.0 - ulg) * 0.5 + ulg / 3.0),
+                                                      Wt[WT_TD]);
+                    fw = f2.x;
+                    fd = f2.y;
                 }
             }
-            double sn, cs;
-            sincospi(2.0 * ph, &sn, &cs);  // |2 ph| <= 1: cheap exact reduction
-            const double e0 = s * cs, e1 = -s * sn;
+            const double2 scp2 = sincospi_ool(2.0 * ph);  // |2 ph| <= 1: cheap exact reduction
+            const double sn = scp2.x, cs = scp2.y;
+            const double sg = SG[G_S], cg = SG[G_C];
+            const double e0 = sg * cs, e1 = -sg * sn;
             double eb = 0.0, D = 0.0;
             if (swB) {
                 eb = double(r[2]) * FX_INV;
-                D = (e0 * double(r[3]) + e1 * double(r[4]) + c * double(r[5])) * (FX_INV * vs);
+                D = (e0 * double(r[3]) + e1 * double(r[4]) + cg * double(r[5])) * (FX_INV * snorm[3]);
             } else if (own) {
-                direct_spot_donor(AB + NWD + NDISC, sbw, DONp, ph, h, e0, e1, c, itb, eb, D);
+                const double2 ed2 = direct_spot_donor(AB + NWD + NDISC, sbw, DONp, ph, h, e0, e1, cg, snorm[0]);
+                eb = ed2.x;
+                D = ed2.y;
             }
             double beam = 0.0;
-            if (bden > 0.0) beam = (fis + (1.0 - fis) * fmax(nb0 * e0 + nb1 * e1 + nb2 * c, 0.0)) / bden;
+            const double bden = SG[G_BDEN], fis = SG[G_FIS];
+            if (bden > 0.0)
+                beam = (fis + (1.0 - fis) * fmax(SG[G_NB0] * e0 + SG[G_NB1] * e1 + SG[G_NB2] * cg, 0.0)) / bden;
             sbs += beam * (1.0 - eb);
-            srs += D / dn;
+            srs += D / snorm[2];
             __syncthreads();  // the next pass rewrites the tile buffers
         }
         if (own) {
-            const double fwv = wdF * (1.0 - fw), fdv = dF * (1.0 - fd);
-            const double fb = sF * sbs / S, fr = rsF * srs / S;
+            const double fwv = SG[G_WDF] * (1.0 - fw), fdv = SG[G_DF] * (1.0 - fd);
+            const double fb = SG[G_SF] * sbs / S, fr = SG[G_RSF] * srs / S;
             const double f = fwv + fdv + fb + fr;
             const int pi = t0 + tid;
             if (L.flux) L.flux[size_t(pair) * n + pi] = f;
@@ -1281,7 +1337,7 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
                 L.comps[(size_t(3) * L.npairs + pair) * n + pi] = fr;
             }
             if (CHI && !GP) {
-                const double r = (py - f) / pye;
+                const double r = (L.y[p] - f) / L.ye[p];  // loaded here: no registers held over the passes
                 chi += isnan(f) ? INFINITY : r * r;
             }
         }
@@ -1290,9 +1346,10 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
             // after the last pass); wave 0 carries the filter across tiles
             if (own) {
                 TB.lo[tid] = px;
-                TB.hi[tid] = pye;
-                TB.iw[tid] = py - (wdF * (1.0 - fw) + dF * (1.0 - fd) + sF * sbs / S + rsF * srs / S);
-                TB.cell[tid] = gp_block(px, L.gp_ecl[2 * e], L.gp_ecl[2 * e + 1], G[G_GP_DCP], phi0);
+                TB.hi[tid] = L.ye[p];
+                TB.iw[tid] = L.y[p] - (SG[G_WDF] * (1.0 - fw) + SG[G_DF] * (1.0 - fd) + SG[G_SF] * sbs / S +
+                                   SG[G_RSF] * srs / S);
+                TB.cell[tid] = gp_block(px, L.gp_ecl[2 * e], L.gp_ecl[2 * e + 1], SG[G_GP_DCP], SG[G_PHI0]);
             }
             __syncthreads();
             if (wv == 0) {
