@@ -1082,7 +1082,7 @@ __device__ inline void finish_walker(const LikeArgs& L, int pair, int tid, bool 
 // ln_like of the residuals (a Kalman filter over each tile's sorted points,
 // run by wave 0 while the other waves wait at the tile barrier)
 template <int MODE>
-__global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
+__global__ __launch_bounds__(LIKE_THREADS, (MODE == 2) ? 1 : LIKE_MINW) void k_lnlike(LikeArgs L)
 {
     constexpr bool CHI = MODE != 0, GP = MODE == 2;
 #ifdef LFG_PROFILE_LIKE
