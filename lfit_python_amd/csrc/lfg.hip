@@ -33,6 +33,14 @@ constexpr int ELEM_BLOCK = 256;
 // per-pair weight block written by k_elements: disc ring weights, the disc
 // total 2 pi [P(rdisc) - P(rin)], spot element weights
 constexpr int WT_DISC = 0, WT_TD = NDISC_R, WT_BS = 24, WT_N = WT_BS + NBS;
+// WD/disc eclipse intervals are stored in sweep order: slot g of a pair's
+// interval table holds element sweep_item(g) (stride-37 permutation: a wave's
+// 64 lanes sweep elements of different rings, so their LDS atomics spread),
+// and k_lnlike reads its items as coalesced rows; slot_of inverts it
+// (37 * 1173 = 1 mod 1400).  Spot elements keep their own slots.
+__device__ __forceinline__ int sweep_item(int g) { return g < NWD + NDISC ? (g * 37) % (NWD + NDISC) : g; }
+__device__ __forceinline__ int slot_of(int k) { return k < NWD + NDISC ? (k * 1173) % (NWD + NDISC) : k; }
+static_assert(NWD + NDISC == 1400 && (37 * 1173) % 1400 == 1, "sweep permutation inverse");
 // per unique donor tile: vx, vy, vz, arc centre, arc half-width (phase units)
 constexpr int DON_STRIDE = 5;
 
@@ -514,10 +522,10 @@ __global__ __launch_bounds__(ELEM_BLOCK, ELEM_MINW) void k_elements(const double
     element_interval_fast(R, Px, Py, Pz, s, c, G[G_RCAL], G[G_REFF], a, b);
 #endif
     const size_t o = size_t(pair) * NEL;
-    AB[o + k] = make_double2(a, b);
+    AB[o + slot_of(k)] = make_double2(a, b);
     if (km != k) {
         const bool ecl = a < b;
-        AB[o + km] = ecl ? make_double2(-b, -a) : make_double2(1.0, -1.0);
+        AB[o + slot_of(km)] = ecl ? make_double2(-b, -a) : make_double2(1.0, -1.0);
     }
 }
 
@@ -530,7 +538,7 @@ __global__ void k_expand(const double* __restrict__ geo, const int* __restrict__
     const int pair = int(t / NEL), k = int(t - long(pair) * NEL);
     if (pair >= npairs || status[pair] != ST_OK) return;
     const double* G = geo + size_t(pair) * LFG_NGEO;
-    const double2 ab = AB[size_t(pair) * NEL + k];
+    const double2 ab = AB[size_t(pair) * NEL + slot_of(k)];
     if (A) A[size_t(pair) * NEL + k] = ab.x;
     if (B) B[size_t(pair) * NEL + k] = ab.y;
     double w;
@@ -866,7 +874,6 @@ __device__ __forceinline__ void apply_runs(const Runs& R, double a, double b, do
 // WD/disc element of sweep slot g: a stride-37 permutation of [0, NWD + NDISC)
 // so that the lanes of a wave take elements of different rings and azimuths
 // (their runs start at different points: fewer same-address LDS atomics)
-__device__ __forceinline__ int sweep_item(int g) { return g < NWD + NDISC ? (g * 37) % (NWD + NDISC) : g; }
 
 // ring of WD/disc element k: WD ring r holds 4 r^2 <= k < 4 (r + 1)^2, disc
 // rings follow (NDISC_AZ elements each)
@@ -1007,7 +1014,7 @@ __device__ __noinline__ double2 direct_wd_disc(const double2* __restrict__ AB, c
         const int k1 = ring < NWD_RINGS ? 4 * (ring + 1) * (ring + 1) : k0 + NDISC_AZ;
         double acc = 0.0;
         for (int k = k0; k < k1; ++k) {
-            const double2 ab = AB[k];
+            const double2 ab = AB[slot_of(k)];
             acc += (wk > 0.0) ? fmax(fmin(ab.y, hi) - fmax(ab.x, lo), 0.0)
                               : ((phc > ab.x && phc < ab.y) ? 1.0 : 0.0);
         }
@@ -1152,8 +1159,8 @@ __global__ __launch_bounds__(LIKE_THREADS, (MODE == 2) ? 1 : LIKE_MINW) void k_l
     constexpr int NI = (NWD + NDISC + nt - 1) / nt;
     double2 abk[NI];
     for (int i = 0; i < NI; ++i) {
-        const int k = sweep_item(tid + i * nt);
-        abk[i] = (k < NWD + NDISC) ? AB[k] : make_double2(1.0, -1.0);
+        const int g = tid + i * nt;
+        abk[i] = (g < NWD + NDISC) ? AB[g] : make_double2(1.0, -1.0);
     }
     double2 abB = make_double2(1.0, -1.0);
     double wB = 0.0;
