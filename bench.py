@@ -107,12 +107,21 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # LFG_BENCH_BACKEND=gloo rehearses the multi-rank flow with every rank on
+    # the GPUs there are (e.g. two ranks on a one-GPU box); the driver's runs
+    # use RCCL ("nccl"), one rank per GPU
+    backend = os.environ.get("LFG_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local %= torch.cuda.device_count()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from lfit_python_amd import _native, batch, sampler, synthetic
     from lfit_python_amd.lfit import flux_batch

@@ -67,6 +67,16 @@ struct Roche {
     double q, cA, cB, mu, xl1, pl1, Rs, Rs2;
 };
 
+// 1/sqrt(x) for finite x > 0: v_rsq_f64 and one third-order correction (the
+// ocml form without its zero/infinity select, which adds a dependent level;
+// a lone stream wave is bound by dependent FP64 latency, ~30 cycles a level)
+__device__ __forceinline__ double rsqrt_pos(double x)
+{
+    const double y = __builtin_amdgcn_rsq(x);
+    const double e = fma(-x * y, y, 1.0);
+    return fma(y * e, fma(e, 0.375, 0.5), y);
+}
+
 __device__ __forceinline__ double rpot(const Roche& R, double x, double y, double z)
 {
     const double dx = x - 1.0;
@@ -301,10 +311,10 @@ __device__ __forceinline__ void cone_point(const Roche& R, double Px, double Py,
     const double ex = s * cs, ey = -s * sn;
     const double x = fma(t, ex, Px), y = fma(t, ey, Py), z = fma(t, c, Pz);
     const double r1s = x * x + y * y + z * z;
-    const double ir1 = rsqrt(r1s), ir1s = ir1 * ir1;
+    const double ir1 = rsqrt_pos(r1s), ir1s = ir1 * ir1;
     const double dx = x - 1.0;
     const double r2s = dx * dx + y * y + z * z;
-    const double ir2 = rsqrt(r2s), ir2s = ir2 * ir2;
+    const double ir2 = rsqrt_pos(r2s), ir2s = ir2 * ir2;
     const double i1 = R.cA * ir1s * ir1, i2 = R.cB * ir2s * ir2, i12 = i1 + i2;
     const double xm = x - R.mu;
     o.phi = -R.cA * ir1 - R.cB * ir2 - xm * xm - y * y;
@@ -574,10 +584,10 @@ __device__ inline int findi_fast(const Roche& R, double dphi, double& inc_deg)
                 const double ex = s * cth, ey = -s * sth;
                 const double x = t * ex, y = t * ey, z = t * c;
                 const double r1s = x * x + y * y + z * z;
-                const double ir1 = rsqrt(r1s), ir1s = ir1 * ir1;
+                const double ir1 = rsqrt_pos(r1s), ir1s = ir1 * ir1;
                 const double dx = x - 1.0;
                 const double r2s = dx * dx + y * y + z * z;
-                const double ir2 = rsqrt(r2s), ir2s = ir2 * ir2;
+                const double ir2 = rsqrt_pos(r2s), ir2s = ir2 * ir2;
                 const double i1 = R.cA * ir1s * ir1, i2 = R.cB * ir2s * ir2, i12 = i1 + i2;
                 const double xm = x - R.mu;
                 const double phi = -R.cA * ir1 - R.cB * ir2 - xm * xm - y * y;
@@ -618,10 +628,10 @@ struct StreamState { double x, y, vx, vy; };
 __device__ __forceinline__ StreamState stream_deriv(const Roche& R, const StreamState& s)
 {
     const double m1 = 0.5 * R.cA, m2 = 0.5 * R.cB;
-    const double ir1 = rsqrt(s.x * s.x + s.y * s.y);
+    const double ir1 = rsqrt_pos(s.x * s.x + s.y * s.y);
     const double i1 = m1 * ir1 * ir1 * ir1;
     const double dx = s.x - 1.0;
-    const double ir2 = rsqrt(dx * dx + s.y * s.y);
+    const double ir2 = rsqrt_pos(dx * dx + s.y * s.y);
     const double i2 = m2 * ir2 * ir2 * ir2;
     const double Ux = i1 * s.x + i2 * dx - (s.x - R.mu);
     const double Uy = (i1 + i2 - 1.0) * s.y;
@@ -676,9 +686,14 @@ __device__ inline StreamState stream_start(const Roche& R)
 __device__ inline int bspot(const Roche& R, double rad, double out[4])
 {
     if (!(rad > 0.0) || !(rad < R.xl1)) return ST_BAD_STREAM;
+    // the loop tests squared radii: the exit branch waits on one fma level,
+    // not on a sqrt (~5 dependent levels); r itself only sets the next dt,
+    // which runs beside k1
     StreamState s = stream_start(R);
-    double r = sqrt(s.x * s.x + s.y * s.y);
+    double r2c = s.x * s.x + s.y * s.y;
+    const double rad2 = rad * rad;
     for (int n = 0; n < STREAM_MAXSTEP; ++n) {
+        const double r = sqrt(r2c);
         const double dt = fmin(STREAM_KAPPA * r * sqrt(r), STREAM_DTMAX);
         const StreamState k1 = stream_deriv(R, s);
         const StreamState k2 = stream_deriv(R, axpy(s, 0.5 * dt, k1));
@@ -689,10 +704,10 @@ __device__ inline int bspot(const Roche& R, double rad, double out[4])
                        s.y + h6 * (k1.y + 2.0 * k2.y + 2.0 * k3.y + k4.y),
                        s.vx + h6 * (k1.vx + 2.0 * k2.vx + 2.0 * k3.vx + k4.vx),
                        s.vy + h6 * (k1.vy + 2.0 * k2.vy + 2.0 * k3.vy + k4.vy)};
-        const double rn = sqrt(sn.x * sn.x + sn.y * sn.y);
-        if (rn < rad) {  // Hermite crossing, safeguarded Newton on |H|^2 - rad^2
-            const double r2 = rad * rad;
-            const double f0 = r * r - r2, f1 = rn * rn - r2;
+        const double rn2 = sn.x * sn.x + sn.y * sn.y;
+        if (rn2 < rad2) {  // Hermite crossing, safeguarded Newton on |H|^2 - rad^2
+            const double r2 = rad2;
+            const double f0 = r2c - r2, f1 = rn2 - r2;
             double lo = 0.0, hi = 1.0, tau = f0 / (f0 - f1), p[4];
             for (int it = 0; it < 100; ++it) {
                 hermite(s, sn, dt, tau, p);
@@ -707,9 +722,9 @@ __device__ inline int bspot(const Roche& R, double rad, double out[4])
             hermite(s, sn, dt, tau, out);
             return ST_OK;
         }
-        if (rn > r && n > 0) return ST_BAD_STREAM;
+        if (rn2 > r2c && n > 0) return ST_BAD_STREAM;
         s = sn;
-        r = rn;
+        r2c = rn2;
     }
     return ST_BAD_STREAM;
 }
