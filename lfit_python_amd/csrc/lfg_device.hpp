@@ -360,6 +360,16 @@ struct Tan {
     int st;
 };
 
+// 1/x for finite x != 0: v_rcp_f64 and one Newton correction (the IEEE
+// quotient's div_scale/div_fmas/div_fixup sequence is ~10 issue slots; a
+// Newton step only needs its length to a few ulp -- the root it converges to
+// is fixed by F = 0, not by the step)
+__device__ __forceinline__ double rcp_fast(double x)
+{
+    const double y = __builtin_amdgcn_rcp(x);
+    return fma(y, fma(-x, y, 1.0), y);
+}
+
 // one branch-free step (two solves can run interleaved in one lane)
 __device__ __forceinline__ void tangency_step(const Roche& R, double Px, double Py, double Pz, double s, double c,
                                               bool ingress, Tan& T)
@@ -371,7 +381,7 @@ __device__ __forceinline__ void tangency_step(const Roche& R, double Px, double 
     const double J21 = T.t * o.etHe + o.gth, J22 = o.eHe;
     const double det = J11 * J22 - J12 * J21;
     const bool bad = !(det != 0.0);
-    const double idet = 1.0 / det;
+    const double idet = rcp_fast(det);
     double dth = -(F1 * J22 - o.F2 * J12) * idet;
     const double dt = -(J11 * o.F2 - J21 * F1) * idet;
     dth = fmin(fmax(dth, -0.05), 0.05);
@@ -425,7 +435,7 @@ __device__ inline int cone_exists(const Roche& R, double Px, double Py, double P
         const double Htt = o.eHe, Hht = o.gth + t * o.etHe, Hhh = t * t * o.ethHeth + t * o.gtt;
         const double det = Hhh * Htt - Hht * Hht;
         if (!(Hhh > 0.0 && Htt > 0.0 && det > 0.0)) return -1;
-        const double idet = 1.0 / det;
+        const double idet = rcp_fast(det);
         double dth = -(Htt * Gth - Hht * Gt) * idet;
         double dt = -(Hhh * Gt - Hht * Gth) * idet;
         const double big = fmax(fabs(dth), fabs(dt));
