@@ -291,7 +291,10 @@ def main():
                                       else "single eclipse", args.npts, args.nsub, args.walkers),
                        "walkers_total": W, "eclipses": E, "ndim": tree.ndim,
                        "parallelism": "walker shards x%d, replicated Philox RNG, "
-                                      "all_gather of ln_prob per half-step" % world,
+                                      "all_gather of ln_prob per half-step (%s)" % (
+                                          world, "ncclAllGather on the compute stream"
+                                          if os.environ.get("LFG_RCCL_DIRECT", "1") != "0"
+                                          else "torch ProcessGroupNCCL"),
                        },
             "roofline": {"bound": "hbm", "kernel": kname, "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,

@@ -13,6 +13,7 @@ each half and exchanges W/2 doubles per half-step; the accept step is then
 identical on every rank, so positions never travel.
 """
 import ctypes
+import os
 
 import numpy as np
 
@@ -130,6 +131,7 @@ class EnsembleSampler:
         self.force_shard = False
         self.shard_timer = None
         self._q_sh = self._zf_sh = self._lnp_sh = None
+        self._rccl = None  # direct RCCL all-gather (built at the first nccl exchange)
         # HIP-graph replay of whole iterations (single rank, HIP ops): the first
         # step() after enabling runs eagerly, the next captures, later ones replay
         self.use_graph = False
@@ -141,6 +143,18 @@ class EnsembleSampler:
     def _gather(self, out, mine):
         import torch.distributed as dist
         if dist.get_backend(self.group) == "nccl":
+            # ncclAllGather on the kernels' own stream (comm.py); LFG_RCCL_DIRECT=0
+            # keeps torch's ProcessGroupNCCL path (its stream hand-off ~6 us more)
+            if self._rccl is None:
+                direct = os.environ.get("LFG_RCCL_DIRECT", "1") != "0"
+                if direct:
+                    from .comm import RcclAllGather
+                    self._rccl = RcclAllGather(self.group)
+                else:
+                    self._rccl = False
+            if self._rccl:
+                self._rccl(out, mine)
+                return
             dist.all_gather_into_tensor(out, mine, group=self.group)
         else:
             dist.all_gather(list(out.chunk(self.world)), mine, group=self.group)

@@ -96,3 +96,14 @@ def test_product_path_fails_loudly_without_gpu():
         lfit.CV(TRUTH18).calcFlux(TRUTH18, np.linspace(-0.1, 0.1, 11))
     with pytest.raises(RuntimeError, match="GPU"):
         roche.xl1(0.1)
+
+
+def test_rccl_unique_id_round_trip_keeps_nul_bytes():
+    # the id travels as bytes through broadcast_object_list (comm.py); a NUL
+    # inside it must not truncate it
+    from lfit_python_amd import comm
+    raw = bytes([7, 0, 9]) + bytes(range(125))
+    uid = comm.uid_from(raw)
+    assert comm.uid_bytes(uid) == raw
+    with pytest.raises(ValueError):
+        comm.uid_from(raw[:100])
