@@ -57,7 +57,7 @@ PER_PAIR = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100)  # ~20 ms timed: one host hiccup stays small
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=2, choices=(2, 3, 5),
                     help="BASELINE.json config: 2 (the metric's, default), 3 (3-band x 4-eclipse tree, "
