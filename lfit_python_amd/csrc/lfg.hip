@@ -1295,8 +1295,9 @@ __global__ __launch_bounds__(LIKE_THREADS, (MODE == 2) ? 1 : LIKE_MINW) void k_l
             }
             __syncthreads();
             LIKE_STAMP(3);
-            long long r[6];
-            block_scan<6>(sacc, spart, tid, r);
+            long long r[6] = {0, 0, 0, 0, 0, 0};
+            if (j == 0) block_scan<6>(sacc, spart, tid, r);
+            else block_scan<4>(sacc + 2, spart + 2, tid, r + 2);  // sub-bin passes: spot and donor only
             LIKE_STAMP(4);
             if (j == 0) {
                 if (swA) {
