@@ -1330,7 +1330,11 @@ __global__ __launch_bounds__(LIKE_THREADS, (MODE == 2) ? 1 : LIKE_MINW) void k_l
                 beam = (fis + (1.0 - fis) * fmax(SG[G_NB0] * e0 + SG[G_NB1] * e1 + SG[G_NB2] * cg, 0.0)) / bden;
             sbs += beam * (1.0 - eb);
             srs += D / snorm[2];
-            __syncthreads();  // the next pass rewrites the tile buffers
+            // no barrier before the next pass rewrites the tile buffers: every
+            // read of TA/TB/sph/scp/sacc/sflag of this pass precedes the
+            // block scan's barriers (after them only registers, part[] and
+            // the pass-invariant LDS are read, none of which the next
+            // pass's prologue writes)
         }
         if (own) {
             const double fwv = SG[G_WDF] * (1.0 - fw), fdv = SG[G_DF] * (1.0 - fd);
