@@ -70,6 +70,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--exchange-path", action="store_true",
+                    help="one GPU: a one-rank RCCL group and the multi-rank code path with its real "
+                         "exchange (shard kernels, ncclAllGather on the compute stream, k_accept_regen)")
     ap.add_argument("--seed", type=int, default=20261015)
     ap.add_argument("--time-every", type=int, default=4,
                     help="record the dominant kernel's event pair on every k-th ln_prob call of the timed region")
@@ -116,9 +119,16 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
-    if world > 1:
+    if args.exchange_path and world == 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29541")
+        args.shard_path = True
+    if world > 1 or args.exchange_path:
         import torch.distributed as dist
-        if backend == "nccl":
+        if world == 1:
+            dist.init_process_group(backend, rank=0, world_size=1,
+                                    **({"device_id": dev} if backend == "nccl" else {}))
+        elif backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
@@ -146,6 +156,7 @@ def main():
         p0, scat, W, lambda p: ev(torch.as_tensor(p, device=dev)).cpu().numpy(), seed=args.seed)
     S = sampler.EnsembleSampler(W, tree.ndim, ev, seed=args.seed)
     S.force_shard = args.shard_path
+    S.force_exchange = args.exchange_path
     S.set_state(init)
 
     # HIP events around kernels of lfg_lnprob calls (include/lfg.h LFG_NEV)
@@ -309,6 +320,7 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))
+    S.close()
     if dist:
         dist.destroy_process_group()
 

@@ -129,6 +129,7 @@ class EnsembleSampler:
         # (lfg_stretch_accept_regen); shard_timer replaces evaluator.step_shard
         self.fuse_shard = hasattr(evaluator, "step_shard") and isinstance(self.ops, HipStretchOps)
         self.force_shard = False
+        self.force_exchange = False  # one rank: still exchange through the collective (rehearsal)
         self.shard_timer = None
         self._q_sh = self._zf_sh = self._lnp_sh = None
         self._rccl = None  # direct RCCL all-gather (built at the first nccl exchange)
@@ -267,12 +268,19 @@ class EnsembleSampler:
         f = self.shard_timer or self.ev.step_shard
         f(self.pos, half, self.a, self.seed, self.iteration, self.rank * self.shard, self._q_sh, self._zf_sh,
           self._lnp_sh)
-        if self.world > 1:
+        if self.world > 1 or self.force_exchange:
             self._gather(self.lnp_new, self._lnp_sh)
         else:
             self.lnp_new.copy_(self._lnp_sh)
         self.ops.accept_regen(self.pos, self.lnp, half, self.a, self.lnp_new, self.seed, self.iteration,
                               self.naccept)
+
+    def close(self):
+        """Release the direct RCCL communicator (every rank, before the
+        process group is destroyed)."""
+        if self._rccl:
+            self._rccl.close()
+        self._rccl = None
 
     def run_mcmc(self, p0, nsteps, store=True, lnp0=None):
         """emcee-style run; returns (pos, lnp) as numpy.  With store=True the

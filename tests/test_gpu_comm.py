@@ -71,4 +71,5 @@ def test_sampler_exchange_uses_direct_rccl(nccl_world1):
     torch.cuda.synchronize()
     assert isinstance(S._rccl, RcclAllGather)
     assert torch.equal(out, mine)
-    S._rccl.close()
+    S.close()
+    assert S._rccl is None
