@@ -139,6 +139,7 @@ def run(input_file, quiet=False, debug=False, seed=0, chain_file="chain_prod.txt
         first = False
         done += k
     acc = float(np.mean(S.acceptance_fraction))
+    S.close()  # the direct RCCL communicator, before the process group goes
     say("Mean acceptance fraction: {:.3f}".format(acc))
     return {"chain_file": chain_file, "acceptance": acc, "nwalkers": nwalkers, "npars": npars, "nprod": nprod}
 
