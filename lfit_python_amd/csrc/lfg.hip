@@ -402,8 +402,16 @@ __global__ __launch_bounds__(ELEM_BLOCK, ELEM_MINW) void k_elements(const double
     // the stream lanes' status into the pair status (MODEL_SPEC 6 order:
     // setup failures first); every item skips a pair that failed either.
     const int pair = int(blockIdx.x % unsigned(npairs));
-    const int u = int(blockIdx.x / unsigned(npairs)) * int(blockDim.x) + int(threadIdx.x);
-    if (u >= NUNIQ) return;
+    const int v = int(blockIdx.x / unsigned(npairs)) * int(blockDim.x) + int(threadIdx.x);
+    if (v >= NUNIQ) return;
+#ifndef LFG_EXP_OLDORDER
+    // launch order WD, disc, spot, donor: the last chunk, dispatched last,
+    // holds the cheap donor items (one 1-D root) instead of spot tangencies
+    constexpr int V_BS = U_WD + U_DISC;
+    const int u = (v < V_BS) ? v : (v < V_BS + U_BS ? U_MAIN + (v - V_BS) : v - U_BS);
+#else
+    const int u = v;
+#endif
 #if defined(LFG_EXP_NODONOR)  // experiment builds: time one region alone
     if (u >= U_WD + U_DISC && u < U_MAIN) return;
 #elif defined(LFG_EXP_ONLYDONOR)
