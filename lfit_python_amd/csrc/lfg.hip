@@ -26,7 +26,10 @@ using namespace lfg;
 namespace {
 
 constexpr int SETUP_BLOCK = 64;
-constexpr int ELEM_BLOCK = 256;
+#ifndef LFG_ELEM_BLOCK
+#define LFG_ELEM_BLOCK 64  // one wave: the item chunks dispatch at wave granularity (36.0 vs 37.6 us at 256, 36.5 at 128)
+#endif
+constexpr int ELEM_BLOCK = LFG_ELEM_BLOCK;
 #ifndef ELEM_MINW
 #define ELEM_MINW 1  // minimum waves per SIMD of k_elements
 #endif
