@@ -303,9 +303,11 @@ def main():
                        "walkers_total": W, "eclipses": E, "ndim": tree.ndim,
                        "parallelism": "walker shards x%d, replicated Philox RNG, "
                                       "all_gather of ln_prob per half-step (%s)" % (
-                                          world, "ncclAllGather on the compute stream"
-                                          if os.environ.get("LFG_RCCL_DIRECT", "1") != "0"
-                                          else "torch ProcessGroupNCCL"),
+                                          world, "one rank: no exchange" if dist is None
+                                          else ("%s all_gather" % backend if backend != "nccl"
+                                                else ("ncclAllGather on the compute stream"
+                                                      if os.environ.get("LFG_RCCL_DIRECT", "1") != "0"
+                                                      else "torch ProcessGroupNCCL"))),
                        },
             "roofline": {"bound": "hbm", "kernel": kname, "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
