@@ -265,7 +265,9 @@ def main():
 
     # counter-derived traffic and executed FP64 FLOPs of the same kernel
     # (rocprofv3 --pmc passes, tools/pmc_profile.sh -> profiles/r01/pmc_traffic.json)
-    row, meta = pmc_row(kname)
+    # the committed PMC pass is of the default workload (config 2, 300 points,
+    # nsub 1); per-pair counters do not carry over to other point counts
+    row, meta = pmc_row(kname) if (args.config == 2 and args.npts == 300 and args.nsub == 1) else (None, None)
     traffic = fp64 = None
     if row and meta:
         scale = shard * E / float(meta.get("pairs_per_launch", shard * E))
