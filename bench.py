@@ -7,24 +7,44 @@ A step is one emcee iteration of the whole ensemble: two half-steps of
 propose -> batched ln_prob of the proposals (k_setup, k_elements, k_lnlike)
 -> accept.  On one GPU a half-step is those three kernels alone
 (lfg_stretch_step_half: the proposal formed in k_setup, the acceptance in
-k_lnlike); with N ranks each proposes, evaluates its shard (lfg_lnprob),
-all_gathers ln_prob, and every rank accepts.  value = walkers x steps /
-time, max over ranks, inputs resident in HBM.  Per-GPU work is fixed (weak
-scaling): --walkers per GPU, total = walkers x N.
+k_lnlike); with N ranks each rank evaluates its shard of the half
+(lfg_stretch_step_shard), ncclAllGather's the shard's ln_prob on the compute
+stream, and every rank accepts (lfg_stretch_accept_regen).  value = walkers
+x steps / time, max over ranks, inputs resident in HBM.
+
+Configs (BASELINE.json):
+  2   1024 walkers per GPU, weak scaling (the metric's config; default)
+  3   3-band x 4-eclipse tree, 2048 walkers per GPU, weak
+  4   the 16384-walker ensemble sharded over the N GPUs: strong scaling
+      (16384 / N walkers per GPU; at N = 8, 2048 per GPU)
+  5   10000 points x 5 sub-samples, 4096 walkers per GPU, weak
+  gp  the reference's shipped useGP = 1 example (87 parameters, 6 eclipses,
+      its real light curves), 1024 walkers per GPU, weak
+
+Launch: `python bench.py --gpus N` with N > 1 spawns N rank processes itself
+(before anything touches the GPU), one per GPU; under torchrun WORLD_SIZE
+must equal --gpus.
 
 Kernel timing: the last warmup step records HIP events around every kernel
 (include/lfg.h LFG_NEV, on the caller stream all kernels run on) and picks
-the dominant kernel; every ln_prob call of the timed region then records a
-start/stop event pair around that kernel only.  (A timing event is a queue barrier: events around all kernels
-cost ~20 % of the step, so they stay out of the timed region.)
+the dominant kernel; in the timed region every --time-every-th ln_prob call
+records a start/stop event pair around that kernel only.  (A timing event is
+a queue barrier: events around all kernels cost ~20 % of the step, so they
+stay out of the timed region.)
 
-  python bench.py [--gpus N --steps K --warmup W]
-  torchrun --nproc-per-node N bench.py --gpus N ...
+Roofline (MODEL_SPEC.md section 11): the path is FP64-VALU bound.  Achieved
+= walker evals/s per GPU x E x the counted algorithmic FLOPs per
+walker-eclipse evaluation (F_setup + 900 roots x F_geom + N S (1500 x 3 +
+400 x 6 + 40)), against the 78.6 TFLOP/s FP64 vector peak.  The HBM
+fraction uses SURVEY.md 8(d)'s bytes (8 ndim + 8 per walker, 32 N per
+eclipse per launch); the element tables the kernels hand each other are
+reported apart as materialised bytes.
 """
 import argparse
 import ctypes
 import json
 import os
+import socket
 import sys
 import time
 
@@ -36,39 +56,68 @@ sys.path.insert(0, ROOT)
 # MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md; FP64 vector = spec)
 HBM_PEAK_GBS = 8000.0
 FP64_PEAK_TFLOPS = 78.6
-PMC_FILE = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
+PMC_FILES = [os.path.join(ROOT, "profiles", r, "pmc_traffic.json") for r in ("r02", "r01")]
 
 NEV = 4  # LFG_NEV (include/lfg.h)
 # (name as rocprofv3 prints it, start event, end event)
-KERNELS = [("k_setup", 0, 1), ("k_elements", 1, 2), ("k_lnlike<1>", 2, 3)]
+KERNELS = [("k_setup", 0, 1), ("k_elements", 1, 2), ("k_lnlike", 2, 3)]
 
-# Algorithmic HBM bytes per (walker, eclipse) pair of each kernel (DESIGN.md
-# section 3): what the kernel must read and write, counted once.
+# Counted algorithmic FP64 work per walker-eclipse evaluation (MODEL_SPEC.md
+# section 11; tools/flop_count.py -> profiles/r02/flops_c2.json, the config-2
+# walker ball): setup + stream + prior lanes, per element root (900
+# symmetry-unique roots per pair), and the direct-form accumulation per
+# element per point per sub-phase
+F_SETUP = 7555.0
+F_GEOM_ROOT = 1309.0
+N_ROOTS = 900
+F_ACC_ECL, F_ACC_DON, F_POINT = 3.0, 6.0, 40.0
+N_ECL, N_DON = 1500, 400
+F_GP_POINT = 150.0   # one Kalman step (MODEL_SPEC 10.4)
+
+# builder's intermediate tables per (walker, eclipse) pair:
+# what each kernel reads and writes of the tables the kernels hand each other
 NEL, U_DON, DON_STRIDE = 1500, 100, 5
-GEO_SETUP, GEO_BSPOT, GEO_READ = 41, 5, 40   # geometry doubles written / read
-WT_N = 124                                     # weight doubles per pair
-PER_PAIR = {
-    "k_setup": 18 * 8 + GEO_SETUP * 8 + 4 + 3 * 8 + GEO_BSPOT * 8 + 4,   # setup + stream lanes
+GEO_SETUP, GEO_BSPOT, GEO_READ = 41, 5, 40
+WT_N = 124
+MATERIALISED_PER_PAIR = {
+    "k_setup": 18 * 8 + GEO_SETUP * 8 + 4 + 3 * 8 + GEO_BSPOT * 8 + 4,
     "k_elements": GEO_READ * 8 + 8 + NEL * 16 + U_DON * DON_STRIDE * 8 + WT_N * 8,
-    "k_lnlike<1>": GEO_READ * 8 + 4 + NEL * 16 + U_DON * DON_STRIDE * 8 + WT_N * 8 + 8,
+    "k_lnlike": GEO_READ * 8 + 4 + NEL * 16 + U_DON * DON_STRIDE * 8 + WT_N * 8 + 8,
+}
+
+CONFIGS = {
+    "2": dict(walkers=1024, npts=300, nsub=1, scaling="weak",
+              desc="config 2: single eclipse, complex 18-par bright spot, %d phase pts, nsub %d, "
+                   "%d walkers/GPU, emcee stretch move"),
+    "3": dict(walkers=2048, npts=300, nsub=1, scaling="weak",
+              desc="config 3: 3-band x 4-eclipse tree (shared q/dphi/rwd), complex bright spot, %d phase pts "
+                   "per eclipse, nsub %d, %d walkers/GPU"),
+    "4": dict(walkers_total=16384, npts=300, nsub=1, scaling="strong",
+              desc="config 4: 16384-walker ensemble sharded over the GPUs, single eclipse, complex bright spot, "
+                   "%d phase pts, nsub %d, %d walkers/GPU"),
+    "5": dict(walkers=4096, npts=10000, nsub=5, scaling="weak",
+              desc="config 5: single eclipse, complex bright spot, %d phase pts, nsub %d sub-samples, "
+                   "%d walkers/GPU"),
+    "gp": dict(walkers=1024, npts=None, nsub=1, scaling="weak",
+               desc="the reference's useGP = 1 example (test_data/mcmc_input.dat: 87 parameters, 3 bands x 2 "
+                    "eclipses, its real light curves, Matern-3/2 GP likelihood), %s pts, nsub %d, %d walkers/GPU"),
 }
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks); N > 1 without torchrun spawns the N ranks here")
     ap.add_argument("--steps", type=int, default=100)  # ~20 ms timed: one host hiccup stays small
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 5),
-                    help="BASELINE.json config: 2 (the metric's, default), 3 (3-band x 4-eclipse tree, "
-                         "2048 walkers), 5 (10000 points x 5 sub-samples, 4096 walkers)")
+    ap.add_argument("--config", default="2", choices=sorted(CONFIGS), help="BASELINE.json config (see above)")
     ap.add_argument("--walkers", type=int, default=None, help="walkers per GPU (default: the config's)")
     ap.add_argument("--npts", type=int, default=None)
     ap.add_argument("--nsub", type=int, default=None)
     ap.add_argument("--shard-path", action="store_true",
                     help="run the multi-rank half-step (lfg_stretch_step_shard + accept_regen) on one rank")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: every core this process may run on")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--exchange-path", action="store_true",
                     help="one GPU: a one-rank RCCL group and the multi-rank code path with its real "
@@ -76,36 +125,90 @@ def parse():
     ap.add_argument("--seed", type=int, default=20261015)
     ap.add_argument("--time-every", type=int, default=4,
                     help="record the dominant kernel's event pair on every k-th ln_prob call of the timed region")
-    args = ap.parse_args()
-    dflt = {2: (1024, 300, 1), 3: (2048, 300, 1), 5: (4096, 10000, 5)}[args.config]
-    args.walkers = args.walkers or dflt[0]
-    args.npts = args.npts or dflt[1]
-    args.nsub = args.nsub or dflt[2]
+    args = ap.parse_args(argv)
+    cfg = CONFIGS[args.config]
+    args.npts = args.npts or cfg["npts"]
+    args.nsub = args.nsub or cfg["nsub"]
     return args
 
 
-def algo_bytes(kernel, pairs, walkers, ndim, E, npts):
-    b = PER_PAIR[kernel] * pairs
-    if kernel == "k_setup":
-        b += walkers * (ndim * 8 + 8)          # per-walker prior lane
-    if kernel == "k_lnlike<1>":
-        b += E * npts * 4 * 8                   # x, y, ye, w once per launch
-        b += walkers * (8 * 2 + E * 8 * 2)      # fused combine: prior, lnp; 2 Roche priors per eclipse
-    return b
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _rank_entry(rank, argv, world, port):
+    """One spawned rank (fresh interpreter, nothing touched the GPU before)."""
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    run(parse(argv))
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if args.gpus is not None and int(env_world) != args.gpus:
+            sys.exit("bench.py: WORLD_SIZE=%s but --gpus %d" % (env_world, args.gpus))
+        return run(args)
+    n = args.gpus or 1
+    if n == 1:
+        return run(args)
+    # N ranks, one per GPU, spawned before any HIP call in this process
+    import torch.multiprocessing as mp
+    mp.start_processes(_rank_entry, args=(argv, n, _free_port()), nprocs=n, join=True, start_method="spawn")
+    return 0
+
+
+def walker_count(args, world):
+    cfg = CONFIGS[args.config]
+    if args.walkers:
+        return args.walkers
+    if "walkers_total" in cfg:
+        tot = cfg["walkers_total"]
+        if tot % (2 * world):
+            raise SystemExit("config 4: 16384 walkers do not shard over %d ranks" % world)
+        return tot // world
+    return cfg["walkers"]
+
+
+def build_model(args, flux_fn):
+    from lfit_python_amd import cvmodel, synthetic
+    if args.config == "gp":
+        return cvmodel.construct_model(os.path.join(ROOT, "tests", "golden", "ref_test_data", "mcmc_input.dat"))
+    if args.config == "3":
+        return synthetic.config_tree(4, args.npts, flux_fn=flux_fn, nsub=args.nsub)
+    return synthetic.config_single(npts=args.npts, flux_fn=flux_fn, nsub=args.nsub)
+
+
+def flops_per_pair(npts, nsub, gp):
+    """Counted algorithmic FP64 FLOPs of one walker-eclipse evaluation, by
+    kernel (MODEL_SPEC.md section 11)."""
+    acc = npts * nsub * (N_ECL * F_ACC_ECL + N_DON * F_ACC_DON + F_POINT)
+    if gp:
+        acc += npts * F_GP_POINT
+    return {"k_setup": F_SETUP, "k_elements": N_ROOTS * F_GEOM_ROOT, "k_lnlike": acc}
 
 
 def pmc_row(kernel):
     """Counter-derived bytes / FLOPs per launch of `kernel` (profiles/), or None."""
-    try:
-        d = json.load(open(PMC_FILE))
-    except (OSError, ValueError):
-        return None, None
-    row = d.get("kernels", {}).get(kernel)
-    return row, d.get("meta", {})
+    for path in PMC_FILES:
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        row = d.get("kernels", {}).get(kernel)
+        if row is None:
+            row = d.get("kernels", {}).get(kernel + "<1>")
+        return row, d.get("meta", {}), path
+    return None, None, None
 
 
-def main():
-    args = parse()
+def run(args):
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -121,7 +224,7 @@ def main():
     dist = None
     if args.exchange_path and world == 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29541")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
         args.shard_path = True
     if world > 1 or args.exchange_path:
         import torch.distributed as dist
@@ -133,7 +236,7 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    from lfit_python_amd import _native, batch, sampler, synthetic
+    from lfit_python_amd import _native, batch, sampler
     from lfit_python_amd.lfit import flux_batch
     _native.require_gpu()
     L = _native.lib()
@@ -143,13 +246,11 @@ def main():
         assert int(st[0].item()) == 0
         return f[0].cpu().numpy()
 
-    if args.config == 3:
-        model = synthetic.config_tree(4, args.npts, flux_fn=flux_fn, nsub=args.nsub)
-    else:
-        model = synthetic.config_single(npts=args.npts, flux_fn=flux_fn, nsub=args.nsub)
+    model = build_model(args, flux_fn)
     tree = batch.compile_tree(model, nsub=args.nsub)
-    ev = batch.LnProbEvaluator(tree, device=dev, max_walkers=args.walkers * world)
-    W = args.walkers * world
+    per_gpu = walker_count(args, world)
+    W = per_gpu * world
+    ev = batch.LnProbEvaluator(tree, device=dev, max_walkers=W)
     p0 = np.array(model.dynasty_par_vals)
     scat = sampler.comp_scatter(model.dynasty_par_names, 0.1)
     init = sampler.initialise_walkers(
@@ -253,37 +354,61 @@ def main():
         elapsed = float(t.item())
 
     # the dominant kernel's device time over the timed region
-    shard = events[0][1] if events else W // 2
+    shard = events[0][1] if events else W // 2   # walkers per launch
     dom_ms, ncalls = kernel_ms([KERNELS[dom]])
     avg_dom = float(dom_ms[0])
     E = tree.E
     npts = int(np.max(np.diff(tree.offsets)))
-    algo = algo_bytes(kname, shard * E, shard, tree.ndim, E, npts)
-    achieved = algo / (avg_dom * 1e-3) / 1e9
     value = W * args.steps / elapsed
     acc = float(np.mean(S.acceptance_fraction))
 
-    # counter-derived traffic and executed FP64 FLOPs of the same kernel
-    # (rocprofv3 --pmc passes, tools/pmc_profile.sh -> profiles/r01/pmc_traffic.json)
+    # ---- FP64 roofline on counted algorithmic FLOPs (MODEL_SPEC 11)
+    fpp = flops_per_pair(npts, tree.nsub, tree.gp)
+    f_eval = E * sum(fpp.values())                       # per walker evaluation
+    tf = value / world * f_eval / 1e12                   # per GPU, whole step
+    pairs = shard * E
+    dom_flops = fpp[kname] * pairs
+    dom_tf = dom_flops / (avg_dom * 1e-3) / 1e12
+    kern = {}
+    for n, m in calib.items():
+        f = fpp[n] * pairs
+        kern[n] = {"warmup_ms": m, "alg_flops_per_launch": f,
+                   "tflops": f / (m * 1e-3) / 1e12 if m > 0 else None,
+                   "frac": f / (m * 1e-3) / 1e12 / FP64_PEAK_TFLOPS if m > 0 else None}
+
+    # ---- HBM: SURVEY 8(d) algorithmic bytes per half-step; materialised tables apart
+    half_s = elapsed / args.steps / 2.0
+    hbm_bytes = shard * (8 * tree.ndim + 8) + 32 * npts * E
+    hbm_gbs = hbm_bytes / half_s / 1e9
+    mat = MATERIALISED_PER_PAIR[kname] * pairs
+
+    # counter-derived traffic and executed FP64 FLOPs of the dominant kernel
+    # (rocprofv3 --pmc passes, tools/pmc_profile.sh -> profiles/r0N/pmc_traffic.json);
     # the committed PMC pass is of the default workload (config 2, 300 points,
-    # nsub 1); per-pair counters do not carry over to other point counts
-    row, meta = pmc_row(kname) if (args.config == 2 and args.npts == 300 and args.nsub == 1) else (None, None)
-    traffic = fp64 = None
+    # nsub 1): per-pair counters do not carry over to other workloads
+    row, meta, pmc_path = pmc_row(kname) if (args.config == "2" and args.npts == 300 and args.nsub == 1) \
+        else (None, None, None)
+    traffic = fp64x = None
     if row and meta:
-        scale = shard * E / float(meta.get("pairs_per_launch", shard * E))
+        scale = pairs / float(meta.get("pairs_per_launch", pairs))
         if "traffic_bytes" in row:
             traffic = row["traffic_bytes"] * scale
         if "fp64_flops" in row:
             f = row["fp64_flops"] * scale
-            tf = f / (avg_dom * 1e-3) / 1e12
-            fp64 = {"executed_flops": f, "achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": tf / FP64_PEAK_TFLOPS, "source": os.path.relpath(PMC_FILE, ROOT)}
+            fp64x = {"executed_flops_per_launch": f, "tflops": f / (avg_dom * 1e-3) / 1e12,
+                     "frac": f / (avg_dom * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+                     "source": os.path.relpath(pmc_path, ROOT)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(tree, S.pos.cpu().numpy(), args)
 
     if rank == 0:
+        cfg = CONFIGS[args.config]
+        xch = ("one rank: no exchange" if dist is None
+               else ("%s all_gather" % backend if backend != "nccl"
+                     else ("ncclAllGather on the compute stream" if os.environ.get("LFG_RCCL_DIRECT", "1") != "0"
+                           else "torch ProcessGroupNCCL")))
         line = {
             "metric": "walker ln_prob evals/sec (300-pt phase, complex BS) at 1/2/4/8 MI355X",
             "value": value,
@@ -293,40 +418,58 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": cfg["scaling"],
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic light curve (model at mcmc_input.dat eclipse-0 truth + N(0, 0.004)); "
-                    "walkers from the comp_scat ball of mcmcfit.py",
-            "config": {"workload": "config %d: %s, complex 18-par bright spot, "
-                                   "%d phase pts, nsub %d, %d walkers/GPU, emcee stretch move"
-                                   % (args.config, "3-band x 4-eclipse tree" if args.config == 3
-                                      else "single eclipse", args.npts, args.nsub, args.walkers),
-                       "walkers_total": W, "eclipses": E, "ndim": tree.ndim,
-                       "parallelism": "walker shards x%d, replicated Philox RNG, "
-                                      "all_gather of ln_prob per half-step (%s)" % (
-                                          world, "one rank: no exchange" if dist is None
-                                          else ("%s all_gather" % backend if backend != "nccl"
-                                                else ("ncclAllGather on the compute stream"
-                                                      if os.environ.get("LFG_RCCL_DIRECT", "1") != "0"
-                                                      else "torch ProcessGroupNCCL"))),
-                       },
-            "roofline": {"bound": "hbm", "kernel": kname, "achieved": achieved,
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic, "algo_bytes_per_launch": algo,
-                         "avg_launch_ms": float(avg_dom),
-                         "fp64_valu": fp64,
-                         "note": "FP64-VALU bound root finding (DESIGN.md 3); HBM fraction reported per contract; "
-                                 "traffic = FETCH_SIZE x2 + WRITE_SIZE per launch from the committed PMC pass"},
-            "kernel_ms_per_launch_warmup": calib,
-            "launches_timed": ncalls,
+            "data": ("the reference's own light curves (test_data/lightcurves, tests/golden/ref_test_data)"
+                     if args.config == "gp" else
+                     "synthetic light curve (model at mcmc_input.dat eclipse-0 truth + N(0, 0.004))")
+                    + "; walkers from the comp_scat ball of mcmcfit.py",
+            "config": {"workload": cfg["desc"] % (args.npts if args.npts else "166-303", args.nsub, per_gpu),
+                       "walkers_total": W, "walkers_per_gpu": per_gpu, "eclipses": E, "ndim": tree.ndim,
+                       "parallelism": "walker shards x%d, replicated Philox RNG, one all_gather of ln_prob "
+                                      "per half-step (%s)" % (world, xch)},
+            "roofline": {
+                "bound": "fp64_valu", "achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": tf / FP64_PEAK_TFLOPS, "traffic": traffic,
+                "basis": "counted algorithmic FP64 FLOPs per walker-eclipse eval x evals/s per GPU over the "
+                         "whole step (MODEL_SPEC 11): F_setup + 900 roots x F_geom + N S (1500 x 3 + 400 x 6 + 40)",
+                "flops_per_walker_eval": f_eval,
+                "flops_per_pair": fpp,
+                "kernel": {"name": kname, "avg_launch_ms": avg_dom, "launches_timed": ncalls,
+                           "alg_flops_per_launch": dom_flops, "achieved": dom_tf,
+                           "frac": dom_tf / FP64_PEAK_TFLOPS, "executed_fp64": fp64x,
+                           "traffic_bytes_per_launch": traffic},
+                "kernels_warmup": kern,
+                "hbm": {"algorithmic_bytes_per_half_step": hbm_bytes, "achieved": hbm_gbs, "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": hbm_gbs / HBM_PEAK_GBS,
+                        "basis": "SURVEY 8(d): 8 ndim + 8 B per walker + 32 N B per eclipse per launch",
+                        "materialised_bytes_per_launch": {"kernel": kname, "bytes": mat,
+                                                          "note": "element tables the kernels hand each other "
+                                                                  "(DESIGN.md 3): an intermediate, not 8(d) work"}},
+            },
             "acceptance_fraction": acc,
             "cpu_baseline": cpu,
         }
-        print(json.dumps(line))
+        print(json.dumps(line), flush=True)
     S.close()
     if dist:
         dist.destroy_process_group()
+    return 0
+
+
+def _usable_cpus():
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    try:  # a cgroup CPU quota caps what the threads can use
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(round(int(q) / int(p)))))
+    except (OSError, ValueError):
+        pass
+    return n
 
 
 def cpu_baseline(tree, walkers, args):
@@ -341,13 +484,14 @@ def cpu_baseline(tree, walkers, args):
     except (subprocess.CalledProcessError, FileNotFoundError):
         path = orc.LIB_PATH
     o = orc.Oracle(path)
-    nthr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    avail = _usable_cpus()
+    nthr = args.cpu_threads if args.cpu_threads > 0 else avail
     batch = walkers[: max(nthr * 4, 64)]
-    o.lnprob_batch(batch[:nthr], tree, nsub=args.nsub, nthreads=nthr)  # warm
+    o.lnprob_batch(batch[:nthr], tree, nsub=tree.nsub, nthreads=nthr)  # warm
     n, t0 = 0, time.perf_counter()
     used = nthr
     while True:
-        _, _, used = o.lnprob_batch(batch, tree, nsub=args.nsub, nthreads=nthr)
+        _, _, used = o.lnprob_batch(batch, tree, nsub=tree.nsub, nthreads=nthr)
         n += batch.shape[0]
         el = time.perf_counter() - t0
         if el >= args.cpu_seconds:
@@ -362,10 +506,13 @@ def cpu_baseline(tree, walkers, args):
     except OSError:
         pass
     return {"value": n / el, "unit": "walker ln_prob evals/s", "cores": int(used), "kind": "port",
-            "sample": "%d ln_prob evals (%d-walker batches of the same tree) in %.1f s, "
-                      "oracle/lfg_oracle.c -O3 -march=native OpenMP" % (n, batch.shape[0], el),
-            "cpu": model}
+            "sample": "%d ln_prob evals (%d-walker batches of the same tree and walkers) in %.1f s: "
+                      "oracle/lfg_oracle.c -O3 -march=native, OpenMP over walkers; the oracle's algorithm, "
+                      "not the GPU's: nested ray-minimum solver per element (MODEL_SPEC 4.3), all 1900 "
+                      "elements solved directly (no mirror symmetry), direct element x point accumulation"
+                      % (n, batch.shape[0], el),
+            "cpu": model, "host_cpus": os.cpu_count(), "cpus_available": avail}
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

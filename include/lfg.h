@@ -84,6 +84,10 @@ typedef struct lfg_tree {
                                  (CVModel.py:548-576)                       */
     const int* gp_ecl;        /* [dev] E*2: first and last eclipse number of
                                  the changepoint list (CVModel.py:582-590)  */
+    /* 1: a fixed (isVar = 0) parameter lies outside its prior, so
+     * Node.ln_prior is -inf for every walker (model.py:439-441 checks every
+     * parameter, variable or not); ln_prob = -inf on every path */
+    int fixed_invalid;
 } lfg_tree;
 
 /* scratch bytes needed for W parameter sets x E eclipses */

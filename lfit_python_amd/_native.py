@@ -52,6 +52,7 @@ class LfgTree(ctypes.Structure):
         ("gp", ctypes.c_int),
         ("gp_gather", ctypes.c_void_p), ("gp_base", ctypes.c_void_p),
         ("gp_ecl", ctypes.c_void_p),
+        ("fixed_invalid", ctypes.c_int),
     ]
 
 

@@ -152,9 +152,12 @@ class LnProbEvaluator:
             tree.E, tree.ndim, tree.nsub, tree.max_n, p('gather'), p('npars'), p('consts'),
             p('off'), p('x'), p('y'), p('ye'), p('w'), p('prior_type'), p('prior_p1'),
             p('prior_p2'), p('prior_norm'), int(tree.roche_priors), int(tree.gp),
-            p('gp_gather'), p('gp_base'), p('gp_ecl'))
+            p('gp_gather'), p('gp_base'), p('gp_ecl'), int(tree.fixed_invalid))
         self._ws = None
         self._ws_walkers = 0
+        # bumped whenever the workspace is reallocated: a captured HIP graph
+        # holds the old pointer (sampler.EnsembleSampler re-captures on change)
+        self.generation = 0
         if max_walkers:
             self._ensure(max_walkers)
 
@@ -178,6 +181,7 @@ class LnProbEvaluator:
             nbytes = self.L.lfg_workspace_size(W, self.tree.E)
             self._ws = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
             self._ws_walkers = W
+            self.generation += 1
 
     def __call__(self, walkers, out=None, lnlike_e=None):
         """walkers: float64 device tensor [W, ndim] -> lnp [W] (same stream)."""
@@ -195,9 +199,7 @@ class LnProbEvaluator:
                                ctypes.c_void_p(lnlike_e.data_ptr()) if lnlike_e is not None else None,
                                ctypes.c_void_p(self._ws.data_ptr()), self._ws.numel(),
                                _native.stream_ptr(self.device))
-        _native.check(rc, "lfg_lnprob")
-        if self.tree.fixed_invalid:
-            out.fill_(-np.inf)
+        _native.check(rc, "lfg_lnprob")  # fixed_invalid trees: -inf from k_setup's prior lanes
         return out
 
 
@@ -249,8 +251,6 @@ class LnProbEvaluator:
                                 ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(self._ws.data_ptr()),
                                 self._ws.numel(), _native.stream_ptr(self.device))
         _native.check(rc, "lfg_lnprior")
-        if self.tree.fixed_invalid:
-            out.fill_(-np.inf)
         return out
 
 

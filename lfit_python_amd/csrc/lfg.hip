@@ -122,6 +122,7 @@ struct SetupArgs {
     // the batch is walkers lo .. lo + W - 1 of the ns-walker half (ns = W,
     // lo = 0 on one process; a rank's shard with lfg_stretch_step_shard)
     int lo, ns;
+    int fixed_invalid;  // lfg_tree.fixed_invalid: every prior lane gives -inf
 };
 
 // where a lane reads walker w's parameters: the walker row, or the
@@ -225,7 +226,7 @@ __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
                 lp += prior_lnprob(A.prior_type[d], A.prior_p1[d], A.prior_p2[d], A.prior_norm[d],
                                    gather_par(A, P, d));
         }
-        A.prior[w] = lp;
+        A.prior[w] = A.fixed_invalid ? -INFINITY : lp;
         if (A.done) A.done[w] = 0;
         return;
     }
@@ -1697,6 +1698,7 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
     SetupArgs S{walkers, W, T->ndim, T->E, 18, T->gather, T->npars, T->consts, T->prior_type, T->prior_p1,
                 T->prior_p2, T->prior_norm, T->roche_priors, ws.geo, ws.status, ws.prior, ws.bstatus, T->gp,
                 T->gp_gather, T->gp_base, ws.done};
+    S.fixed_invalid = T->fixed_invalid;
     if (prop) {
         S.pos = prop->pos;
         S.a = prop->a;
@@ -1734,6 +1736,7 @@ int lfg_lnprior(const double* walkers, int W, const lfg_tree* T, double* lnprior
     SetupArgs S{walkers, W, T->ndim, T->E, 18, T->gather, T->npars, T->consts, T->prior_type, T->prior_p1,
                 T->prior_p2, T->prior_norm, T->roche_priors, ws.geo, ws.status, ws.prior, ws.bstatus, 0,
                 nullptr, nullptr, nullptr};
+    S.fixed_invalid = T->fixed_invalid;
     const int nlanes = 2 * W * T->E + W;
     hipLaunchKernelGGL(k_setup, dim3((nlanes + SETUP_BLOCK - 1) / SETUP_BLOCK), dim3(SETUP_BLOCK), 0, st, S);
     int rc = launch_ok();

@@ -93,9 +93,9 @@ def run(input_file, quiet=False, debug=False, seed=0, chain_file="chain_prod.txt
         for par, lab in model.descendant_params():
             if not par.isValid:
                 say("  -> {}_{}".format(par.name, lab))
-        return None
+        return {"status": "prior_violation"}
     if not rc["fit"]:
-        return None
+        return {"status": "no_fit"}  # mcmcfit.py:181-182: report only
     if rc["usePT"]:
         raise NotImplementedError("parallel tempering (usePT = 1, ptemcee) is out of scope")
 
@@ -105,7 +105,7 @@ def run(input_file, quiet=False, debug=False, seed=0, chain_file="chain_prod.txt
     say("\n\nThe MCMC has {:d} variables and {:d} walkers".format(npars, nwalkers))
     say("(It should have at least 2*npars, {:d} walkers)".format(2 * npars))
     if nwalkers < 2 * npars:
-        return None
+        return {"status": "too_few_walkers"}  # mcmcfit.py:195-196
     s1, s2 = scatter_vectors(names, rc)
     if rc["double_burnin"] and s2 is None:
         raise NameError("double_burnin needs comp_scat = 1 (the reference defines p0_scatter_2 only then)")
@@ -124,7 +124,7 @@ def run(input_file, quiet=False, debug=False, seed=0, chain_file="chain_prod.txt
         p0 = sampler.initialise_walkers(pos[np.argmax(prob)], s2, nwalkers, prior_fn, seed=rng_seed + 1)
         pos, prob = S.run_mcmc(p0, rc["nburn"], store=False)
 
-    S.reset()
+    S.reset()  # clears the counters; the RNG stream carries on (emcee's rstate0=rState)
     say("Starting the main MCMC chain. Probably going to take a while!")
     nprod = rc["nprod"]
     chunk = chunk or max(1, min(nprod, (1 << 28) // max(1, nwalkers * (npars + 1) * 8)))
@@ -141,7 +141,8 @@ def run(input_file, quiet=False, debug=False, seed=0, chain_file="chain_prod.txt
     acc = float(np.mean(S.acceptance_fraction))
     S.close()  # the direct RCCL communicator, before the process group goes
     say("Mean acceptance fraction: {:.3f}".format(acc))
-    return {"chain_file": chain_file, "acceptance": acc, "nwalkers": nwalkers, "npars": npars, "nprod": nprod}
+    return {"status": "ok", "chain_file": chain_file, "acceptance": acc, "nwalkers": nwalkers, "npars": npars,
+            "nprod": nprod}
 
 
 def main(argv=None):
@@ -161,7 +162,10 @@ def main(argv=None):
     out = run(args.input, quiet=args.quiet, debug=args.debug, seed=args.seed, chain_file=args.chain)
     if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
-    return 0 if out is not None else 1
+    # the reference leaves through a bare exit() (status 0) for a report-only
+    # run (fit = 0) and for too few walkers; a start that violates the priors
+    # is an error here (non-zero), so wrapping scripts can tell it apart
+    return 1 if out["status"] == "prior_violation" else 0
 
 
 if __name__ == "__main__":

@@ -114,7 +114,11 @@ class EnsembleSampler:
         self.zfac = torch.empty(ns, **f64)
         self.lnp_new = torch.empty(ns, **f64)
         self.naccept = torch.zeros(self.W, dtype=torch.int32, device=self.dev)
-        self.iteration = 0
+        self.iteration = 0   # emcee's counter: reset() clears it (acceptance fractions)
+        # Philox step counter of every draw: monotone over the sampler's life,
+        # so the production run after reset() never replays burn-in draws
+        # (the reference hands the burn-in RNG state on, mcmc_utils.py:135-183)
+        self.rng_step = 0
         self.chain = None
         self.lnprob_chain = None
         self.timer = None  # optional callable(walkers) -> lnp used instead of self.ev
@@ -137,6 +141,7 @@ class EnsembleSampler:
         # step() after enabling runs eagerly, the next captures, later ones replay
         self.use_graph = False
         self._graph = None
+        self._graph_gen = None  # evaluator workspace generation the graph was captured on
         self._step_dev = None
         self._dev_iter = 0
         self._warm = False  # one eager iteration (allocations, side stream) before capture
@@ -201,11 +206,11 @@ class EnsembleSampler:
     def _sync_step_dev(self):
         import torch
         if self._step_dev is None:
-            self._step_dev = torch.full((1,), self.iteration, dtype=torch.int64, device=self.dev)
-            self._dev_iter = self.iteration
-        elif self._dev_iter != self.iteration:  # iteration changed from outside (reset)
-            self._step_dev.fill_(self.iteration)
-            self._dev_iter = self.iteration
+            self._step_dev = torch.full((1,), self.rng_step, dtype=torch.int64, device=self.dev)
+            self._dev_iter = self.rng_step
+        elif self._dev_iter != self.rng_step:  # the counter was set from outside (set_rng_state)
+            self._step_dev.fill_(self.rng_step)
+            self._dev_iter = self.rng_step
 
     def capture_iteration(self, evaluator=None):
         """A HIP graph of one whole emcee iteration (single rank, HIP ops) that
@@ -225,11 +230,17 @@ class EnsembleSampler:
         self._sync_step_dev()
         g.replay()
         self.iteration += 1
+        self.rng_step += 1
         self._dev_iter += 1
 
     def _graph_step(self):
-        if self._graph is None:
+        # the graph bakes in the evaluator's workspace pointer: re-capture when
+        # the evaluator has reallocated it since (batch.LnProbEvaluator.generation)
+        gen = getattr(self.ev, "generation", None)
+        if self._graph is None or gen != self._graph_gen:
+            self._graph = None
             self._graph = self.capture_iteration()
+            self._graph_gen = gen
         self.replay(self._graph)
 
     def step(self):
@@ -241,13 +252,13 @@ class EnsembleSampler:
         for half in (0, 1):
             if self.world == 1 and self.fuse and self.timer is None and not self.force_shard:
                 f = self.half_timer or self.ev.step_half
-                f(self.pos, self.lnp, half, self.a, self.seed, self.iteration, self.q, self.zfac, self.naccept,
+                f(self.pos, self.lnp, half, self.a, self.seed, self.rng_step, self.q, self.zfac, self.naccept,
                   lnp_new=self.lnp_new)
                 continue
             if (self.world > 1 or self.force_shard) and self.fuse_shard and self.timer is None:
                 self._shard_half(half)
                 continue
-            self.ops.propose(self.pos, half, self.a, self.seed, self.iteration, self.q, self.zfac)
+            self.ops.propose(self.pos, half, self.a, self.seed, self.rng_step, self.q, self.zfac)
             if self.world == 1:
                 self._eval(self.q, self.lnp_new)
             else:
@@ -255,8 +266,9 @@ class EnsembleSampler:
                 mine = self._eval(self.q[lo:lo + self.shard], None)
                 self._gather(self.lnp_new, mine)
             self.ops.accept(self.pos, self.lnp, half, self.q, self.zfac, self.lnp_new, self.seed,
-                            self.iteration, self.naccept)
+                            self.rng_step, self.naccept)
         self.iteration += 1
+        self.rng_step += 1
 
     def _shard_half(self, half):
         import torch
@@ -266,13 +278,13 @@ class EnsembleSampler:
             self._zf_sh = torch.empty(self.shard, **f64)
             self._lnp_sh = torch.empty(self.shard, **f64)
         f = self.shard_timer or self.ev.step_shard
-        f(self.pos, half, self.a, self.seed, self.iteration, self.rank * self.shard, self._q_sh, self._zf_sh,
+        f(self.pos, half, self.a, self.seed, self.rng_step, self.rank * self.shard, self._q_sh, self._zf_sh,
           self._lnp_sh)
         if self.world > 1 or self.force_exchange:
             self._gather(self.lnp_new, self._lnp_sh)
         else:
             self.lnp_new.copy_(self._lnp_sh)
-        self.ops.accept_regen(self.pos, self.lnp, half, self.a, self.lnp_new, self.seed, self.iteration,
+        self.ops.accept_regen(self.pos, self.lnp, half, self.a, self.lnp_new, self.seed, self.rng_step,
                               self.naccept)
 
     def close(self):
@@ -303,9 +315,21 @@ class EnsembleSampler:
         return (self.naccept.double() / max(self.iteration, 1)).cpu().numpy()
 
     def reset(self):
+        """emcee's reset: clears the chain, the iteration count and the
+        acceptance counters; the RNG stream carries on (rng_step is kept)."""
         self.iteration = 0
         self.naccept.zero_()
         self.chain = self.lnprob_chain = None
+
+    @property
+    def random_state(self):
+        """The RNG state, emcee's `state` / `rstate0`: the Philox counter of
+        the next iteration (the key is the seed)."""
+        return self.rng_step
+
+    @random_state.setter
+    def random_state(self, step):
+        self.rng_step = int(step)
 
 
 def initialise_walkers(p, scatter, nwalkers, ln_prob_fn, seed=0, max_rounds=1000):

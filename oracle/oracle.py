@@ -178,4 +178,6 @@ class Oracle:
             F(tree.gp_base[:, :3].reshape(-1)) if gp else None,
             I(tree.gp_ecl.reshape(-1)) if gp else None,
             lnp.ctypes.data_as(_dp), lle.ctypes.data_as(_dp), int(nthreads))
+        if getattr(tree, "fixed_invalid", False):  # an invalid fixed parameter: Node.ln_prior = -inf
+            lnp[:] = -np.inf
         return lnp, lle, used
