@@ -276,6 +276,30 @@ int lfg_gp_lnlike(const double* x, const double* ye, const double* res, int W,
                   int N, const double* hyp, const double* blocks, int nb,
                   double* lnlike, void* stream);
 
+/*
+ * lfit's component objects (MODEL_SPEC 5.6): the unit-normalised flux of one
+ * component for W parameter sets, at inclination inc (degrees, not dphi),
+ * on a caller-chosen grid.  Replaces
+ *   lfit.PyWhiteDwarf(rwd/xl1, ulimb).calcFlux(q, inc, phi, width)   kind 0
+ *   lfit.PyDisc(q, rwd/xl1, rdisc, dexp, npts).calcFlux(...)         kind 1
+ *   lfit.PySpot(q, rdisc, az, fis, scale, exp1, exp2, tilt, yaw,
+ *               complex).calcFlux(...)                                kind 2
+ *   lfit.PyDonor(q, npts).calcFlux(...)                              kind 3
+ * (testCV.py:27-49, fitEcl.py:21-24).  cpars [dev] W x ncp with ncp = 2
+ * (rwd/xl1, ulimb), 3 (rwd/xl1, rdisc/xl1, dexp), 8 (rdisc/xl1, az, fis,
+ * scale/xl1, exp1, exp2, tilt, yaw), 0 (donor: cpars unused);
+ * q, inc [dev] W; grids: disc n1 rings x n2 azimuths, spot n1 strip
+ * elements, donor n1 bands x n2 azimuths (the WD grid is fixed, 400 tiles);
+ * x, w [dev] N phases (used as given: no phi0) and exposure half-widths
+ * (w = NULL: points); out [dev] W x N; status [dev] W.  Scratch ws of at
+ * least lfg_component_workspace_size(kind, W, n1, n2) bytes.
+ */
+size_t lfg_component_workspace_size(int kind, int W, int n1, int n2);
+int lfg_component(int kind, const double* cpars, int ncp, const double* q,
+                  const double* inc, int W, int n1, int n2, const double* x,
+                  const double* w, int N, double* out, int* status, void* ws,
+                  size_t ws_bytes, void* stream);
+
 /* hipEvent helpers for hosts without a HIP binding (ctypes) */
 int lfg_event_create(void** ev);
 int lfg_event_destroy(void* ev);

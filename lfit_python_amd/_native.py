@@ -15,7 +15,7 @@ LIB_DIR = os.path.join(_HERE, "_lib")
 LIB_PATH = os.path.join(LIB_DIR, "liblfg_hip.so")
 # diagnostic builds (e.g. -DLFG_PROFILE_SETUP) are loaded through LFG_LIB
 LOAD_PATH = os.environ.get("LFG_LIB", LIB_PATH)
-SOURCES = [os.path.join(_HERE, "csrc", "lfg.hip")]
+SOURCES = [os.path.join(_HERE, "csrc", "lfg.hip"), os.path.join(_HERE, "csrc", "lfg_components.hip")]
 HEADERS = [os.path.join(_HERE, "csrc", "lfg_device.hpp"),
            os.path.join(_HERE, "csrc", "lfg_tables.hpp"),
            os.path.join(REPO, "include", "lfg.h")]
@@ -61,7 +61,8 @@ EXPORTS = ("lfg_workspace_size", "lfg_flux", "lfg_lnprob", "lfg_lnprior", "lfg_l
            "lfg_stretch_accept_regen",
            "lfg_elements", "lfg_roche", "lfg_stretch_propose", "lfg_stretch_accept",
            "lfg_stretch_propose_dev", "lfg_stretch_accept_dev", "lfg_event_create", "lfg_event_destroy",
-           "lfg_event_elapsed_ms", "lfg_wdphases", "lfg_gp_lnlike", "lfg_version")
+           "lfg_event_elapsed_ms", "lfg_wdphases", "lfg_gp_lnlike", "lfg_component_workspace_size",
+           "lfg_component", "lfg_version")
 
 
 def build(force=False, verbose=False):
@@ -143,6 +144,10 @@ def lib():
         L.lfg_wdphases.argtypes = [vp, vp, vp, ip, ip, vp, vp, vp, vp]
         L.lfg_gp_lnlike.restype = ip
         L.lfg_gp_lnlike.argtypes = [vp, vp, vp, ip, ip, vp, vp, ip, vp, vp]
+        L.lfg_component_workspace_size.restype = sz
+        L.lfg_component_workspace_size.argtypes = [ip, ip, ip, ip]
+        L.lfg_component.restype = ip
+        L.lfg_component.argtypes = [ip, vp, ip, vp, vp, ip, ip, ip, vp, vp, ip, vp, vp, vp, sz, vp]
         L.lfg_version.restype = ctypes.c_char_p
         L.lfg_version.argtypes = []
         _lib = L

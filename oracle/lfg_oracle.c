@@ -1021,3 +1021,153 @@ int lfo_lnprob_batch_gp(const double* walkers, int W, int ndim,
     }
     return used;
 }
+
+/* --------------------------------------------- component objects (5.6)
+ * lfit's PyWhiteDwarf / PyDisc / PySpot / PyDonor (testCV.py:27-49,
+ * fitEcl.py:21-24): one component, unit-normalised ("flux at maximum
+ * light" = 1), at a given inclination, on a caller-chosen grid.  Each
+ * element and tile is built as in build_elements (5.1-5.4), with
+ * n1 x n2 disc rings x azimuths or donor bands x azimuths.  Phases are
+ * used as given (no phi0), reduced to [-1/2, 1/2); w = exposure half-width. */
+int lfo_component(int kind, const double* cp, double q, double inc_deg, int n1, int n2,
+                  const double* x, const double* w, int n, double* out)
+{
+    Roche R;
+    int st = roche_init(&R, q);
+    if (!st && !(inc_deg > 0.0 && inc_deg <= 90.0)) st = LFO_BAD_ARGS;
+    if (!st && (kind < 0 || kind > 3 || ((kind == 1 || kind == 3) && (n1 < 1 || n2 < 1)) ||
+                (kind == 2 && n1 < 1)))
+        st = LFO_BAD_ARGS;
+    if (st) {
+        fill_nan(out, n);
+        return st;
+    }
+    const double i = inc_deg * DEG, s = sin(i), c = cos(i), Reff = eggleton(q);
+    int nel = (kind == 0) ? LFO_NWD : (kind == 2 ? n1 : n1 * n2);
+    double* a = (double*)malloc(sizeof(double) * nel);
+    double* b = (double*)malloc(sizeof(double) * nel);
+    double* wg = (double*)malloc(sizeof(double) * nel);
+    double (*dv)[3] = (double (*)[3])malloc(sizeof(double) * 3 * nel);
+    double tot = 0.0, nb[3] = {0.0, 0.0, 0.0}, bden = 0.0, fis = 0.0;
+    int k = 0;
+    if (kind == 0) {  /* cp: rwd (units of xl1), ulimb */
+        const double rwd_a = cp[0] * R.xl1, u = cp[1];
+        if (!(rwd_a > 0.0) || !(rwd_a < R.xl1)) st = LFO_BAD_GEOMETRY;
+        for (int ir = 0; !st && ir < LFO_NWD_RINGS; ++ir) {
+            double r0 = (double)ir / LFO_NWD_RINGS, r1 = (double)(ir + 1) / LFO_NWD_RINGS;
+            int nk = 4 * (2 * ir + 1);
+            double F0 = (1.0 - u) * 0.5 * r0 * r0 - u * pow(1.0 - r0 * r0, 1.5) / 3.0;
+            double F1 = (1.0 - u) * 0.5 * r1 * r1 - u * pow(1.0 - r1 * r1, 1.5) / 3.0;
+            double wring = (TWO_PI / nk) * (F1 - F0);
+            double rc = sqrt(0.5 * (r0 * r0 + r1 * r1)), mu0 = sqrt(1.0 - rc * rc);
+            for (int j = 0; j < nk; ++j, ++k) {
+                double psi = TWO_PI * (j + 0.5) / nk, cps = cos(psi), sps = sin(psi);
+                double P[3] = {rwd_a * (-rc * sps * c + mu0 * s), rwd_a * (rc * cps), rwd_a * (rc * sps * s + mu0 * c)};
+                element_interval(&R, P, s, c, Reff, &a[k], &b[k]);
+                wg[k] = wring;
+                tot += wring;
+            }
+        }
+    } else if (kind == 1) {  /* cp: rwd, rdisc (units of xl1), dexp */
+        const double rin = cp[0] * R.xl1, rout = cp[1] * R.xl1, ex = 2.0 - cp[2];
+        if (!(rin > 0.0) || !(rout > rin) || !(rout < R.xl1)) st = LFO_BAD_GEOMETRY;
+        const double dr = (rout - rin) / n1;
+        for (int ir = 0; !st && ir < n1; ++ir) {
+            double r0 = rin + ir * dr, r1 = rin + (ir + 1) * dr, rc = 0.5 * (r0 + r1);
+            double I = (fabs(ex) < 1e-10) ? log(r1 / r0) : (pow(r1, ex) - pow(r0, ex)) / ex;
+            double wring = (TWO_PI / n2) * I;
+            for (int j = 0; j < n2; ++j, ++k) {
+                double al = TWO_PI * (j + 0.5) / n2;
+                double P[3] = {rc * cos(al), rc * sin(al), 0.0};
+                element_interval(&R, P, s, c, Reff, &a[k], &b[k]);
+                wg[k] = wring;
+                tot += wring;
+            }
+        }
+    } else if (kind == 2) {  /* cp: rdisc (xl1), az, fis, scale (xl1), exp1, exp2, tilt, yaw */
+        const double rdisc_a = cp[0] * R.xl1, az = cp[1], scale = cp[3], e1 = cp[4], e2 = cp[5];
+        double bs[4];
+        fis = cp[2];
+        if (!(rdisc_a > 0.0) || !(rdisc_a < R.xl1) || !(scale > 0.0) || !(e1 > 0.0) || !(e2 > 0.0))
+            st = LFO_BAD_GEOMETRY;
+        if (!st) st = bspot_R(&R, rdisc_a, bs);
+        if (!st) {
+            const double l = scale * R.xl1, upk = pow(e1 / e2, 1.0 / e2);
+            const double lnpk = e1 * log(upk) - pow(upk, e2), umax = bs_profile_root(e1, e2, lnpk);
+            const double t = cp[6] * DEG, psi = (az - 90.0 + cp[7]) * DEG;
+            nb[0] = sin(t) * cos(psi);
+            nb[1] = sin(t) * sin(psi);
+            nb[2] = cos(t);
+            bden = fis + (1.0 - fis) * fmax(fabs(sin(t)) * s + cos(t) * c, 0.0);
+            const double du = umax / n1, ca = cos(az * DEG), sa = sin(az * DEG);
+            for (int j = 0; j < n1; ++j, ++k) {
+                double uk = (j + 0.5) * du;
+                double off = l * (uk - upk);
+                double P[3] = {bs[0] + off * ca, bs[1] + off * sa, 0.0};
+                element_interval(&R, P, s, c, Reff, &a[k], &b[k]);
+                wg[k] = exp(e1 * log(uk) - pow(uk, e2) - lnpk);
+                tot += wg[k];
+            }
+        }
+    } else {  /* donor: n1 theta' bands x n2 azimuths */
+        for (int it = 0; it < n1; ++it) {
+            double t0 = PI * it / n1, t1 = PI * (it + 1) / n1, tc = 0.5 * (t0 + t1);
+            double dOm = (cos(t0) - cos(t1)) * (TWO_PI / n2);
+            for (int ip = 0; ip < n2; ++ip, ++k) {
+                double ph = TWO_PI * (ip + 0.5) / n2;
+                double d[3] = {-cos(tc), sin(tc) * cos(ph), sin(tc) * sin(ph)};
+                double lo = 0.0, hi = R.Rs, r = Reff, g[3];
+                if (!(r > lo && r < hi)) r = 0.5 * hi;
+                for (int itr = 0; itr < ROOT_MAXIT; ++itr) {
+                    double X0 = 1.0 + r * d[0], X1 = r * d[1], X2 = r * d[2];
+                    double f = pot(&R, X0, X1, X2) - R.pl1;
+                    grad_pot(&R, X0, X1, X2, g);
+                    double df = g[0] * d[0] + g[1] * d[1] + g[2] * d[2];
+                    if (f > 0.0) hi = r; else lo = r;
+                    if (df > 0.0 && fabs(f / df) <= ROOT_LAST) { r -= f / df; break; }
+                    double rn = (df > 0.0) ? r - f / df : 0.5 * (lo + hi);
+                    if (!(rn > lo && rn < hi)) rn = 0.5 * (lo + hi);
+                    r = rn;
+                }
+                grad_pot(&R, 1.0 + r * d[0], r * d[1], r * d[2], g);
+                double gn = sqrt(g[0] * g[0] + g[1] * g[1] + g[2] * g[2]);
+                double dA = r * r * dOm / ((g[0] * d[0] + g[1] * d[1] + g[2] * d[2]) / gn);
+                for (int m = 0; m < 3; ++m) dv[k][m] = dA * g[m] / gn;
+                double v = -s * dv[k][1] + c * dv[k][2];  /* quadrature, e = (0, -s, c) */
+                if (v > 0.0) tot += v;
+            }
+        }
+    }
+    if (!st) {
+        for (int p = 0; p < n; ++p) {
+            double ph = x[p], h = w ? w[p] : 0.0;
+            ph -= floor(ph + 0.5);
+            double acc = 0.0;
+            if (kind == 3) {
+                double th = TWO_PI * ph, e0 = s * cos(th), e1 = -s * sin(th);
+                for (int j = 0; j < nel; ++j) {
+                    double v = dv[j][0] * e0 + dv[j][1] * e1 + dv[j][2] * c;
+                    if (v > 0.0) acc += v;
+                }
+                out[p] = acc / tot;
+                continue;
+            }
+            for (int j = 0; j < nel; ++j) acc += wg[j] * vis(a[j], b[j], ph, h);
+            double f = acc / tot;
+            if (kind == 2) {
+                double th = TWO_PI * ph, e0 = s * cos(th), e1 = -s * sin(th);
+                double beam = 0.0;
+                if (bden > 0.0) beam = (fis + (1.0 - fis) * fmax(nb[0] * e0 + nb[1] * e1 + nb[2] * c, 0.0)) / bden;
+                f *= beam;
+            }
+            out[p] = f;
+        }
+    } else {
+        fill_nan(out, n);
+    }
+    free(a);
+    free(b);
+    free(wg);
+    free(dv);
+    return st;
+}

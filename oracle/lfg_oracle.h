@@ -102,6 +102,15 @@ int lfo_lnprob_batch_gp(const double* walkers, int W, int ndim,
                         const int* gp_ecl, double* lnp, double* lnlike_e,
                         int nthreads);
 
+/* lfit's component objects (testCV.py:27-49; MODEL_SPEC 5.6): unit-
+ * normalised flux of one component at inclination inc_deg, phases x used as
+ * given, half-widths w (NULL: points).  kind 0 white dwarf cp = {rwd/xl1,
+ * ulimb}; 1 disc cp = {rwd/xl1, rdisc/xl1, dexp}, n1 x n2 rings x azimuths;
+ * 2 bright spot cp = {rdisc/xl1, az, fis, scale/xl1, exp1, exp2, tilt, yaw},
+ * n1 strip elements; 3 donor, n1 x n2 bands x azimuths. */
+int lfo_component(int kind, const double* cp, double q, double inc_deg, int n1, int n2,
+                  const double* x, const double* w, int n, double* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -70,6 +70,8 @@ class Oracle:
         lib.lfo_gp_lnlike.argtypes = [_dp, _dp, _dp, ctypes.c_int, ctypes.c_double, ctypes.c_double,
                                       ctypes.c_double, _dp, ctypes.c_int]
         lib.lfo_gp_base_dcp.argtypes = [ctypes.c_double, ctypes.c_double, ctypes.c_double, _dp]
+        lib.lfo_component.argtypes = [ctypes.c_int, _dp, ctypes.c_double, ctypes.c_double, ctypes.c_int,
+                                      ctypes.c_int, _dp, _dp, ctypes.c_int, _dp]
         self.lib = lib
 
     # roche -----------------------------------------------------------------
@@ -134,6 +136,16 @@ class Oracle:
         if components:
             return st, out
         return st, out[0]
+
+    def component(self, kind, cp, q, inc, x, w=None, n1=0, n2=0):
+        """lfo_component: one unit-normalised component (MODEL_SPEC 5.6)."""
+        cp, cpp = _f(cp if len(cp) else [0.0])
+        x, xp = _f(x)
+        w_, wp = _f(w) if w is not None else (None, None)
+        out = np.empty(x.shape[0])
+        st = self.lib.lfo_component(int(kind), cpp, float(q), float(inc), int(n1), int(n2), xp, wp, x.shape[0],
+                                    out.ctypes.data_as(_dp))
+        return st, out
 
     def elements(self, pars):
         pars, pp = _f(pars)
