@@ -53,7 +53,12 @@ extern "C" {
  * CV parameter order is lfit's (CVModel.py:384-388; README.md:24-43), so the
  * tree's yaw/tilt storage order (CVModel.py:376-380) is swapped in `gather`.
  */
-typedef struct lfg_tree {
+typedef struct lfg_tree lfg_tree;
+/* scratch bytes lfg_lnprob & co. need for W walkers of `tree` (GP trees
+ * also keep every pair's residuals, W x E x max_n doubles) */
+size_t lfg_workspace_size_tree(int W, const lfg_tree* tree);
+
+struct lfg_tree {
     int E;                    /* eclipses (leaves)                          */
     int ndim;                 /* walker vector length                       */
     int nsub;                 /* exposure sub-bins S >= 1 (1 = native)      */
@@ -88,9 +93,10 @@ typedef struct lfg_tree {
      * Node.ln_prior is -inf for every walker (model.py:439-441 checks every
      * parameter, variable or not); ln_prob = -inf on every path */
     int fixed_invalid;
-} lfg_tree;
+};
 
-/* scratch bytes needed for W parameter sets x E eclipses */
+/* scratch bytes needed for W parameter sets x E eclipses (chi^2 trees and
+ * lfg_flux / lfg_elements) */
 size_t lfg_workspace_size(int W, int E);
 
 /*

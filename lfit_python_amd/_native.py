@@ -56,7 +56,7 @@ class LfgTree(ctypes.Structure):
     ]
 
 
-EXPORTS = ("lfg_workspace_size", "lfg_flux", "lfg_lnprob", "lfg_lnprior", "lfg_lnprob_timed",
+EXPORTS = ("lfg_workspace_size", "lfg_workspace_size_tree", "lfg_flux", "lfg_lnprob", "lfg_lnprior", "lfg_lnprob_timed",
            "lfg_stretch_lnprob_accept", "lfg_stretch_step_half", "lfg_stretch_step_shard",
            "lfg_stretch_accept_regen",
            "lfg_elements", "lfg_roche", "lfg_stretch_propose", "lfg_stretch_accept",
@@ -101,6 +101,8 @@ def lib():
         vp, ip, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
         L.lfg_workspace_size.restype = sz
         L.lfg_workspace_size.argtypes = [ip, ip]
+        L.lfg_workspace_size_tree.restype = sz
+        L.lfg_workspace_size_tree.argtypes = [ip, ctypes.POINTER(LfgTree)]
         L.lfg_flux.restype = ip
         L.lfg_flux.argtypes = [vp, ip, ip, vp, vp, ip, ip, vp, vp, vp, vp, sz, vp]
         L.lfg_lnprob.restype = ip

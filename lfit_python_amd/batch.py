@@ -178,7 +178,7 @@ class LnProbEvaluator:
     def _ensure(self, W):
         import torch
         if W > self._ws_walkers:
-            nbytes = self.L.lfg_workspace_size(W, self.tree.E)
+            nbytes = self.L.lfg_workspace_size_tree(W, ctypes.byref(self.ctree))
             self._ws = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
             self._ws_walkers = W
             self.generation += 1

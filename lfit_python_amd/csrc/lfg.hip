@@ -61,12 +61,13 @@ struct Ws {
     double* prior;
     double* lle;
     int* done;      // [W] eclipses finished per walker (k_lnlike's fused combine, E > 1)
+    double* res;    // [pairs][gp_n] GP trees: residuals y - flux (k_lnlike<2> -> k_gp_like)
     size_t total;
 };
 
 inline size_t align256(size_t v) { return (v + 255) & ~size_t(255); }
 
-Ws carve(void* base, int W, int E)
+Ws carve(void* base, int W, int E, int gp_n = 0)
 {
     const size_t pairs = size_t(W) * size_t(E);
     Ws ws{};
@@ -82,6 +83,7 @@ Ws carve(void* base, int W, int E)
     ws.prior = reinterpret_cast<double*>(take(size_t(W) * sizeof(double)));
     ws.lle = reinterpret_cast<double*>(take(pairs * sizeof(double)));
     ws.done = reinterpret_cast<int*>(take(size_t(W) * sizeof(int)));
+    ws.res = gp_n > 0 ? reinterpret_cast<double*>(take(pairs * size_t(gp_n) * sizeof(double))) : nullptr;
     ws.total = off;
     return ws;
 }
@@ -640,6 +642,7 @@ struct LikeArgs {
     int ndim, half;
     unsigned long long seed, step;
     int* naccept;
+    double* res;  // MODE 2: [pairs][N] residuals for k_gp_like
 };
 
 
@@ -1101,7 +1104,7 @@ __device__ inline void finish_walker(const LikeArgs& L, int pair, int tid, bool 
 // ln_like of the residuals (a Kalman filter over each tile's sorted points,
 // run by wave 0 while the other waves wait at the tile barrier)
 template <int MODE>
-__global__ __launch_bounds__(LIKE_THREADS, (MODE == 2) ? 1 : LIKE_MINW) void k_lnlike(LikeArgs L)
+__global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
 {
     constexpr bool CHI = MODE != 0, GP = MODE == 2;
 #ifdef LFG_PROFILE_LIKE
@@ -1143,7 +1146,7 @@ __global__ __launch_bounds__(LIKE_THREADS, (MODE == 2) ? 1 : LIKE_MINW) void k_l
     // fused acceptance with one eclipse per walker: the proposal's coordinates
     // (one per lane), the uniform draw and the old ln_prob are fetched here,
     // off the tail of the block (combine_walker does it for E > 1)
-    const bool acc1 = CHI && L.pos && L.E == 1;
+    const bool acc1 = CHI && !GP && L.pos && L.E == 1;
     double aq = 0.0;
     if (acc1) {
         const int wg = L.half * L.npairs + pair;
@@ -1198,7 +1201,7 @@ __global__ __launch_bounds__(LIKE_THREADS, (MODE == 2) ? 1 : LIKE_MINW) void k_l
             if (L.comps)
                 for (int m = 0; m < 4; ++m) L.comps[(size_t(m) * L.npairs + pair) * n + p] = NAN;
         }
-        if (CHI) {
+        if (CHI && !GP) {  // GP trees: k_gp_like sees the status and finishes the pair
             if (tid == 0) L.lle[pair] = -INFINITY;
             finish_walker(L, pair, tid, acc1, aq, sacc1, sflag);
         }
@@ -1243,7 +1246,6 @@ __global__ __launch_bounds__(LIKE_THREADS, (MODE == 2) ? 1 : LIKE_MINW) void k_l
     const double* SG = sgeo;
     const int S = L.nsub;
     double chi = 0.0;
-    GPFilter gpf;  // GP mode, wave 0
     for (int t0 = 0; t0 < n; t0 += LIKE_TILE) {
         const int m = min(LIKE_TILE, n - t0);
         LIKE_STAMP(0);
@@ -1364,33 +1366,11 @@ __global__ __launch_bounds__(LIKE_THREADS, (MODE == 2) ? 1 : LIKE_MINW) void k_l
                 const double r = (L.y[p] - f) / L.ye[p];  // loaded here: no registers held over the passes
                 chi += isnan(f) ? INFINITY : r * r;
             }
-        }
-        if (GP) {
-            // residuals y - flux of the tile in LDS (the sweep buffers are free
-            // after the last pass); wave 0 carries the filter across tiles
-            if (own) {
-                TB.lo[tid] = px;
-                TB.hi[tid] = L.ye[p];
-                TB.iw[tid] = L.y[p] - (SG[G_WDF] * (1.0 - fw) + SG[G_DF] * (1.0 - fd) + SG[G_SF] * sbs / S +
-                                   SG[G_RSF] * srs / S);
-                TB.cell[tid] = gp_block(px, L.gp_ecl[2 * e], L.gp_ecl[2 * e + 1], SG[G_GP_DCP], SG[G_PHI0]);
-            }
-            __syncthreads();
-            if (wv == 0) {
-                if (t0 == 0) gpf.init(G[G_GP_AIN], G[G_GP_AOUT], 3.0 / (G[G_GP_LAM] * G[G_GP_LAM]));
-                for (int p = 0; p < m; ++p) gpf.step(TB.lo[p], TB.hi[p], TB.iw[p], TB.cell[p]);
-            }
-            __syncthreads();
+            if (GP) L.res[size_t(pair) * L.N + pi] = L.y[p] - f;  // the filter runs in k_gp_like
         }
         LIKE_STAMP(5);
     }
-    if (GP) {
-        if (tid == 0) {
-            const bool okp = G[G_GP_OK] != 0.0;
-            L.lle[pair] = (okp && n > 0) ? gpf.lnlike() : (okp ? 0.0 : -INFINITY);
-        }
-        finish_walker(L, pair, tid, acc1, aq, sacc1, sflag);
-    } else if (CHI) {
+    if (CHI && !GP) {
         chi = wave_sum(chi);
         if (lane == 0) red[0][wv] = chi;
         __syncthreads();
@@ -1401,6 +1381,132 @@ __global__ __launch_bounds__(LIKE_THREADS, (MODE == 2) ? 1 : LIKE_MINW) void k_l
         }
         finish_walker(L, pair, tid, acc1, aq, sacc1, sflag);
     }
+}
+
+// -------------------------------------------------------------- k_gp_like
+// GP trees (MODEL_SPEC 10.4): the Kalman filter over each pair's residuals
+// (k_lnlike<2> wrote them), one LANE per pair.  The recursion is serial in
+// the points, so a pair's cost is its dependent-latency chain whatever its
+// width; run as wave-uniform code on 64 lanes it cost 64x the VALU issue
+// and, with thousands of pairs, the SIMDs' issue rate set the time.  Lanes
+// of a wave take consecutive pairs (the eclipses of a few walkers); each
+// lane runs its pair's filter on its own points, the state-independent
+// work of a point (transition e^{-u}, changepoint block, log S) off the
+// recursion's dependent chain.  Then ln_like = -1/2 (sum v^2/S + sum ln S
+// + n ln 2 pi) and, as k_lnlike does, ln_prob and the acceptance of the
+// walker once its last eclipse is in.
+constexpr int GP_BLOCK = 64;
+constexpr int GP_CHUNK = 8;
+#ifndef GP_LANES
+#define GP_LANES 64  // pairs per wave (the other lanes idle)
+#endif
+
+__global__ __launch_bounds__(GP_BLOCK) void k_gp_like(LikeArgs L)
+{
+    const int pair = blockIdx.x * GP_LANES + threadIdx.x;
+    if (threadIdx.x >= GP_LANES || pair >= L.npairs) return;
+    const int e = pair % L.E;
+    const int o0 = L.off ? L.off[e] : 0;
+    const int n = L.off ? L.off[e + 1] - o0 : L.N;
+    const double* G = L.geo + size_t(pair) * LFG_NGEO;
+    double lle = -INFINITY;
+    if (L.status[pair] == ST_OK && G[G_GP_OK] != 0.0) {
+        const double ain = G[G_GP_AIN], aout = G[G_GP_AOUT], lam = G[G_GP_LAM];
+        const double dcp = G[G_GP_DCP], phi0 = G[G_PHI0];
+        const int e0 = L.gp_ecl[2 * e], e1 = L.gp_ecl[2 * e + 1];
+        const double* r = L.res + size_t(pair) * L.N;
+        const double* xs = L.x + o0;
+        const double* yes = L.ye + o0;
+        // state (D = P - Pinf, MODEL_SPEC 10.4)
+        double m0 = 0.0, m1 = 0.0, m2 = 0.0, m3 = 0.0;
+        double d00 = 0.0, d01 = 0.0, d11 = 0.0, d22 = 0.0, d23 = 0.0, d33 = 0.0;
+        double d02 = 0.0, d03 = 0.0, d12 = 0.0, d13 = 0.0;
+        double q2 = 0.0, lnS = 0.0, xprev = 0.0;
+        int bp = -1;
+        bool bad = false;
+        // points in chunks of GP_CHUNK: the chunk's loads are issued one
+        // chunk ahead, its transitions and blocks computed side by side,
+        // so that only the recursion itself is serial
+        double cx[GP_CHUNK], cy[GP_CHUNK], cr[GP_CHUNK];
+        auto fetch = [&](int p0, double* X, double* Y, double* Rr) {
+#pragma unroll
+            for (int k = 0; k < GP_CHUNK; ++k) {
+                const int q = min(p0 + k, n - 1);
+                X[k] = xs[q];
+                Y[k] = yes[q];
+                Rr[k] = r[q];
+            }
+        };
+        if (n > 0) fetch(0, cx, cy, cr);
+        for (int p0 = 0; p0 < n; p0 += GP_CHUNK) {
+            double a00[GP_CHUNK], a01[GP_CHUNK], a10[GP_CHUNK], a11[GP_CHUNK], ye2[GP_CHUNK], rv[GP_CHUNK];
+            int blk[GP_CHUNK];
+#pragma unroll
+            for (int k = 0; k < GP_CHUNK; ++k) {
+                const double dd = cx[k] - (k ? cx[k - 1] : xprev);
+                const double u = lam * dd, ex = exp(-u);
+                a00[k] = ex * (1.0 + u);
+                a01[k] = ex * dd;
+                a10[k] = -ex * lam * u;
+                a11[k] = ex * (1.0 - u);
+                ye2[k] = cy[k] * cy[k];
+                rv[k] = cr[k];
+                blk[k] = gp_block(cx[k], e0, e1, dcp, phi0);
+                bad = bad || (p0 + k < n && p0 + k > 0 && !(dd >= 0.0)) || (p0 + k < n && !isfinite(cr[k]));
+            }
+            xprev = cx[GP_CHUNK - 1];
+            if (p0 + GP_CHUNK < n) fetch(p0 + GP_CHUNK, cx, cy, cr);  // in flight during the recursion
+            double prodS = 1.0;  // one log per chunk (S ~ ye^2: eight factors stay far from underflow)
+#pragma unroll
+            for (int k = 0; k < GP_CHUNK; ++k) {
+                if (p0 + k >= n) break;
+                if (p0 + k > 0) {  // predict: m <- Phi m, D <- Phi D Phi^T per 2x2 block
+                    const double f00 = a00[k], f01 = a01[k], f10 = a10[k], f11 = a11[k];
+                    double t0 = f00 * m0 + f01 * m1;
+                    m1 = f10 * m0 + f11 * m1;
+                    m0 = t0;
+                    t0 = f00 * m2 + f01 * m3;
+                    m3 = f10 * m2 + f11 * m3;
+                    m2 = t0;
+                    GPFilter::sym(f00, f01, f10, f11, d00, d01, d11);
+                    GPFilter::sym(f00, f01, f10, f11, d22, d23, d33);
+                    const double t00 = f00 * d02 + f01 * d12, t01 = f00 * d03 + f01 * d13;
+                    const double t10 = f10 * d02 + f11 * d12, t11 = f10 * d03 + f11 * d13;
+                    d02 = t00 * f00 + t01 * f01;
+                    d03 = t00 * f10 + t01 * f11;
+                    d12 = t10 * f00 + t11 * f01;
+                    d13 = t10 * f10 + t11 * f11;
+                }
+                if (blk[k] >= 0 && blk[k] != bp) {  // a new block: its process starts stationary, independent
+                    m2 = m3 = 0.0;
+                    d22 = d23 = d33 = d02 = d03 = d12 = d13 = 0.0;
+                }
+                bp = blk[k];
+                const double a = (blk[k] >= 0) ? 1.0 : 0.0;
+                const double k0 = (d00 + ain) + a * d02, k1 = d01 + a * d12;
+                const double k2 = d02 + a * (d22 + aout), k3 = d03 + a * d23;
+                const double S = fma(a, k2, k0) + ye2[k];
+                const double v = rv[k] - fma(a, m2, m0);
+                const double iS = rcp_fast(S);  // v_rcp_f64 + one Newton step: ~1 ulp, off the IEEE divide's chain
+                bad = bad || !(S > 0.0) || !isfinite(v);
+                q2 = fma(v * v, iS, q2);
+                prodS *= S;
+                const double g = v * iS;
+                m0 = fma(k0, g, m0);
+                m1 = fma(k1, g, m1);
+                m2 = fma(k2, g, m2);
+                m3 = fma(k3, g, m3);
+                d00 -= k0 * k0 * iS; d01 -= k0 * k1 * iS; d11 -= k1 * k1 * iS;
+                d22 -= k2 * k2 * iS; d23 -= k2 * k3 * iS; d33 -= k3 * k3 * iS;
+                d02 -= k0 * k2 * iS; d03 -= k0 * k3 * iS; d12 -= k1 * k2 * iS; d13 -= k1 * k3 * iS;
+            }
+            lnS += log(prodS);
+        }
+        const double v = -0.5 * (q2 + lnS + n * 1.8378770664093454836);  // log(2 pi)
+        lle = (bad || !isfinite(v)) ? -INFINITY : v;
+    }
+    L.lle[pair] = lle;
+    combine_after(L, pair);
 }
 
 // -------------------------------------------------------------- k_combine
@@ -1642,6 +1748,12 @@ size_t lfg_workspace_size(int W, int E)
     return carve(nullptr, W, E).total;
 }
 
+size_t lfg_workspace_size_tree(int W, const lfg_tree* T)
+{
+    if (W <= 0 || !T || T->E <= 0) return 0;
+    return carve(nullptr, W, T->E, T->gp ? T->max_n : 0).total;
+}
+
 int lfg_flux(const double* pars, int W, int P, const double* x, const double* w, int N, int nsub,
              double* flux, double* comps, int* status, void* wsp, size_t ws_bytes, void* stream)
 {
@@ -1689,7 +1801,7 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
                        const Propose* prop = nullptr)
 {
     if (W <= 0 || !T || T->E <= 0 || T->ndim <= 0 || T->nsub < 1 || !walkers || (!lnp && !acc)) return LFG_E_ARGS;
-    Ws ws = carve(wsp, W, T->E);
+    Ws ws = carve(wsp, W, T->E, T->gp ? T->max_n : 0);
     if (!wsp || ws_bytes < ws.total) return LFG_E_WORKSPACE;
     hipStream_t st = static_cast<hipStream_t>(stream);
     auto mark = [&](int i) {
@@ -1719,8 +1831,14 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
                true, acc ? acc->pos : nullptr, acc ? acc->lnp : nullptr, walkers, acc ? acc->zfac : nullptr,
                T->ndim, acc ? acc->half : 0, acc ? acc->seed : 0ull, acc ? acc->step : 0ull,
                acc ? acc->naccept : nullptr};
-    if (T->gp) hipLaunchKernelGGL(k_lnlike<2>, dim3(npairs), dim3(LIKE_THREADS), 0, st, L);
-    else hipLaunchKernelGGL(k_lnlike<1>, dim3(npairs), dim3(LIKE_THREADS), 0, st, L);
+    if (T->gp) {
+        L.res = ws.res;
+        hipLaunchKernelGGL(k_lnlike<2>, dim3(npairs), dim3(LIKE_THREADS), 0, st, L);
+        if ((rc = launch_ok())) return rc;
+        hipLaunchKernelGGL(k_gp_like, dim3((npairs + GP_LANES - 1) / GP_LANES), dim3(GP_BLOCK), 0, st, L);
+    } else {
+        hipLaunchKernelGGL(k_lnlike<1>, dim3(npairs), dim3(LIKE_THREADS), 0, st, L);
+    }
     if ((rc = launch_ok())) return rc;
     mark(3);
     return LFG_OK;

@@ -41,9 +41,9 @@ def test_tree_struct_layout_matches_ctypes(tmp_path):
 #include <stddef.h>
 #include "lfg.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(lfg_tree), offsetof(lfg_tree, gather),
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(lfg_tree), offsetof(lfg_tree, gather),
          offsetof(lfg_tree, x), offsetof(lfg_tree, prior_norm), offsetof(lfg_tree, roche_priors),
-         offsetof(lfg_tree, gp_gather), offsetof(lfg_tree, gp_ecl));
+         offsetof(lfg_tree, gp_gather), offsetof(lfg_tree, gp_ecl), offsetof(lfg_tree, fixed_invalid));
   return 0;
 }''')
     exe = tmp_path / "layout"
@@ -51,7 +51,7 @@ int main(void) {
     got = list(map(int, subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()))
     T = _native.LfgTree
     assert got == [ctypes.sizeof(T), T.gather.offset, T.x.offset, T.prior_norm.offset, T.roche_priors.offset,
-                   T.gp_gather.offset, T.gp_ecl.offset]
+                   T.gp_gather.offset, T.gp_ecl.offset, T.fixed_invalid.offset]
 
 
 def test_constants_agree_with_header():

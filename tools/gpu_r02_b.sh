@@ -1,0 +1,5 @@
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+tools/gpu_steps.sh \
+ "gptest:300:python -u -m pytest tests/test_gpu_lnprob.py tests/test_mcmcfit.py -x -v --timeout 120 --timeout-method thread -k 'gp or GP or lnprior or fit'" \
+ "benchgp:200:python bench.py --config gp --steps 50 --warmup 3 --no-cpu > gpurun_out/bench_r02_gp_b.json" \
+ "profgp:200:rocprofv3 --kernel-trace --stats -d gpurun_out/prof_gp_b -o run -- python3 bench.py --config gp --steps 20 --warmup 2 --no-cpu"
