@@ -185,13 +185,17 @@ def build_model(args, flux_fn):
     return synthetic.config_single(npts=args.npts, flux_fn=flux_fn, nsub=args.nsub)
 
 
-def flops_per_pair(npts, nsub, gp):
+def flops_per_pair(npts, nsub, gp, fused=True):
     """Counted algorithmic FP64 FLOPs of one walker-eclipse evaluation, by
-    kernel (MODEL_SPEC.md section 11)."""
+    kernel (MODEL_SPEC.md section 11).  With the fused element phase
+    (liblfg's default) k_lnlike solves the elements too."""
     acc = npts * nsub * (N_ECL * F_ACC_ECL + N_DON * F_ACC_DON + F_POINT)
     if gp:
         acc += npts * F_GP_POINT
-    return {"k_setup": F_SETUP, "k_elements": N_ROOTS * F_GEOM_ROOT, "k_lnlike": acc}
+    geom = N_ROOTS * F_GEOM_ROOT
+    if fused:
+        return {"k_setup": F_SETUP, "k_elements": 0.0, "k_lnlike": geom + acc}
+    return {"k_setup": F_SETUP, "k_elements": geom, "k_lnlike": acc}
 
 
 def pmc_row(kernel):
@@ -363,7 +367,8 @@ def run(args):
     acc = float(np.mean(S.acceptance_fraction))
 
     # ---- FP64 roofline on counted algorithmic FLOPs (MODEL_SPEC 11)
-    fpp = flops_per_pair(npts, tree.nsub, tree.gp)
+    fused = b"fused" in L.lfg_version()
+    fpp = flops_per_pair(npts, tree.nsub, tree.gp, fused)
     f_eval = E * sum(fpp.values())                       # per walker evaluation
     tf = value / world * f_eval / 1e12                   # per GPU, whole step
     pairs = shard * E
@@ -371,6 +376,8 @@ def run(args):
     dom_tf = dom_flops / (avg_dom * 1e-3) / 1e12
     kern = {}
     for n, m in calib.items():
+        if fused and n == "k_elements":
+            continue  # no such launch: k_lnlike's element phase
         f = fpp[n] * pairs
         kern[n] = {"warmup_ms": m, "alg_flops_per_launch": f,
                    "tflops": f / (m * 1e-3) / 1e12 if m > 0 else None,
@@ -380,7 +387,7 @@ def run(args):
     half_s = elapsed / args.steps / 2.0
     hbm_bytes = shard * (8 * tree.ndim + 8) + 32 * npts * E
     hbm_gbs = hbm_bytes / half_s / 1e9
-    mat = MATERIALISED_PER_PAIR[kname] * pairs
+    mat = 0 if fused else MATERIALISED_PER_PAIR[kname] * pairs
 
     # counter-derived traffic and executed FP64 FLOPs of the dominant kernel
     # (rocprofv3 --pmc passes, tools/pmc_profile.sh -> profiles/r0N/pmc_traffic.json);

@@ -643,6 +643,7 @@ struct LikeArgs {
     unsigned long long seed, step;
     int* naccept;
     double* res;  // MODE 2: [pairs][N] residuals for k_gp_like
+    const int* bstatus;  // fused element phase: the stream lanes' status (folded into status here)
 };
 
 
@@ -1040,9 +1041,8 @@ __device__ __noinline__ double2 direct_wd_disc(const double2* __restrict__ AB, c
 }
 
 // direct (point-major) spot eclipse fraction and donor sum for one point
-__device__ __noinline__ double2 direct_spot_donor(const double2* __restrict__ ABs, const double* __restrict__ sbw,
-                                            const double* __restrict__ DONp, double ph, double h, double e0,
-                                            double e1, double c, double itb)
+__device__ __noinline__ double2 direct_spot_donor(const double2* ABs, const double* sbw, const double* DONp, double ph,
+                                                  double h, double e0, double e1, double c, double itb)
 {
     double eb = 0.0, D = 0.0;
     const double l2 = ph - h, h2 = ph + h;
@@ -1060,6 +1060,126 @@ __device__ __noinline__ double2 direct_spot_donor(const double2* __restrict__ AB
         D += fmax(A1 + fmax(y, A1), 0.0) + fmax(A2 + fmax(y, A2), 0.0);
     }
     return make_double2(eb, D);
+}
+
+
+// ---- the fused element phase of k_lnlike (FUSED = true) ----
+// k_elements' item body (MODEL_SPEC 5, 4.3) with its outputs in the block's
+// LDS instead of HBM: WD/disc intervals in sweep order into `stage`, spot
+// intervals and weights into sab / sbw, donor tiles into sdq, disc ring
+// weights and the disc total into swt.  ABg (nullable): the pair's global
+// interval table, kept only when a window of the pair is unsorted and the
+// direct (point-major) WD/disc path may need every interval.
+__device__ __noinline__ void element_item(int u, const double* __restrict__ G, double2* stage, double2* sab,
+                                             double* sbw, double* sdq, double* swt, double2* ABg)
+{
+    const Roche R{G[G_Q], G[G_CA], G[G_CB], G[G_MU], G[G_XL1], G[G_PL1], G[G_RS], G[G_RS2]};
+    const double s = G[G_S], c = G[G_C];
+    if (u >= U_WD + U_DISC && u < U_MAIN) {  // donor tile (MODEL_SPEC 5.4), phi' in (0, pi/2)
+        const int uu = u - (U_WD + U_DISC);
+        const int it = uu / (NDONOR_P / 4), ip = uu - it * (NDONOR_P / 4);
+        const double stc = kDonSt[it], ctc = kDonCt[it];
+        const double dx = -ctc, dy = stc * kDonCp[ip], dz = stc * kDonSp[ip];
+        double lo = 0.0, hi = R.Rs, r = G[G_REFF];
+        if (!(r > lo && r < hi)) r = 0.5 * hi;
+        double gx, gy, gz;
+        for (int itr = 0; itr < ROOT_MAXIT; ++itr) {
+            const double X0 = fma(r, dx, 1.0), X1 = r * dy, X2 = r * dz;
+            const double f = rpot_grad(R, X0, X1, X2, gx, gy, gz) - R.pl1;
+            const double df = gx * dx + gy * dy + gz * dz;
+            if (f > 0.0) hi = r; else lo = r;
+            if (df > 0.0 && fabs(f / df) <= ROOT_LAST) { r -= f / df; break; }
+            double rn = (df > 0.0) ? r - f / df : 0.5 * (lo + hi);
+            if (!(rn > lo && rn < hi)) rn = 0.5 * (lo + hi);
+            r = rn;
+        }
+        rgrad(R, fma(r, dx, 1.0), r * dy, r * dz, gx, gy, gz);
+        const double ig = rsqrt(gx * gx + gy * gy + gz * gz);
+        const double nx = gx * ig, ny = gy * ig, nz = gz * ig;
+        const double dA = r * r * kDonOmega[it] / (nx * dx + ny * dy + nz * dz);
+        const double vx = dA * nx, vy = dA * ny, vz = dA * nz;
+        const double srho = s * sqrt(vx * vx + vy * vy);
+        const double kap = (srho > 0.0) ? -c * vz / srho : (c * vz > 0.0 ? -2.0 : 2.0);
+        double* D = sdq + uu * DON_STRIDE;
+        D[0] = vx;
+        D[1] = vy;
+        D[2] = vz;
+        D[3] = -atan2(vy, vx) * (1.0 / TWO_PI);
+        D[4] = acos(fmin(fmax(kap, -1.0), 1.0)) * (1.0 / TWO_PI);
+        return;
+    }
+    double Px, Py, Pz;
+    int k, km;
+    if (u < U_WD) {  // white dwarf tile (MODEL_SPEC 5.1), cos(psi) > 0 half
+        const int ir = wd_ring_of(u);
+        const int nk = 4 * (2 * ir + 1), q4 = nk / 4, jj = u - 2 * ir * ir;
+        const int j = (jj < q4) ? jj : jj - q4 + 3 * q4;
+        const int jm = (j < nk / 2) ? nk / 2 - 1 - j : 3 * nk / 2 - 1 - j;
+        k = 4 * ir * ir + j;
+        km = 4 * ir * ir + jm;
+        const double rc = kWdRc[ir], mu0 = kWdMu0[ir];
+        const double cp = kWdCos[u], sp = kWdSin[u];
+        const double rw = G[G_RWD];
+        Px = rw * (-rc * sp * c + mu0 * s);
+        Py = rw * (rc * cp);
+        Pz = rw * (rc * sp * s + mu0 * c);
+    } else if (u < U_WD + U_DISC) {  // disc (MODEL_SPEC 5.2), alpha in (0, pi)
+        const int uu = u - U_WD;
+        const int ir = uu / (NDISC_AZ / 2), j = uu - ir * (NDISC_AZ / 2);
+        k = NWD + ir * NDISC_AZ + j;
+        km = NWD + ir * NDISC_AZ + NDISC_AZ - 1 - j;
+        const double rin = G[G_RWD];
+        const double rc = rin + (ir + 0.5) * ((G[G_RDISC] - rin) / NDISC_R);
+        if (j == 0) {
+            swt[WT_DISC + ir] = disc_ring_weight(ir, G);
+            if (ir == 0) swt[WT_TD] = TWO_PI * (disc_boundary(NDISC_R, G) - disc_boundary(0, G));
+        }
+        Px = rc * kDiscCos[j];
+        Py = rc * kDiscSin[j];
+        Pz = 0.0;
+    } else {  // bright-spot strip (MODEL_SPEC 5.3): no mirror partner
+        const int j = u - U_MAIN;
+        k = km = NWD + NDISC + j;
+        const double uk = (j + 0.5) * (G[G_UMAX] / NBS);
+        sbw[j] = bs_weight(j, G);
+        const double off = G[G_L] * (uk - G[G_UPK]);
+        Px = fma(off, G[G_CAZ], G[G_BSX]);
+        Py = fma(off, G[G_SAZ], G[G_BSY]);
+        Pz = 0.0;
+    }
+    double a, b;
+    element_interval_fast(R, Px, Py, Pz, s, c, G[G_RCAL], G[G_REFF], a, b);
+    if (k >= NWD + NDISC) {
+        sab[k - NWD - NDISC] = make_double2(a, b);
+        if (ABg) ABg[k] = make_double2(a, b);
+        return;
+    }
+    const double2 mir = (a < b) ? make_double2(-b, -a) : make_double2(1.0, -1.0);
+    stage[slot_of(k)] = make_double2(a, b);
+    stage[slot_of(km)] = mir;
+    if (ABg) {
+        ABg[slot_of(k)] = make_double2(a, b);
+        ABg[slot_of(km)] = mir;
+    }
+}
+
+// does every exposure window of the pair's points come in sorted order
+// (the sweep's precondition; MODEL_SPEC 6 restated)?  1 when not: the
+// direct WD/disc path will need the global interval table
+__device__ __forceinline__ int windows_unsorted(const LikeArgs& L, int o0, int n, double phi0, int tid)
+{
+    int bad = 0;
+    for (int p = tid; p < n; p += LIKE_THREADS) {
+        const double hw = L.w ? L.w[o0 + p] : 0.0;
+        const double ph = wrap_phase(L.x[o0 + p] - phi0);
+        bad |= (hw >= 0.0) ? 0 : 1;
+        if (p > 0) {
+            const double hwb = L.w ? L.w[o0 + p - 1] : 0.0;
+            const double phb = wrap_phase(L.x[o0 + p - 1] - phi0);
+            bad |= (ph - hw < phb - hwb || ph + hw < phb + hwb) ? 1 : 0;
+        }
+    }
+    return bad;
 }
 
 #ifdef LFG_PROFILE_LIKE  // diagnostic build only: phase stamps (first tile) into spare geo slots 41..46
@@ -1103,7 +1223,9 @@ __device__ inline void finish_walker(const LikeArgs& L, int pair, int tid, bool 
 // MODE 0: flux (and components) only; 1: fused chi^2 -> ln_like; 2: GP
 // ln_like of the residuals (a Kalman filter over each tile's sorted points,
 // run by wave 0 while the other waves wait at the tile barrier)
-template <int MODE>
+// FUSED: the pair's element intervals are solved in this block (the
+// element phase) straight into LDS, instead of read from k_elements' table
+template <int MODE, bool FUSED>
 __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
 {
     constexpr bool CHI = MODE != 0, GP = MODE == 2;
@@ -1131,6 +1253,7 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
     __shared__ long long spart[6][LIKE_THREADS / 64];
     __shared__ double red[3][LIKE_THREADS / 64];
     __shared__ int sflag[2];
+    __shared__ double swt[FUSED ? WT_N : 1];      // fused: disc ring weights and total (spot weights in sbw)
 
     constexpr int nt = LIKE_THREADS, nw = LIKE_THREADS / 64;
     const int pair = blockIdx.x;
@@ -1158,42 +1281,91 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
             sacc1[2] = L.lnp_ens[wg];
         }
     }
-    // every global load of the prologue is issued before anything waits on
-    // one (the status included): a single memory round trip
-    const int st = L.status[pair];
-    const double s = G[G_S], c = G[G_C], ul = G[G_ULIMB];
-    const double td = Wt[WT_TD];
+    int st;
+    double s, c, ul, td;
     double px = 0.0, pw = 0.0;  // tile-0 point of this thread (y, ye: read where chi^2 is formed)
-    if (tid < n) {
-        px = L.x[o0 + tid];
-        pw = L.w ? L.w[o0 + tid] : 0.0;
-    }
     // this thread's sweep items, held in registers for every tile: WD/disc
     // elements sweep_item(tid + i nt) with their ring weights, spot element
     // tid (< NBS), donor tile (last NDONOR lanes)
     constexpr int NI = (NWD + NDISC + nt - 1) / nt;
     double2 abk[NI];
-    for (int i = 0; i < NI; ++i) {
-        const int g = tid + i * nt;
-        abk[i] = (g < NWD + NDISC) ? AB[g] : make_double2(1.0, -1.0);
-    }
     double2 abB = make_double2(1.0, -1.0);
     double wB = 0.0;
     double dq[DON_STRIDE] = {0.0, 0.0, 0.0, 0.0, 0.0};
-    if (tid < NBS) {
-        abB = AB[NWD + NDISC + tid];
-        wB = Wt[WT_BS + tid];
-    } else if (tid >= nt - NDONOR) {
-        const int t = tid - (nt - NDONOR);
-        for (int i = 0; i < DON_STRIDE; ++i) dq[i] = DONp[(t >> 2) * DON_STRIDE + i];
-    }
-    double gv = 0.0;  // one geometry word per lane for sgeo
-    if (tid >= NBS + NWD_RINGS + NDISC_R && tid < NBS + NWD_RINGS + NDISC_R + G_COUNT)
-        gv = G[tid - (NBS + NWD_RINGS + NDISC_R)];
+    double gv = 0.0;     // one geometry word per lane for sgeo
     double wring = 0.0;  // ring weights for the direct path
-    if (tid >= NBS && tid < NBS + NWD_RINGS) wring = wd_ring_weight(tid - NBS, ul);
-    else if (tid >= NBS + NWD_RINGS && tid < NBS + NWD_RINGS + NDISC_R)
-        wring = Wt[WT_DISC + tid - NBS - NWD_RINGS];
+    if constexpr (FUSED) {
+        // the element phase: status (setup failures first, then the stream:
+        // MODEL_SPEC 6), geometry into LDS, every symmetry-unique element of
+        // the pair solved by the block's lanes into LDS
+        st = L.status[pair];
+        const int bst = L.bstatus[pair];
+        if (st == ST_OK && bst != ST_OK) st = bst;
+        if (tid < G_COUNT) sgeo[tid] = G[tid];
+        if (tid < n) {
+            px = L.x[o0 + tid];
+            pw = L.w ? L.w[o0 + tid] : 0.0;
+        }
+        if (tid == 0) {
+            sflag[0] = 0;
+            if (st != L.status[pair]) const_cast<int*>(L.status)[pair] = st;
+        }
+        __syncthreads();
+        if (st == ST_OK) {
+            if (windows_unsorted(L, o0, n, sgeo[G_PHI0], tid)) atomicOr(&sflag[0], 1);
+            __syncthreads();
+            double2* stage = reinterpret_cast<double2*>(&sacc[0][0]);  // free until the first pass
+            double2* ABg = sflag[0] ? const_cast<double2*>(AB) : nullptr;
+            for (int u = tid; u < NUNIQ; u += nt) element_item(u, sgeo, stage, sab, sbw, sdq, swt, ABg);
+            __syncthreads();
+            for (int i = 0; i < NI; ++i) {
+                const int g = tid + i * nt;
+                abk[i] = (g < NWD + NDISC) ? stage[g] : make_double2(1.0, -1.0);
+            }
+            if (tid < NBS) {
+                abB = sab[tid];
+                wB = sbw[tid];
+            } else if (tid >= nt - NDONOR) {
+                const int t = tid - (nt - NDONOR);
+                for (int i = 0; i < DON_STRIDE; ++i) dq[i] = sdq[(t >> 2) * DON_STRIDE + i];
+            }
+        }
+        s = sgeo[G_S];
+        c = sgeo[G_C];
+        ul = sgeo[G_ULIMB];
+        td = swt[WT_TD];
+        if (tid >= NBS && tid < NBS + NWD_RINGS) wring = wd_ring_weight(tid - NBS, ul);
+        else if (tid >= NBS + NWD_RINGS && tid < NBS + NWD_RINGS + NDISC_R)
+            wring = swt[WT_DISC + tid - NBS - NWD_RINGS];
+    } else {
+        // every global load of the prologue is issued before anything waits on
+        // one (the status included): a single memory round trip
+        st = L.status[pair];
+        s = G[G_S];
+        c = G[G_C];
+        ul = G[G_ULIMB];
+        td = Wt[WT_TD];
+        if (tid < n) {
+            px = L.x[o0 + tid];
+            pw = L.w ? L.w[o0 + tid] : 0.0;
+        }
+        for (int i = 0; i < NI; ++i) {
+            const int g = tid + i * nt;
+            abk[i] = (g < NWD + NDISC) ? AB[g] : make_double2(1.0, -1.0);
+        }
+        if (tid < NBS) {
+            abB = AB[NWD + NDISC + tid];
+            wB = Wt[WT_BS + tid];
+        } else if (tid >= nt - NDONOR) {
+            const int t = tid - (nt - NDONOR);
+            for (int i = 0; i < DON_STRIDE; ++i) dq[i] = DONp[(t >> 2) * DON_STRIDE + i];
+        }
+        if (tid >= NBS + NWD_RINGS + NDISC_R && tid < NBS + NWD_RINGS + NDISC_R + G_COUNT)
+            gv = G[tid - (NBS + NWD_RINGS + NDISC_R)];
+        if (tid >= NBS && tid < NBS + NWD_RINGS) wring = wd_ring_weight(tid - NBS, ul);
+        else if (tid >= NBS + NWD_RINGS && tid < NBS + NWD_RINGS + NDISC_R)
+            wring = Wt[WT_DISC + tid - NBS - NWD_RINGS];
+    }
 
     if (st != ST_OK) {
         for (int p = tid; p < n; p += nt) {
@@ -1209,7 +1381,7 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
     }
     double tb = 0.0, dn = 0.0, vs = 0.0;
     if (tid < NBS) {
-        sbw[tid] = wB;
+        if (!FUSED) sbw[tid] = wB;
         tb = wB;
     } else if (tid >= nt - NDONOR) {
         // donor normalisation at quadrature (theta = pi/2): e = (0, -s, c)
@@ -1219,11 +1391,13 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
         vs = fabs(dq[0]) + fabs(dq[1]) + fabs(dq[2]);
     }
     if (tid >= NBS && tid < NBS + NWD_RINGS + NDISC_R) swr[tid - NBS] = wring;
-    if (tid >= NBS + NWD_RINGS + NDISC_R && tid < NBS + NWD_RINGS + NDISC_R + G_COUNT)
-        sgeo[tid - (NBS + NWD_RINGS + NDISC_R)] = gv;
-    if (tid < NBS) sab[tid] = abB;
-    else if (tid >= nt - NDONOR && ((tid - (nt - NDONOR)) & 3) == 0)
-        for (int i = 0; i < DON_STRIDE; ++i) sdq[((tid - (nt - NDONOR)) >> 2) * DON_STRIDE + i] = dq[i];
+    if (!FUSED) {
+        if (tid >= NBS + NWD_RINGS + NDISC_R && tid < NBS + NWD_RINGS + NDISC_R + G_COUNT)
+            sgeo[tid - (NBS + NWD_RINGS + NDISC_R)] = gv;
+        if (tid < NBS) sab[tid] = abB;
+        else if (tid >= nt - NDONOR && ((tid - (nt - NDONOR)) & 3) == 0)
+            for (int i = 0; i < DON_STRIDE; ++i) sdq[((tid - (nt - NDONOR)) >> 2) * DON_STRIDE + i] = dq[i];
+    }
     tb = wave_sum(tb);
     dn = wave_sum(dn);
     vs = wave_sum(vs);
@@ -1320,7 +1494,7 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
                 } else if (own) {  // unsorted / mixed widths: every element against this point
                     const double ulg = SG[G_ULIMB];
                     const double2 f2 = direct_wd_disc(AB, swr, phc, wk, TWO_PI * ((1.0 - ulg) * 0.5 + ulg / 3.0),
-                                                      Wt[WT_TD]);
+                                                      FUSED ? swt[WT_TD] : Wt[WT_TD]);
                     fw = f2.x;
                     fd = f2.y;
                 }
@@ -1334,7 +1508,7 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
                 eb = double(r[2]) * FX_INV;
                 D = (e0 * double(r[3]) + e1 * double(r[4]) + cg * double(r[5])) * (FX_INV * snorm[3]);
             } else if (own) {
-                const double2 ed2 = direct_spot_donor(AB + NWD + NDISC, sbw, DONp, ph, h, e0, e1, cg, snorm[0]);
+                const double2 ed2 = direct_spot_donor(sab, sbw, sdq, ph, h, e0, e1, cg, snorm[0]);
                 eb = ed2.x;
                 D = ed2.y;
             }
@@ -1719,7 +1893,19 @@ inline int launch_ok() { return hipGetLastError() == hipSuccess ? LFG_OK : LFG_E
 // k_setup (setup, prior and stream lanes) then k_elements, on the caller's
 // stream.  ev (nullable, LFG_NEV events): 0 before k_setup, 1 after k_setup,
 // 2 after k_elements
-int run_front(const SetupArgs& S, const Ws& ws, hipStream_t st, void* const* ev)
+// k_elements then k_lnlike<MODE, false>.  A build with LFG_FUSED solves the
+// elements inside k_lnlike instead (k_lnlike<MODE, true>): measured at
+// config 2 it is slower, 64.5 us vs 33.7 + 28.3 us (its element phase runs
+// at 4 waves/SIMD with a 1.76-round item imbalance per block, where
+// k_elements' independent one-wave blocks keep 5 waves/SIMD busy;
+// profiles/r02/bench_c2_fused_by_grid.txt), so it stays an option
+#ifdef LFG_FUSED
+constexpr bool kFused = true;
+#else
+constexpr bool kFused = false;
+#endif
+
+int run_front(const SetupArgs& S, const Ws& ws, hipStream_t st, void* const* ev, bool elements = !kFused)
 {
     auto mark = [&](int i) {
         if (ev && ev[i]) (void)hipEventRecord(static_cast<hipEvent_t>(ev[i]), st);
@@ -1730,10 +1916,12 @@ int run_front(const SetupArgs& S, const Ws& ws, hipStream_t st, void* const* ev)
     hipLaunchKernelGGL(k_setup, dim3((nlanes + SETUP_BLOCK - 1) / SETUP_BLOCK), dim3(SETUP_BLOCK), 0, st, S);
     if (launch_ok() != LFG_OK) return LFG_E_LAUNCH;
     mark(1);
-    constexpr int chunks = (NUNIQ + ELEM_BLOCK - 1) / ELEM_BLOCK;
-    hipLaunchKernelGGL(k_elements, dim3(unsigned(npairs) * chunks), dim3(ELEM_BLOCK), 0, st, ws.geo, ws.status,
-                       npairs, ws.ab, ws.donor, ws.wts, ws.bstatus);
-    if (launch_ok() != LFG_OK) return LFG_E_LAUNCH;
+    if (elements) {
+        constexpr int chunks = (NUNIQ + ELEM_BLOCK - 1) / ELEM_BLOCK;
+        hipLaunchKernelGGL(k_elements, dim3(unsigned(npairs) * chunks), dim3(ELEM_BLOCK), 0, st, ws.geo, ws.status,
+                           npairs, ws.ab, ws.donor, ws.wts, ws.bstatus);
+        if (launch_ok() != LFG_OK) return LFG_E_LAUNCH;
+    }
     mark(2);
     return LFG_OK;
 }
@@ -1769,7 +1957,8 @@ int lfg_flux(const double* pars, int W, int P, const double* x, const double* w,
         LikeArgs L{ws.geo, ws.status, ws.ab, ws.donor, ws.wts, 1, nullptr, N, x, nullptr, nullptr, w,
                    nsub, flux, comps, nullptr, W, nullptr, nullptr, nullptr, nullptr, false, nullptr,
                    nullptr, nullptr, nullptr, 0, 0, 0ull, 0ull, nullptr};
-        hipLaunchKernelGGL(k_lnlike<0>, dim3(W), dim3(LIKE_THREADS), 0, st, L);
+        L.bstatus = ws.bstatus;
+        hipLaunchKernelGGL((k_lnlike<0, kFused>), dim3(W), dim3(LIKE_THREADS), 0, st, L);
         if ((rc = launch_ok())) return rc;
     }
     if (status && hipMemcpyAsync(status, ws.status, sizeof(int) * W, hipMemcpyDeviceToDevice, st) != hipSuccess)
@@ -1831,13 +2020,14 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
                true, acc ? acc->pos : nullptr, acc ? acc->lnp : nullptr, walkers, acc ? acc->zfac : nullptr,
                T->ndim, acc ? acc->half : 0, acc ? acc->seed : 0ull, acc ? acc->step : 0ull,
                acc ? acc->naccept : nullptr};
+    L.bstatus = ws.bstatus;
     if (T->gp) {
         L.res = ws.res;
-        hipLaunchKernelGGL(k_lnlike<2>, dim3(npairs), dim3(LIKE_THREADS), 0, st, L);
+        hipLaunchKernelGGL((k_lnlike<2, kFused>), dim3(npairs), dim3(LIKE_THREADS), 0, st, L);
         if ((rc = launch_ok())) return rc;
         hipLaunchKernelGGL(k_gp_like, dim3((npairs + GP_LANES - 1) / GP_LANES), dim3(GP_BLOCK), 0, st, L);
     } else {
-        hipLaunchKernelGGL(k_lnlike<1>, dim3(npairs), dim3(LIKE_THREADS), 0, st, L);
+        hipLaunchKernelGGL((k_lnlike<1, kFused>), dim3(npairs), dim3(LIKE_THREADS), 0, st, L);
     }
     if ((rc = launch_ok())) return rc;
     mark(3);
@@ -2002,7 +2192,7 @@ int lfg_elements(const double* pars, int W, int P, double* a, double* b, double*
     hipStream_t st = static_cast<hipStream_t>(stream);
     SetupArgs S{pars, W, P, 1, P, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
                 ws.geo, ws.status, ws.prior, ws.bstatus, 0, nullptr, nullptr, nullptr};
-    int rc = run_front(S, ws, st, nullptr);
+    int rc = run_front(S, ws, st, nullptr, true);  // the white-box tables come from k_elements
     if (rc) return rc;
     if (a || b || wgt || donor) {
         const long nt = long(W) * NEL;
@@ -2047,7 +2237,7 @@ int lfg_gp_lnlike(const double* x, const double* ye, const double* res, int W, i
     return launch_ok();
 }
 
-const char* lfg_version(void) { return "lfg 0.1.0 gfx950 fp64"; }
+const char* lfg_version(void) { return kFused ? "lfg 0.2.0 gfx950 fp64 fused-elements" : "lfg 0.2.0 gfx950 fp64"; }
 
 #ifdef LFG_COUNT_ITERS
 // diagnostic builds only: read and clear the iteration counters of k_elements
