@@ -77,6 +77,17 @@ __device__ __forceinline__ double rsqrt_pos(double x)
     return fma(y * e, fma(e, 0.375, 0.5), y);
 }
 
+// 1/x for finite x != 0: v_rcp_f64 and one Newton correction (the IEEE
+// quotient's div_scale/div_fmas/div_fixup sequence is ~10 issue slots; a
+// Newton step only needs its length to a few ulp -- the root it converges to
+// is fixed by F = 0, not by the step; on the serial setup chains every IEEE
+// quotient is ~7 dependent levels more than this)
+__device__ __forceinline__ double rcp_fast(double x)
+{
+    const double y = __builtin_amdgcn_rcp(x);
+    return fma(y, fma(-x, y, 1.0), y);
+}
+
 __device__ __forceinline__ double rpot(const Roche& R, double x, double y, double z)
 {
     const double dx = x - 1.0;
@@ -116,16 +127,17 @@ __device__ __forceinline__ void rgrad(const Roche& R, double x, double y, double
 // MODEL_SPEC 4.1: L1 point, safeguarded Newton on dPhi/dx (monotone on (0,1))
 __device__ inline double xl1_solve(double q)
 {
-    const double cA = 2.0 / (1.0 + q), cB = q * cA, mu = q / (1.0 + q);
+    const double i1q = rcp_fast(1.0 + q);
+    const double cA = 2.0 * i1q, cB = q * cA, mu = q * i1q;
     double lo = 0.0, hi = 1.0;
-    double x = 1.0 - cbrt(q / (3.0 * (1.0 + q)));
+    double x = 1.0 - cbrt(mu * (1.0 / 3.0));
     for (int it = 0; it < 200; ++it) {
         const double omx = 1.0 - x;
-        const double ix = 1.0 / x, io = 1.0 / omx;
+        const double ix = rcp_fast(x), io = rcp_fast(omx);
         const double f = cA * ix * ix - cB * io * io - 2.0 * (x - mu);
         const double df = -2.0 * cA * ix * ix * ix - 2.0 * cB * io * io * io - 2.0;
         if (f > 0.0) lo = x; else hi = x;
-        const double step = f / df;
+        const double step = f * rcp_fast(df);
         if (fabs(step) <= ROOT_LAST) { x -= step; break; }  // converged: last Newton step
         double xn = x - step;
         if (!(xn > lo && xn < hi)) xn = 0.5 * (lo + hi);
@@ -138,9 +150,10 @@ __device__ inline int roche_init(Roche& R, double q)
 {
     if (!(q > 0.0) || !isfinite(q)) return ST_BAD_Q;
     R.q = q;
-    R.cA = 2.0 / (1.0 + q);
+    const double i1q = rcp_fast(1.0 + q);
+    R.cA = 2.0 * i1q;
     R.cB = q * R.cA;
-    R.mu = q / (1.0 + q);
+    R.mu = q * i1q;
     R.xl1 = xl1_solve(q);
     R.pl1 = rpot(R, R.xl1, 0.0, 0.0);
     R.Rs = 1.0 - R.xl1;
@@ -359,16 +372,6 @@ struct Tan {
     double th, cs, sn, t;
     int st;
 };
-
-// 1/x for finite x != 0: v_rcp_f64 and one Newton correction (the IEEE
-// quotient's div_scale/div_fmas/div_fixup sequence is ~10 issue slots; a
-// Newton step only needs its length to a few ulp -- the root it converges to
-// is fixed by F = 0, not by the step)
-__device__ __forceinline__ double rcp_fast(double x)
-{
-    const double y = __builtin_amdgcn_rcp(x);
-    return fma(y, fma(-x, y, 1.0), y);
-}
 
 // one branch-free step (two solves can run interleaved in one lane)
 __device__ __forceinline__ void tangency_step(const Roche& R, double Px, double Py, double Pz, double s, double c,
@@ -604,7 +607,7 @@ __device__ inline int findi_fast(const Roche& R, double dphi, double& inc_deg)
                 const double gx = i1 * x + i2 * dx - 2.0 * xm, gy = (i12 - 2.0) * y, gz = i12 * z;
                 const double p1 = t, p2 = t - ex;
                 const double k1 = 3.0 * i1 * ir1s, k2 = 3.0 * i2 * ir2s;
-                const double r = c / s;
+                const double r = c * rcp_fast(s);
                 const double ecx = -r * cth, ecy = r * sth;
                 const double F1 = phi - R.pl1, F2 = gx * ex + gy * ey + gz * c;
                 const double gec = gx * ecx + gy * ecy + gz;
@@ -613,8 +616,9 @@ __device__ inline int findi_fast(const Roche& R, double dphi, double& inc_deg)
                 const double J22 = i12 - k1 * p1 * p1 - k2 * p2 * p2 - 2.0 * (ex * ex + ey * ey);
                 const double det = J11 * J22 - J12 * J21;
                 if (!(det != 0.0)) break;
-                double dc = -(F1 * J22 - F2 * J12) / det;
-                const double dt = -(J11 * F2 - J21 * F1) / det;
+                const double idet = rcp_fast(det);
+                double dc = -(F1 * J22 - F2 * J12) * idet;
+                const double dt = -(J11 * F2 - J21 * F1) * idet;
                 dc = fmin(fmax(dc, -0.05), 0.05);
                 c += dc;
                 t += dt;
@@ -653,7 +657,7 @@ __device__ __forceinline__ StreamState axpy(const StreamState& s, double a, cons
     return StreamState{fma(a, k.x, s.x), fma(a, k.y, s.y), fma(a, k.vx, s.vx), fma(a, k.vy, s.vy)};
 }
 
-__device__ inline void hermite(const StreamState& s0, const StreamState& s1, double dt,
+__device__ inline void hermite(const StreamState& s0, const StreamState& s1, double dt, double idt,
                                double tau, double out[4])
 {
     const double t2 = tau * tau, t3 = t2 * tau;
@@ -663,8 +667,8 @@ __device__ inline void hermite(const StreamState& s0, const StreamState& s1, dou
     const double d01 = -6.0 * t2 + 6.0 * tau, d11 = 3.0 * t2 - 2.0 * tau;
     out[0] = h00 * s0.x + h10 * dt * s0.vx + h01 * s1.x + h11 * dt * s1.vx;
     out[1] = h00 * s0.y + h10 * dt * s0.vy + h01 * s1.y + h11 * dt * s1.vy;
-    out[2] = (d00 * s0.x + d01 * s1.x) / dt + d10 * s0.vx + d11 * s1.vx;
-    out[3] = (d00 * s0.y + d01 * s1.y) / dt + d10 * s0.vy + d11 * s1.vy;
+    out[2] = fma(d00 * s0.x + d01 * s1.x, idt, d10 * s0.vx + d11 * s1.vx);
+    out[3] = fma(d00 * s0.y + d01 * s1.y, idt, d10 * s0.vy + d11 * s1.vy);
 }
 
 // second-order point of the L1 unstable manifold (MODEL_SPEC 4.5)
@@ -672,12 +676,12 @@ __device__ inline StreamState stream_start(const Roche& R)
 {
     const double x1 = R.xl1;
     const double m1 = 0.5 * R.cA, m2 = 0.5 * R.cB;
-    const double ix1 = 1.0 / x1, irs = 1.0 / R.Rs;
+    const double ix1 = rcp_fast(x1), irs = rcp_fast(R.Rs);
     const double K = m1 * ix1 * ix1 * ix1 + m2 * irs * irs * irs;
     const double Uxx = -2.0 * K - 1.0, Uyy = K - 1.0;
     const double L = 0.5 * ((K - 2.0) + sqrt((K - 2.0) * (K - 2.0) + 4.0 * (2.0 * K + 1.0) * (K - 1.0)));
     const double lam = sqrt(L);
-    const double B = -(L - 2.0 * K - 1.0) / (2.0 * lam);
+    const double B = -(L - 2.0 * K - 1.0) * (0.5 * rcp_fast(lam));
     const double inrm = rsqrt(1.0 + B * B);
     const double v0 = -inrm, v1 = B * inrm;
     const double Uxxx = 6.0 * m1 * ix1 * ix1 * ix1 * ix1 - 6.0 * m2 * irs * irs * irs * irs;
@@ -685,7 +689,7 @@ __device__ inline StreamState stream_start(const Roche& R)
     const double N2x = -0.5 * (Uxxx * v0 * v0 + Uxyy * v1 * v1);
     const double N2y = -Uxyy * v0 * v1;
     const double a11 = Uxx + 4.0 * L, a22 = Uyy + 4.0 * L;
-    const double idet = 1.0 / (a11 * a22 + 16.0 * L);
+    const double idet = rcp_fast(a11 * a22 + 16.0 * L);
     const double w0 = (N2x * a22 + 4.0 * lam * N2y) * idet;
     const double w1 = (a11 * N2y - 4.0 * lam * N2x) * idet;
     const double d = STREAM_DELTA, d2 = d * d;
@@ -703,13 +707,15 @@ __device__ inline int bspot(const Roche& R, double rad, double out[4])
     double r2c = s.x * s.x + s.y * s.y;
     const double rad2 = rad * rad;
     for (int n = 0; n < STREAM_MAXSTEP; ++n) {
-        const double r = sqrt(r2c);
-        const double dt = fmin(STREAM_KAPPA * r * sqrt(r), STREAM_DTMAX);
+        // r^(3/2) = r2 (r2 (r2)^(-1/2))^(-1/2): two v_rsq steps, where two
+        // IEEE square roots in series made dt (not k1) the step's critical path
+        const double r32 = r2c * rsqrt_pos(r2c * rsqrt_pos(r2c));
+        const double dt = fmin(STREAM_KAPPA * r32, STREAM_DTMAX);
         const StreamState k1 = stream_deriv(R, s);
         const StreamState k2 = stream_deriv(R, axpy(s, 0.5 * dt, k1));
         const StreamState k3 = stream_deriv(R, axpy(s, 0.5 * dt, k2));
         const StreamState k4 = stream_deriv(R, axpy(s, dt, k3));
-        const double h6 = dt / 6.0;
+        const double h6 = dt * (1.0 / 6.0);
         StreamState sn{s.x + h6 * (k1.x + 2.0 * k2.x + 2.0 * k3.x + k4.x),
                        s.y + h6 * (k1.y + 2.0 * k2.y + 2.0 * k3.y + k4.y),
                        s.vx + h6 * (k1.vx + 2.0 * k2.vx + 2.0 * k3.vx + k4.vx),
@@ -718,18 +724,20 @@ __device__ inline int bspot(const Roche& R, double rad, double out[4])
         if (rn2 < rad2) {  // Hermite crossing, safeguarded Newton on |H|^2 - rad^2
             const double r2 = rad2;
             const double f0 = r2c - r2, f1 = rn2 - r2;
-            double lo = 0.0, hi = 1.0, tau = f0 / (f0 - f1), p[4];
+            const double idt = rcp_fast(dt);
+            double lo = 0.0, hi = 1.0, tau = f0 * rcp_fast(f0 - f1), p[4];
             for (int it = 0; it < 100; ++it) {
-                hermite(s, sn, dt, tau, p);
+                hermite(s, sn, dt, idt, tau, p);
                 const double f = p[0] * p[0] + p[1] * p[1] - r2;
                 const double df = 2.0 * dt * (p[0] * p[2] + p[1] * p[3]);
                 if (f > 0.0) lo = tau; else hi = tau;
-                if (df != 0.0 && fabs(f / df) <= ROOT_LAST) { tau -= f / df; break; }  // last Newton step
-                double tn = (df != 0.0) ? tau - f / df : 0.5 * (lo + hi);
+                const double step = (df != 0.0) ? f * rcp_fast(df) : 0.0;
+                if (df != 0.0 && fabs(step) <= ROOT_LAST) { tau -= step; break; }  // last Newton step
+                double tn = (df != 0.0) ? tau - step : 0.5 * (lo + hi);
                 if (!(tn > lo && tn < hi)) tn = 0.5 * (lo + hi);
                 tau = tn;
             }
-            hermite(s, sn, dt, tau, out);
+            hermite(s, sn, dt, idt, tau, out);
             return ST_OK;
         }
         if (rn2 > r2c && n > 0) return ST_BAD_STREAM;
@@ -749,7 +757,7 @@ __device__ inline double bs_umax(double a, double b, double lnpk)
     for (int it = 0; it < 200 && v - k * log(v) - C <= 0.0; ++it) v *= 2.0;
     for (int it = 0; it < ROOT_MAXIT; ++it) {
         const double G = v - k * log(v) - C;
-        const double dv = G / (1.0 - k / v);
+        const double dv = G * v * rcp_fast(v - k);  // G / (1 - k / v)
         v -= dv;
         if (fabs(dv) <= ROOT_LAST * v) break;  // quadratic: the error left is ~1e-18 v
     }
