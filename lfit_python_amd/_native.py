@@ -18,6 +18,7 @@ LOAD_PATH = os.environ.get("LFG_LIB", LIB_PATH)
 SOURCES = [os.path.join(_HERE, "csrc", "lfg.hip"), os.path.join(_HERE, "csrc", "lfg_components.hip")]
 HEADERS = [os.path.join(_HERE, "csrc", "lfg_device.hpp"),
            os.path.join(_HERE, "csrc", "lfg_tables.hpp"),
+           os.path.join(_HERE, "csrc", "lfg_stream_table.h"),
            os.path.join(REPO, "include", "lfg.h")]
 INCLUDE = os.path.join(REPO, "include")
 ARCH = "gfx950"

@@ -153,28 +153,47 @@ __device__ __forceinline__ double gather_par(const SetupArgs& A, const Prop& P, 
     return P.cj ? fma(P.s[g] - P.cj[g], P.z, P.cj[g]) : P.s[g];
 }
 
+// Diagnostic build only (-DLFG_PROFILE_SETUP): s_memtime cycle counts of each
+// lane type into spare geo slots 41..47 (GP slots: non-GP trees only; the
+// prior lane writes into the pair of its walker, E = 1 only).
+#ifdef LFG_PROFILE_SETUP
+// 100 MHz start / end stamps of every lane: [lane type][start, end][lane]
+__device__ unsigned long long g_setup_dbg[3][2][4096];
+#define LFG_RT(kind, se, i) if ((i) < 4096) g_setup_dbg[kind][se][i] = __builtin_amdgcn_s_memrealtime()
+#define LFG_T0(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define LFG_DT(slot, v) G[slot] = double(__builtin_amdgcn_s_memtime() - (v))
+#else
+#define LFG_T0(v)
+#define LFG_DT(slot, v)
+#define LFG_RT(kind, se, i)
+#endif
+
 // ------------------------------------------------------- stream lanes of k_setup
-// One lane per (walker, eclipse): the ballistic stream to the disc edge and
-// the spot-dependent Roche prior (CVModel.py:215-316).  Needs only q, rdisc
-// and az, so these lanes run beside the setup lanes of the same launch; the
-// stream status goes to bstatus and is folded into the pair status by
-// k_elements.
+// One lane per (walker, eclipse): the ballistic stream to the disc edge
+// (MODEL_SPEC 4.5, the stream table), the spot-dependent Roche prior
+// (CVModel.py:215-316) and the strip shape (MODEL_SPEC 5.3: peak, tail end).
+// Needs only q, rdisc, az, exp1 and exp2, so these lanes run beside the setup
+// lanes of the same launch; the stream status goes to bstatus and is folded
+// into the pair status by k_elements.
 __device__ inline void bspot_lane(const SetupArgs& A, int t)
 {
+    LFG_T0(tl);
     const int* gat = A.gather ? A.gather : kIdentityGather;
     const int w = t / A.E, e = t - w * A.E;
     const Prop P = make_prop(A, w);
+    const int np = A.npars ? A.npars[e] : A.P;
     const double q = gather_par(A, P, gat[e * 18 + 4]);
     const double rdisc = gather_par(A, P, gat[e * 18 + 6]);
     const double az = gather_par(A, P, gat[e * 18 + 10]);
+    const double a1 = (np == 18) ? gather_par(A, P, gat[e * 18 + 14]) : 2.0;  // MODEL_SPEC 5.3 simple: 2, 1
+    const double a2 = (np == 18) ? gather_par(A, P, gat[e * 18 + 15]) : 1.0;
     double* G = A.geo + size_t(t) * LFG_NGEO;
-#ifdef LFG_PROFILE_SETUP
-    const unsigned long long tp0 = __builtin_amdgcn_s_memtime();
-#endif
+    LFG_T0(tb);
     Roche R;
     int st = (isfinite(q) && isfinite(rdisc) && isfinite(az)) ? roche_init(R, q) : ST_BAD_ARGS;
     double bs[4] = {0.0, 0.0, 0.0, 0.0};
-    if (st == ST_OK) st = bspot(R, rdisc * R.xl1, bs);
+    if (st == ST_OK) st = bspot<false>(R, rdisc * R.xl1, bs);
+    LFG_DT(46, tb);
     double rprior = 0.0;
     if (st != ST_OK) {
         rprior = -INFINITY;
@@ -185,11 +204,56 @@ __device__ inline void bspot_lane(const SetupArgs& A, int t)
         const double minaz = fmax(0.0, tangent - AZ_SLOPE), maxaz = fmin(178.0, tangent + AZ_SLOPE);
         if (az < minaz || az > maxaz) rprior = -INFINITY;
     }
-    G[G_BSX] = bs[0]; G[G_BSY] = bs[1]; G[G_BSVX] = bs[2]; G[G_BSVY] = bs[3];
+    G[G_BSX] = bs[0]; G[G_BSY] = bs[1];
     G[G_RPRIOR_BS] = A.roche_priors ? rprior : 0.0;
+    if (a1 > 0.0 && a2 > 0.0 && isfinite(a1) && isfinite(a2)) {  // else the setup lane fails the pair
+        const double upk = pow(a1 / a2, 1.0 / a2);
+        const double lnpk = a1 * log(upk) - pow(upk, a2);
+        G[G_UPK] = upk; G[G_UMAX] = bs_umax(a1, a2, lnpk); G[G_LNPK] = lnpk;
+        G[G_EXP1] = a1; G[G_EXP2] = a2;
+    }
     A.bstatus[t] = st;
+    LFG_DT(43, tl);
+}
+
+// per-walker lane: LCModel.ln_prior dphi check (CVModel.py:452-473) and
+// Node.ln_prior over the variable parameters (model.py:439-449); with the
+// fused stretch move it also stores the proposal
+__device__ inline void prior_lane(const SetupArgs& A, int w)
+{
+    LFG_T0(tl);
 #ifdef LFG_PROFILE_SETUP
-    G[43] = double(__builtin_amdgcn_s_memtime() - tp0);
+    const unsigned long long trl = __builtin_amdgcn_s_memrealtime();  // 100 MHz: calibrates s_memtime
+#endif
+    const int* gat = A.gather ? A.gather : kIdentityGather;
+    const Prop P = make_prop(A, w);
+    if (A.pos) {  // store the proposal: k_lnlike copies an accepted one into pos
+        double* qo = A.qout + size_t(w) * A.ndim;
+        for (int d = 0; d < A.ndim; ++d) qo[d] = gather_par(A, P, d);
+        A.zfout[w] = (A.ndim - 1.0) * log(P.z);
+    }
+    double lp = 0.0;
+    if (A.roche_priors) {
+        const double q = gather_par(A, P, gat[4]);
+        const double dphi = gather_par(A, P, gat[5]);
+        Roche R;
+        double maxphi;
+        if (roche_init(R, q) != ST_OK || findphi_fast(R, 90.0, maxphi) != ST_OK) lp = -INFINITY;
+        else if (dphi > maxphi - DPHI_TOL) lp = -INFINITY;
+    }
+    if (A.prior_type) {
+        for (int d = 0; d < A.ndim && isfinite(lp); ++d)
+            lp += prior_lnprob(A.prior_type[d], A.prior_p1[d], A.prior_p2[d], A.prior_norm[d],
+                               gather_par(A, P, d));
+    }
+    A.prior[w] = A.fixed_invalid ? -INFINITY : lp;
+    if (A.done) A.done[w] = 0;
+#ifdef LFG_PROFILE_SETUP
+    if (A.E == 1) {
+        double* G = A.geo + size_t(w) * LFG_NGEO;
+        LFG_DT(45, tl);
+        G[41] = double(__builtin_amdgcn_s_memrealtime() - trl);
+    }
 #endif
 }
 
@@ -198,45 +262,35 @@ __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
     const int t = blockIdx.x * SETUP_BLOCK + threadIdx.x;
     const int npairs = A.W * A.E;
     if (t >= 2 * npairs + A.W) return;
-    const int* gat = A.gather ? A.gather : kIdentityGather;
-
+#if defined(LFG_EXP_SETUP_EMPTY)  // experiment build: the launch alone (every pair fails)
+    if (t < npairs) { A.status[t] = ST_BAD_ARGS; A.bstatus[t] = ST_BAD_ARGS; }
+    if (t >= npairs && t < npairs + A.W) A.prior[t - npairs] = -INFINITY;
+    return;
+#endif
+#if defined(LFG_EXP_SETUP_NOPRIOR)  // experiment build: no prior lanes
+    if (t >= npairs && t < npairs + A.W) { A.prior[t - npairs] = 0.0; return; }
+#endif
+#if defined(LFG_EXP_SETUP_NOSTREAM)  // experiment build: no stream work
+    if (t >= npairs + A.W) { A.bstatus[t - npairs - A.W] = ST_BAD_STREAM; return; }
+#endif
     if (t >= npairs + A.W) {  // stream lanes (own waves: npairs + W is a multiple of 64 in the bench)
+        LFG_RT(1, 0, t - npairs - A.W);
         bspot_lane(A, t - npairs - A.W);
+        LFG_RT(1, 1, t - npairs - A.W);
         return;
     }
     if (t >= npairs) {
-        // per-walker lane: LCModel.ln_prior dphi check (CVModel.py:452-473)
-        // and Node.ln_prior over the variable parameters (model.py:439-449)
-        const int w = t - npairs;
-        const Prop P = make_prop(A, w);
-        if (A.pos) {  // store the proposal: k_lnlike copies an accepted one into pos
-            double* qo = A.qout + size_t(w) * A.ndim;
-            for (int d = 0; d < A.ndim; ++d) qo[d] = gather_par(A, P, d);
-            A.zfout[w] = (A.ndim - 1.0) * log(P.z);
-        }
-        double lp = 0.0;
-        if (A.roche_priors) {
-            const double q = gather_par(A, P, gat[4]);
-            const double dphi = gather_par(A, P, gat[5]);
-            Roche R;
-            double maxphi;
-            if (roche_init(R, q) != ST_OK || findphi_fast(R, 90.0, maxphi) != ST_OK) lp = -INFINITY;
-            else if (dphi > maxphi - DPHI_TOL) lp = -INFINITY;
-        }
-        if (A.prior_type) {
-            for (int d = 0; d < A.ndim && isfinite(lp); ++d)
-                lp += prior_lnprob(A.prior_type[d], A.prior_p1[d], A.prior_p2[d], A.prior_norm[d],
-                                   gather_par(A, P, d));
-        }
-        A.prior[w] = A.fixed_invalid ? -INFINITY : lp;
-        if (A.done) A.done[w] = 0;
+        LFG_RT(2, 0, t - npairs);
+        prior_lane(A, t - npairs);
+        LFG_RT(2, 1, t - npairs);
         return;
     }
+    LFG_RT(0, 0, t);
 
+    // setup lane: one per (walker, eclipse)
+    LFG_T0(tl);
+    const int* gat = A.gather ? A.gather : kIdentityGather;
     const int w = t / A.E, e = t - (t / A.E) * A.E;
-#ifdef LFG_PROFILE_SETUP
-    const unsigned long long tlane = __builtin_amdgcn_s_memtime();
-#endif
     const Prop P = make_prop(A, w);
     const int np = A.npars ? A.npars[e] : A.P;
     double p[18];
@@ -252,15 +306,7 @@ __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
     Roche R;
     if (!finite) st = ST_BAD_ARGS;
     else st = roche_init(R, p[4]);
-
-#ifdef LFG_PROFILE_SETUP
-    // diagnostic build only: phase cycle counts into spare geo slots
-    unsigned long long tp0 = __builtin_amdgcn_s_memtime(), tp1 = tp0, tp2 = tp0, tp3 = tp0;
-#define LFG_STAMP(v) (v) = __builtin_amdgcn_s_memtime()
-#else
-#define LFG_STAMP(v)
-#endif
-    LFG_STAMP(tp1);
+    LFG_DT(42, tl);
     if (st == ST_OK) {
         // SimpleEclipse.ln_prior Roche checks not involving the stream (CVModel.py:215-316)
         if (p[6] * R.xl1 > DISC_MAX_A) rprior = -INFINITY;
@@ -269,24 +315,10 @@ __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
     } else {
         rprior = -INFINITY;
     }
-    LFG_STAMP(tp2);
+    LFG_T0(tf);
     double inc = 0.0;
     if (st == ST_OK) st = findi_fast(R, p[5], inc);
-    LFG_STAMP(tp3);
-#ifdef LFG_PROFILE_SETUP
-    {
-        double mp;
-        const unsigned long long ta = __builtin_amdgcn_s_memtime();
-        findphi_fast(R, 90.0, mp);
-        const unsigned long long tb = __builtin_amdgcn_s_memtime();
-        const double um = bs_umax(p[14], p[15], p[14] * log(pow(p[14] / p[15], 1.0 / p[15])) - p[14] / p[15]);
-        const unsigned long long tc2 = __builtin_amdgcn_s_memtime();
-        G[42] = double(tp0 - tlane);
-        G[44] = double(tp3 - tp2);
-        G[45] = double(tb - ta);
-        G[46] = double(tc2 - tb) + 0.0 * um;
-    }
-#endif
+    LFG_DT(44, tf);
     const double rwd_a = p[8] * R.xl1, rdisc_a = p[6] * R.xl1;
     if (st == ST_OK && (!(rwd_a > 0.0) || !(rdisc_a > rwd_a) || !(rdisc_a < R.xl1))) st = ST_BAD_GEOMETRY;
     if (st == ST_OK && (!(p[9] > 0.0) || !(p[14] > 0.0) || !(p[15] > 0.0))) st = ST_BAD_GEOMETRY;
@@ -297,9 +329,6 @@ __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
 
     double s, c;
     sincos(inc * DEG, &s, &c);
-    const double a1 = p[14], a2 = p[15];
-    const double upk = pow(a1 / a2, 1.0 / a2);
-    const double lnpk = a1 * log(upk) - pow(upk, a2);
     const double tilt = p[16] * DEG, psi = (p[10] - 90.0 + p[17]) * DEG;
     double st_, ct_, sp_, cp_;
     sincos(tilt, &st_, &ct_);
@@ -313,8 +342,7 @@ __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
     G[G_S] = s; G[G_C] = c; G[G_INC] = inc;
     G[G_RWD] = rwd_a; G[G_RDISC] = rdisc_a; G[G_REFF] = eggleton(R.q);
     G[G_ULIMB] = p[7]; G[G_DEXP] = p[12];
-    G[G_L] = p[9] * R.xl1; G[G_UPK] = upk; G[G_UMAX] = bs_umax(a1, a2, lnpk); G[G_LNPK] = lnpk;
-    G[G_EXP1] = a1; G[G_EXP2] = a2; G[G_CAZ] = caz; G[G_SAZ] = saz;
+    G[G_L] = p[9] * R.xl1; G[G_CAZ] = caz; G[G_SAZ] = saz;
     G[G_NB0] = st_ * cp_; G[G_NB1] = st_ * sp_; G[G_NB2] = ct_;
     G[G_BDEN] = p[11] + (1.0 - p[11]) * fmax(nmax, 0.0);
     G[G_FIS] = p[11]; G[G_PHI0] = p[13];
@@ -343,9 +371,8 @@ __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
         G[G_GP_DCP] = dcp;
         G[G_GP_OK] = (ok && tau > 0.0 && isfinite(ain) && isfinite(aout)) ? 1.0 : 0.0;
     }
-#ifdef LFG_PROFILE_SETUP
-    G[47] = double(__builtin_amdgcn_s_memtime() - tlane);
-#endif
+    LFG_DT(47, tl);
+    LFG_RT(0, 1, t);
 }
 
 // ------------------------------------------------------------- k_elements
@@ -2236,6 +2263,14 @@ int lfg_gp_lnlike(const double* x, const double* ye, const double* res, int W, i
                        lnlike);
     return launch_ok();
 }
+
+#ifdef LFG_PROFILE_SETUP
+// diagnostic build only: copy the k_setup lane stamps to the host
+int lfg_debug_setup_stamps(unsigned long long* host)
+{
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_setup_dbg), sizeof(g_setup_dbg)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 const char* lfg_version(void) { return kFused ? "lfg 0.2.0 gfx950 fp64 fused-elements" : "lfg 0.2.0 gfx950 fp64"; }
 

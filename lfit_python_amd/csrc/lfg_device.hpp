@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include "lfg_stream_table.h"
+
 namespace lfg {
 
 constexpr double PI = 3.14159265358979323846;
@@ -28,9 +30,11 @@ constexpr double ROOT_LAST = 1e-9;
 constexpr int MIN_MAXIT = 100;
 constexpr double BS_TAIL = 16.0;
 constexpr double STREAM_DELTA = 1e-2;
-constexpr double STREAM_KAPPA = 0.15;
-constexpr double STREAM_DTMAX = 0.15;
-constexpr int STREAM_MAXSTEP = 4000;
+// outside the stream table: RK4 with dt = min(0.15, 0.15 r^1.5) / 32
+// (converged to ~1e-12 a)
+constexpr double STREAM_KAPPA_FINE = 0.15 / 32.0;
+constexpr double STREAM_DTMAX_FINE = 0.15 / 32.0;
+constexpr int STREAM_MAXSTEP_FINE = 128000;
 constexpr double DISC_MAX_A = 0.46;  // CVModel.py:217
 constexpr double AZ_SLOPE = 80.0;    // CVModel.py:282
 constexpr double DPHI_TOL = 1e-6;    // CVModel.py:452
@@ -697,20 +701,22 @@ __device__ inline StreamState stream_start(const Roche& R)
                        d * lam * v1 + d2 * 2.0 * lam * w1};
 }
 
-__device__ inline int bspot(const Roche& R, double rad, double out[4])
+// The converged stream outside the table's domain (MODEL_SPEC 4.5): RK4 with
+// step dt = min(STREAM_DTMAX_FINE, STREAM_KAPPA_FINE r^(3/2)) (~1e-12 a from
+// the DOP853 reference) and the crossing on the cubic Hermite interpolant of
+// the last step.  Slow (~700 steps); the prior ranges never reach it.
+__device__ inline int bspot_rk4(const Roche& R, double rad, double out[4])
 {
-    if (!(rad > 0.0) || !(rad < R.xl1)) return ST_BAD_STREAM;
     // the loop tests squared radii: the exit branch waits on one fma level,
     // not on a sqrt (~5 dependent levels); r itself only sets the next dt,
     // which runs beside k1
     StreamState s = stream_start(R);
     double r2c = s.x * s.x + s.y * s.y;
     const double rad2 = rad * rad;
-    for (int n = 0; n < STREAM_MAXSTEP; ++n) {
-        // r^(3/2) = r2 (r2 (r2)^(-1/2))^(-1/2): two v_rsq steps, where two
-        // IEEE square roots in series made dt (not k1) the step's critical path
+    for (int n = 0; n < STREAM_MAXSTEP_FINE; ++n) {
+        // r^(3/2) = r2 (r2 (r2)^(-1/2))^(-1/2): two v_rsq steps
         const double r32 = r2c * rsqrt_pos(r2c * rsqrt_pos(r2c));
-        const double dt = fmin(STREAM_KAPPA * r32, STREAM_DTMAX);
+        const double dt = fmin(STREAM_KAPPA_FINE * r32, STREAM_DTMAX_FINE);
         const StreamState k1 = stream_deriv(R, s);
         const StreamState k2 = stream_deriv(R, axpy(s, 0.5 * dt, k1));
         const StreamState k3 = stream_deriv(R, axpy(s, 0.5 * dt, k2));
@@ -745,6 +751,77 @@ __device__ inline int bspot(const Roche& R, double rad, double out[4])
         r2c = rn2;
     }
     return ST_BAD_STREAM;
+}
+
+// The converged stream as piecewise tensor Chebyshev series (MODEL_SPEC 4.5,
+// lfg_stream_table.h from tools/gen_stream_table.py): patch (iq, js) of
+// xi = ln q and s = sqrt((r - rmin) / (r0 - rmin)) holds phi, vx, vy.
+__constant__ const double kStRmin[LFG_ST_NQ * (LFG_ST_DR + 1)] = LFG_ST_RMIN;
+__constant__ const double kStCoef[LFG_ST_NQ * LFG_ST_NS * 3 * (LFG_ST_DQ + 1) * (LFG_ST_DS + 1)] = LFG_ST_COEF;
+constexpr double kStSb[LFG_ST_NS + 1] = LFG_ST_SB;
+constexpr int ST_PATCH = (LFG_ST_DQ + 1) * (LFG_ST_DS + 1);
+
+// Clenshaw sum of c[0..n-1] T_k(x)
+template <int N>
+__device__ __forceinline__ double clenshaw(const double* c, double x)
+{
+    const double x2 = x + x;
+    double b1 = 0.0, b2 = 0.0;
+#pragma unroll
+    for (int k = N - 1; k >= 1; --k) {
+        const double t = fma(x2, b1, c[k] - b2);
+        b2 = b1;
+        b1 = t;
+    }
+    return fma(x, b1, c[0] - b2);
+}
+
+// one output of a patch: sum_i T_i(xq) sum_j c[i][j] T_j(xs); the DQ + 1 inner
+// sums are independent chains (13 levels), then one 10-level chain
+__device__ __forceinline__ double st_patch(const double* c, double xq, double xs)
+{
+    double a[LFG_ST_DQ + 1];
+#pragma unroll
+    for (int i = 0; i <= LFG_ST_DQ; ++i) a[i] = clenshaw<LFG_ST_DS + 1>(c + i * (LFG_ST_DS + 1), xs);
+    return clenshaw<LFG_ST_DQ + 1>(a, xq);
+}
+
+// MODEL_SPEC 4.5: bspot(q, rad) -> (x, y, vx, vy) of the converged stream
+// (trm.roche.bspot).  VEL = false leaves out[2..3] unset: the hot path
+// needs the impact point only.
+template <bool VEL = true>
+__device__ inline int bspot(const Roche& R, double rad, double out[4])
+{
+    if (!(rad > 0.0) || !(rad < R.xl1)) return ST_BAD_STREAM;
+    if (!(R.q >= LFG_ST_QLO && R.q <= LFG_ST_QHI))
+        return bspot_rk4(R, rad, out);
+    const double fq = (log(R.q) - LFG_ST_LQLO) * (1.0 / LFG_ST_LQW);
+    const int iq = min(max(int(fq), 0), LFG_ST_NQ - 1);
+    const double xq = 2.0 * (fq - iq) - 1.0;
+    const StreamState s0 = stream_start(R);
+    const double r0 = sqrt(s0.x * s0.x + s0.y * s0.y);
+    const double rmin = exp(clenshaw<LFG_ST_DR + 1>(kStRmin + iq * (LFG_ST_DR + 1), xq));
+    if (!(rad > rmin) || !(rad < r0)) return ST_BAD_STREAM;  // misses the disc / starts inside rad
+    const double s = sqrt((rad - rmin) / (r0 - rmin));
+    if (!(s <= LFG_ST_STOP)) return bspot_rk4(R, rad, out);
+    int js = 0;
+#pragma unroll
+    for (int k = 1; k < LFG_ST_NS; ++k) js += (s >= kStSb[k]) ? 1 : 0;
+    double lo = kStSb[0], w = kStSb[1] - kStSb[0];
+#pragma unroll
+    for (int k = 1; k < LFG_ST_NS; ++k)
+        if (js == k) { lo = kStSb[k]; w = kStSb[k + 1] - kStSb[k]; }
+    const double xs = 2.0 * (s - lo) / w - 1.0;
+    const double* c = kStCoef + size_t(iq * LFG_ST_NS + js) * 3 * ST_PATCH;
+    double sp, cp;
+    sincos(st_patch(c, xq, xs), &sp, &cp);
+    out[0] = rad * cp;
+    out[1] = rad * sp;
+    if (VEL) {
+        out[2] = st_patch(c + ST_PATCH, xq, xs);
+        out[3] = st_patch(c + 2 * ST_PATCH, xq, xs);
+    }
+    return ST_OK;
 }
 
 // MODEL_SPEC 5.3: end of the bright-spot strip, F(u) = BS_TAIL below the peak

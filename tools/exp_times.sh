@@ -1,11 +1,11 @@
 #!/bin/bash
 # rocprofv3 kernel stats of tools/kernel_time.py for the main library and
-# each experiment build given on the command line (lfit_python_amd/_lib/liblfg_hip_<name>.so)
+# each experiment build given on the command line (build/exp/liblfg_<name>.so, tools/build_exp.sh)
 R=$GRAFT_REPO_ROOT
 cd /tmp && export TMPDIR=/tmp
 rm -f $R/gpurun_out/kernel_time_walkers.npy
 for v in main "$@"; do
-  if [ "$v" = main ]; then lib=$R/lfit_python_amd/_lib/liblfg_hip.so; else lib=$R/lfit_python_amd/_lib/liblfg_hip_$v.so; fi
+  if [ "$v" = main ]; then lib=$R/lfit_python_amd/_lib/liblfg_hip.so; else lib=$R/build/exp/liblfg_$v.so; fi
   LFG_LIB=$lib timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/exp_$v -o run --output-format csv \
     -- python3 $R/tools/kernel_time.py 30 > $R/gpurun_out/exp_$v.log 2>&1 || { echo "$v failed"; exit 3; }
   echo "== $v"
