@@ -93,6 +93,14 @@ struct lfg_tree {
      * Node.ln_prior is -inf for every walker (model.py:439-441 checks every
      * parameter, variable or not); ln_prob = -inf on every path */
     int fixed_invalid;
+    /* [dev] ndim x 2, nullable: per-parameter constants of Prior.ln_prob so
+     * the prior lanes need no transcendental per parameter:
+     *   gauss, gaussPos   c0 = -ln(sqrt(2 pi) p2),  c1 = 1 / p2
+     *   uniform           c0 = ln(1 / |p1 - p2|)
+     *   log_uniform, mod_jeff  c0 = -ln(normalise)
+     * (lfit_python_amd.batch.prior_consts).  NULL: each term from
+     * prior_p1/p2/norm directly. */
+    const double* prior_c;
 };
 
 /* scratch bytes needed for W parameter sets x E eclipses (chi^2 trees and

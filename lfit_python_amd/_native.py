@@ -54,6 +54,7 @@ class LfgTree(ctypes.Structure):
         ("gp_gather", ctypes.c_void_p), ("gp_base", ctypes.c_void_p),
         ("gp_ecl", ctypes.c_void_p),
         ("fixed_invalid", ctypes.c_int),
+        ("prior_c", ctypes.c_void_p),
     ]
 
 

@@ -124,6 +124,23 @@ def compile_tree(model, nsub=1):
         gp=gp, gp_gather=gp_gather, gp_base=gp_base, gp_ecl=gp_ecl, order=orders)
 
 
+def prior_consts(tree):
+    """[ndim, 2] constants of Prior.ln_prob (model.py:83-113; include/lfg.h
+    lfg_tree.prior_c), so the device's prior lanes take one log per chunk of
+    parameters instead of one per parameter."""
+    t, p1, p2, nm = tree.prior_type, tree.prior_p1, tree.prior_p2, tree.prior_norm
+    c = np.zeros((len(t), 2), np.float64)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        gs = t <= 1
+        c[gs, 0] = -np.log(np.sqrt(2.0 * np.pi) * p2[gs])
+        c[gs, 1] = 1.0 / p2[gs]
+        un = t == 2
+        c[un, 0] = np.log(1.0 / np.abs(p1[un] - p2[un]))
+        lg = t >= 3
+        c[lg, 0] = -np.log(nm[lg])
+    return c
+
+
 class LnProbEvaluator:
     """Device-resident ln_prob for a compiled tree (one per GPU / stream)."""
 
@@ -141,7 +158,8 @@ class LnProbEvaluator:
             off=t(tree.offsets, i32), x=t(tree.x, f64), y=t(tree.y, f64),
             ye=t(tree.ye, f64), w=t(tree.w, f64),
             prior_type=t(tree.prior_type, i32), prior_p1=t(tree.prior_p1, f64),
-            prior_p2=t(tree.prior_p2, f64), prior_norm=t(tree.prior_norm, f64))
+            prior_p2=t(tree.prior_p2, f64), prior_norm=t(tree.prior_norm, f64),
+            prior_c=t(prior_consts(tree).reshape(-1), f64))
         if tree.gp:
             self._buf.update(gp_gather=t(tree.gp_gather.reshape(-1), i32),
                              gp_base=t(self._gp_base(tree), f64),
@@ -152,7 +170,7 @@ class LnProbEvaluator:
             tree.E, tree.ndim, tree.nsub, tree.max_n, p('gather'), p('npars'), p('consts'),
             p('off'), p('x'), p('y'), p('ye'), p('w'), p('prior_type'), p('prior_p1'),
             p('prior_p2'), p('prior_norm'), int(tree.roche_priors), int(tree.gp),
-            p('gp_gather'), p('gp_base'), p('gp_ecl'), int(tree.fixed_invalid))
+            p('gp_gather'), p('gp_base'), p('gp_ecl'), int(tree.fixed_invalid), p('prior_c'))
         self._ws = None
         self._ws_walkers = 0
         # bumped whenever the workspace is reallocated: a captured HIP graph

@@ -125,6 +125,7 @@ struct SetupArgs {
     // lo = 0 on one process; a rank's shard with lfg_stretch_step_shard)
     int lo, ns;
     int fixed_invalid;  // lfg_tree.fixed_invalid: every prior lane gives -inf
+    const double* prior_c;  // lfg_tree.prior_c (nullable): [ndim][2] Prior.ln_prob constants
 };
 
 // where a lane reads walker w's parameters: the walker row, or the
@@ -153,19 +154,20 @@ __device__ __forceinline__ double gather_par(const SetupArgs& A, const Prop& P, 
     return P.cj ? fma(P.s[g] - P.cj[g], P.z, P.cj[g]) : P.s[g];
 }
 
-// Diagnostic build only (-DLFG_PROFILE_SETUP): s_memtime cycle counts of each
-// lane type into spare geo slots 41..47 (GP slots: non-GP trees only; the
-// prior lane writes into the pair of its walker, E = 1 only).
+// Diagnostic build only (-DLFG_PROFILE_SETUP): s_memtime cycle counts of the
+// phases of each lane into g_setup_cyc[slot][lane] (lfg_debug_setup_cycles):
+//  0-3 setup lane: gather, roche_init, findi, total; 4-7 stream lane: gather,
+//  roche_init, bspot, total; 8 prior lane total, 9 the same in 100 MHz
+//  s_memrealtime ticks (calibrates the shader clock), 10 its roche_init + findphi
 #ifdef LFG_PROFILE_SETUP
-// 100 MHz start / end stamps of every lane: [lane type][start, end][lane]
-__device__ unsigned long long g_setup_dbg[3][2][4096];
-#define LFG_RT(kind, se, i) if ((i) < 4096) g_setup_dbg[kind][se][i] = __builtin_amdgcn_s_memrealtime()
-#define LFG_T0(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
-#define LFG_DT(slot, v) G[slot] = double(__builtin_amdgcn_s_memtime() - (v))
+__device__ unsigned long long g_setup_cyc[11][4096];
+#define LFG_T0(v) unsigned long long v = __builtin_amdgcn_s_memtime()
+#define LFG_CY(slot, i, v) \
+    do { const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+         if ((i) < 4096) g_setup_cyc[slot][i] = now_ - (v); (v) = now_; } while (0)
 #else
 #define LFG_T0(v)
-#define LFG_DT(slot, v)
-#define LFG_RT(kind, se, i)
+#define LFG_CY(slot, i, v)
 #endif
 
 // ------------------------------------------------------- stream lanes of k_setup
@@ -188,12 +190,16 @@ __device__ inline void bspot_lane(const SetupArgs& A, int t)
     const double a1 = (np == 18) ? gather_par(A, P, gat[e * 18 + 14]) : 2.0;  // MODEL_SPEC 5.3 simple: 2, 1
     const double a2 = (np == 18) ? gather_par(A, P, gat[e * 18 + 15]) : 1.0;
     double* G = A.geo + size_t(t) * LFG_NGEO;
-    LFG_T0(tb);
+#ifdef LFG_PROFILE_SETUP
+    unsigned long long tb = tl;
+    LFG_CY(4, t, tb);
+#endif
     Roche R;
     int st = (isfinite(q) && isfinite(rdisc) && isfinite(az)) ? roche_init(R, q) : ST_BAD_ARGS;
+    LFG_CY(5, t, tb);
     double bs[4] = {0.0, 0.0, 0.0, 0.0};
     if (st == ST_OK) st = bspot<false>(R, rdisc * R.xl1, bs);
-    LFG_DT(46, tb);
+    LFG_CY(6, t, tb);
     double rprior = 0.0;
     if (st != ST_OK) {
         rprior = -INFINITY;
@@ -213,7 +219,7 @@ __device__ inline void bspot_lane(const SetupArgs& A, int t)
         G[G_EXP1] = a1; G[G_EXP2] = a2;
     }
     A.bstatus[t] = st;
-    LFG_DT(43, tl);
+    LFG_CY(7, t, tl);
 }
 
 // per-walker lane: LCModel.ln_prior dphi check (CVModel.py:452-473) and
@@ -223,15 +229,10 @@ __device__ inline void prior_lane(const SetupArgs& A, int w)
 {
     LFG_T0(tl);
 #ifdef LFG_PROFILE_SETUP
-    const unsigned long long trl = __builtin_amdgcn_s_memrealtime();  // 100 MHz: calibrates s_memtime
+    unsigned long long trl = __builtin_amdgcn_s_memrealtime(), tr = tl;  // 100 MHz: calibrates s_memtime
 #endif
     const int* gat = A.gather ? A.gather : kIdentityGather;
     const Prop P = make_prop(A, w);
-    if (A.pos) {  // store the proposal: k_lnlike copies an accepted one into pos
-        double* qo = A.qout + size_t(w) * A.ndim;
-        for (int d = 0; d < A.ndim; ++d) qo[d] = gather_par(A, P, d);
-        A.zfout[w] = (A.ndim - 1.0) * log(P.z);
-    }
     double lp = 0.0;
     if (A.roche_priors) {
         const double q = gather_par(A, P, gat[4]);
@@ -240,20 +241,69 @@ __device__ inline void prior_lane(const SetupArgs& A, int w)
         double maxphi;
         if (roche_init(R, q) != ST_OK || findphi_fast(R, 90.0, maxphi) != ST_OK) lp = -INFINITY;
         else if (dphi > maxphi - DPHI_TOL) lp = -INFINITY;
+        LFG_CY(10, w, tr);
     }
-    if (A.prior_type) {
-        for (int d = 0; d < A.ndim && isfinite(lp); ++d)
-            lp += prior_lnprob(A.prior_type[d], A.prior_p1[d], A.prior_p2[d], A.prior_norm[d],
-                               gather_par(A, P, d));
+    // the walker's parameters in chunks of PCH: each chunk's loads are issued
+    // back to back (one memory latency per chunk, not per parameter), then
+    // the proposal is stored and the chunk's prior terms summed in order
+    constexpr int PCH = 16;
+    double* qo = A.pos ? A.qout + size_t(w) * A.ndim : nullptr;
+    for (int d0 = 0; d0 < A.ndim; d0 += PCH) {
+        double v[PCH];
+#pragma unroll
+        for (int k = 0; k < PCH; ++k) v[k] = (d0 + k < A.ndim) ? gather_par(A, P, d0 + k) : 0.0;
+        if (qo) {  // store the proposal: k_lnlike copies an accepted one into pos
+#pragma unroll
+            for (int k = 0; k < PCH; ++k)
+                if (d0 + k < A.ndim) qo[d0 + k] = v[k];
+        }
+        if (A.prior_type && A.prior_c) {
+            // Prior.ln_prob from the tree's constants (include/lfg.h): the
+            // terms c0 - z^2/2 (gauss) or c0, summed in order, and one log of
+            // the chunk's product of log_uniform / mod_jeff arguments
+            double prod = 1.0;
+            bool ok = true;
+#pragma unroll
+            for (int k = 0; k < PCH; ++k) {
+                const int d = d0 + k;
+                if (d < A.ndim) {
+                    const int ty = A.prior_type[d];
+                    const double p1 = A.prior_p1[d], p2 = A.prior_p2[d], c0 = A.prior_c[2 * d];
+                    const double z = (v[k] - p1) * A.prior_c[2 * d + 1];
+                    const double term = (ty <= 1) ? fma(-0.5 * z, z, c0) : c0;
+                    lp += term;
+                    prod *= (ty == 3) ? v[k] : (ty == 4 ? v[k] + p1 : 1.0);
+                    // scipy's pdf underflows to 0 (log -> -inf) below e^-745.13
+                    ok = ok && ((ty <= 1) ? (term > PDF_LN_MIN && (ty == 0 || v[k] > 0.0))
+                                          : (ty == 4 ? (v[k] > 0.0 && v[k] < p2)
+                                                     : (ty <= 3 && v[k] > p1 && v[k] < p2)));
+                }
+            }
+            if (ok && !(prod >= 1e-290 && prod <= 1e290)) {  // product out of range: one log each
+                prod = 0.0;
+                for (int k = 0; k < PCH && d0 + k < A.ndim; ++k) {
+                    const int ty = A.prior_type[d0 + k];
+                    if (ty >= 3) prod += log(ty == 3 ? v[k] : v[k] + A.prior_p1[d0 + k]);
+                }
+                lp -= prod;
+                prod = 1.0;
+            }
+            lp = ok ? lp - log(prod) : -INFINITY;
+        } else if (A.prior_type) {
+#pragma unroll
+            for (int k = 0; k < PCH; ++k) {
+                const int d = d0 + k;
+                if (d < A.ndim)
+                    lp += prior_lnprob(A.prior_type[d], A.prior_p1[d], A.prior_p2[d], A.prior_norm[d], v[k]);
+            }
+        }
     }
+    if (qo) A.zfout[w] = (A.ndim - 1.0) * log(P.z);
     A.prior[w] = A.fixed_invalid ? -INFINITY : lp;
     if (A.done) A.done[w] = 0;
+    LFG_CY(8, w, tl);
 #ifdef LFG_PROFILE_SETUP
-    if (A.E == 1) {
-        double* G = A.geo + size_t(w) * LFG_NGEO;
-        LFG_DT(45, tl);
-        G[41] = double(__builtin_amdgcn_s_memrealtime() - trl);
-    }
+    if (w < 4096) g_setup_cyc[9][w] = __builtin_amdgcn_s_memrealtime() - trl;
 #endif
 }
 
@@ -274,18 +324,13 @@ __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
     if (t >= npairs + A.W) { A.bstatus[t - npairs - A.W] = ST_BAD_STREAM; return; }
 #endif
     if (t >= npairs + A.W) {  // stream lanes (own waves: npairs + W is a multiple of 64 in the bench)
-        LFG_RT(1, 0, t - npairs - A.W);
         bspot_lane(A, t - npairs - A.W);
-        LFG_RT(1, 1, t - npairs - A.W);
         return;
     }
     if (t >= npairs) {
-        LFG_RT(2, 0, t - npairs);
         prior_lane(A, t - npairs);
-        LFG_RT(2, 1, t - npairs);
         return;
     }
-    LFG_RT(0, 0, t);
 
     // setup lane: one per (walker, eclipse)
     LFG_T0(tl);
@@ -301,12 +346,16 @@ __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
     }
     if (np == 14) { p[14] = 2.0; p[15] = 1.0; p[16] = 90.0; p[17] = 0.0; }  // MODEL_SPEC 5.3
     double* G = A.geo + size_t(t) * LFG_NGEO;
+#ifdef LFG_PROFILE_SETUP
+    unsigned long long tf = tl;
+    LFG_CY(0, t, tf);
+#endif
     int st = ST_OK;
     double rprior = 0.0;
     Roche R;
     if (!finite) st = ST_BAD_ARGS;
     else st = roche_init(R, p[4]);
-    LFG_DT(42, tl);
+    LFG_CY(1, t, tf);
     if (st == ST_OK) {
         // SimpleEclipse.ln_prior Roche checks not involving the stream (CVModel.py:215-316)
         if (p[6] * R.xl1 > DISC_MAX_A) rprior = -INFINITY;
@@ -315,10 +364,9 @@ __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
     } else {
         rprior = -INFINITY;
     }
-    LFG_T0(tf);
     double inc = 0.0;
     if (st == ST_OK) st = findi_fast(R, p[5], inc);
-    LFG_DT(44, tf);
+    LFG_CY(2, t, tf);
     const double rwd_a = p[8] * R.xl1, rdisc_a = p[6] * R.xl1;
     if (st == ST_OK && (!(rwd_a > 0.0) || !(rdisc_a > rwd_a) || !(rdisc_a < R.xl1))) st = ST_BAD_GEOMETRY;
     if (st == ST_OK && (!(p[9] > 0.0) || !(p[14] > 0.0) || !(p[15] > 0.0))) st = ST_BAD_GEOMETRY;
@@ -371,8 +419,7 @@ __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
         G[G_GP_DCP] = dcp;
         G[G_GP_OK] = (ok && tau > 0.0 && isfinite(ain) && isfinite(aout)) ? 1.0 : 0.0;
     }
-    LFG_DT(47, tl);
-    LFG_RT(0, 1, t);
+    LFG_CY(3, t, tl);
 }
 
 // ------------------------------------------------------------- k_elements
@@ -2027,6 +2074,7 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
                 T->prior_p2, T->prior_norm, T->roche_priors, ws.geo, ws.status, ws.prior, ws.bstatus, T->gp,
                 T->gp_gather, T->gp_base, ws.done};
     S.fixed_invalid = T->fixed_invalid;
+    S.prior_c = T->prior_c;
     if (prop) {
         S.pos = prop->pos;
         S.a = prop->a;
@@ -2072,6 +2120,7 @@ int lfg_lnprior(const double* walkers, int W, const lfg_tree* T, double* lnprior
                 T->prior_p2, T->prior_norm, T->roche_priors, ws.geo, ws.status, ws.prior, ws.bstatus, 0,
                 nullptr, nullptr, nullptr};
     S.fixed_invalid = T->fixed_invalid;
+    S.prior_c = T->prior_c;
     const int nlanes = 2 * W * T->E + W;
     hipLaunchKernelGGL(k_setup, dim3((nlanes + SETUP_BLOCK - 1) / SETUP_BLOCK), dim3(SETUP_BLOCK), 0, st, S);
     int rc = launch_ok();
@@ -2266,9 +2315,9 @@ int lfg_gp_lnlike(const double* x, const double* ye, const double* res, int W, i
 
 #ifdef LFG_PROFILE_SETUP
 // diagnostic build only: copy the k_setup lane stamps to the host
-int lfg_debug_setup_stamps(unsigned long long* host)
+int lfg_debug_setup_cycles(unsigned long long* host)
 {
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_setup_dbg), sizeof(g_setup_dbg)) == hipSuccess ? 0 : -1;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_setup_cyc), sizeof(g_setup_cyc)) == hipSuccess ? 0 : -1;
 }
 #endif
 

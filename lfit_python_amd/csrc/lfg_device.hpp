@@ -997,4 +997,8 @@ __device__ inline double prior_lnprob(int type, double p1, double p2, double nor
     return -INFINITY;
 }
 
+// ln of the smallest positive double (a denormal): below it scipy's pdf is
+// 0 and log(pdf) -inf (model.py:85-89)
+constexpr double PDF_LN_MIN = -745.1332191019412;
+
 }  // namespace lfg

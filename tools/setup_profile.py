@@ -28,20 +28,16 @@ W = init.shape[0]
 for _ in range(3):
     ev(torch.as_tensor(init, device=dev))
 torch.cuda.synchronize()
-g = ev._ws[:W * 48 * 8].view(torch.float64).reshape(W, 48).cpu().numpy()
-for k, name in [(42, 'setup: gather + roche_init'), (44, 'setup: findi'), (47, 'setup lane'),
-                (46, 'stream: roche_init + bspot'), (43, 'stream lane'), (45, 'prior lane')]:
-    v = g[:, k]
-    print('%-28s cycles mean %9.0f  max %9.0f' % (name, v.mean(), v.max()))
-print('shader clock over the prior lanes: %.0f MHz' % (100.0 * g[:, 45].sum() / g[:, 41].sum()))
 import ctypes  # noqa: E402
 from lfit_python_amd import _native  # noqa: E402
 L = _native.lib()
-buf = np.zeros((3, 2, 4096), dtype=np.uint64)
-L.lfg_debug_setup_stamps(ctypes.c_void_p(buf.ctypes.data))
-n = {0: W, 1: W, 2: W}
-t0 = min(int(buf[k, 0, :n[k]].min()) for k in n)
-for k, name in [(0, 'setup'), (1, 'stream'), (2, 'prior')]:
-    st, en = (buf[k, 0, :n[k]].astype(np.int64) - t0) / 100.0, (buf[k, 1, :n[k]].astype(np.int64) - t0) / 100.0
-    print('%-7s lanes: start %.2f..%.2f us  end %.2f..%.2f us  (median end %.2f)' % (
-        name, st.min(), st.max(), en.min(), en.max(), np.median(en)))
+cyc = np.zeros((11, 4096), dtype=np.uint64)
+L.lfg_debug_setup_cycles(ctypes.c_void_p(cyc.ctypes.data))
+cyc = cyc[:, :W].astype(np.float64)
+names = ['setup: gather', 'setup: roche_init', 'setup: findi', 'setup lane total',
+         'stream: gather', 'stream: roche_init', 'stream: bspot (table)', 'stream lane total',
+         'prior lane total', None, 'prior: roche_init + findphi90']
+for k, name in enumerate(names):
+    if name:
+        print('%-30s cycles mean %8.0f  max %8.0f' % (name, cyc[k].mean(), cyc[k].max()))
+print('shader clock over the prior lanes: %.0f MHz' % (100.0 * cyc[8].sum() / cyc[9].sum()))
