@@ -195,10 +195,11 @@ __device__ inline void bspot_lane(const SetupArgs& A, int t)
     LFG_CY(4, t, tb);
 #endif
     Roche R;
-    int st = (isfinite(q) && isfinite(rdisc) && isfinite(az)) ? roche_init(R, q) : ST_BAD_ARGS;
+    QPatch qp;
+    int st = (isfinite(q) && isfinite(rdisc) && isfinite(az)) ? roche_init(R, q, &qp) : ST_BAD_ARGS;
     LFG_CY(5, t, tb);
     double bs[4] = {0.0, 0.0, 0.0, 0.0};
-    if (st == ST_OK) st = bspot<false>(R, rdisc * R.xl1, bs);
+    if (st == ST_OK) st = bspot<false>(R, rdisc * R.xl1, bs, &qp);
     LFG_CY(6, t, tb);
     double rprior = 0.0;
     if (st != ST_OK) {
@@ -235,12 +236,19 @@ __device__ inline void prior_lane(const SetupArgs& A, int w)
     const Prop P = make_prop(A, w);
     double lp = 0.0;
     if (A.roche_priors) {
+        // LCModel.ln_prior: dphi <= findphi(q, 90) - 1e-6, findphi from the
+        // q series of the stream table (~1e-16; the solver outside its range)
         const double q = gather_par(A, P, gat[4]);
         const double dphi = gather_par(A, P, gat[5]);
-        Roche R;
+        const QPatch qp = q_patch(q);
         double maxphi;
-        if (roche_init(R, q) != ST_OK || findphi_fast(R, 90.0, maxphi) != ST_OK) lp = -INFINITY;
-        else if (dphi > maxphi - DPHI_TOL) lp = -INFINITY;
+        if (qp.iq >= 0) {
+            maxphi = q_series(kStPhi90, qp);
+        } else {
+            Roche R;
+            if (roche_init(R, q) != ST_OK || findphi_fast(R, 90.0, maxphi) != ST_OK) maxphi = -INFINITY;
+        }
+        if (!(dphi <= maxphi - DPHI_TOL)) lp = -INFINITY;
         LFG_CY(10, w, tr);
     }
     // the walker's parameters in chunks of PCH: each chunk's loads are issued

@@ -128,13 +128,54 @@ __device__ __forceinline__ void rgrad(const Roche& R, double x, double y, double
     gz = (i1 + i2) * z;
 }
 
-// MODEL_SPEC 4.1: L1 point, safeguarded Newton on dPhi/dx (monotone on (0,1))
-__device__ inline double xl1_solve(double q)
+// Patch of ln q in the q series of lfg_stream_table.h (tools/gen_stream_table.py):
+// iq < 0 when q lies outside [LFG_ST_QLO, LFG_ST_QHI]
+struct QPatch {
+    int iq;
+    double xq;
+};
+
+__constant__ const double kStXl1[LFG_ST_NQ * (LFG_ST_DR + 1)] = LFG_ST_XL1;
+__constant__ const double kStPhi90[LFG_ST_NQ * (LFG_ST_DR + 1)] = LFG_ST_PHI90;
+
+// Clenshaw sum of c[0..n-1] T_k(x)
+template <int N>
+__device__ __forceinline__ double clenshaw(const double* c, double x)
+{
+    const double x2 = x + x;
+    double b1 = 0.0, b2 = 0.0;
+#pragma unroll
+    for (int k = N - 1; k >= 1; --k) {
+        const double t = fma(x2, b1, c[k] - b2);
+        b2 = b1;
+        b1 = t;
+    }
+    return fma(x, b1, c[0] - b2);
+}
+
+__device__ inline QPatch q_patch(double q)
+{
+    if (!(q >= LFG_ST_QLO && q <= LFG_ST_QHI)) return QPatch{-1, 0.0};
+    const double fq = (log(q) - LFG_ST_LQLO) * (1.0 / LFG_ST_LQW);
+    const int iq = min(max(int(fq), 0), LFG_ST_NQ - 1);
+    return QPatch{iq, 2.0 * (fq - iq) - 1.0};
+}
+
+// a 1-D q series of the table (LFG_ST_XL1, LFG_ST_PHI90, LFG_ST_RMIN layout)
+__device__ __forceinline__ double q_series(const double* tab, const QPatch& p)
+{
+    return clenshaw<LFG_ST_DR + 1>(tab + p.iq * (LFG_ST_DR + 1), p.xq);
+}
+
+// MODEL_SPEC 4.1: L1 point, safeguarded Newton on dPhi/dx (monotone on (0,1)),
+// from x0: the q series of xl1 (within ~1e-16: one Newton step confirms it)
+// or 1 - (mu/3)^(1/3)
+__device__ inline double xl1_solve(double q, double x0)
 {
     const double i1q = rcp_fast(1.0 + q);
     const double cA = 2.0 * i1q, cB = q * cA, mu = q * i1q;
     double lo = 0.0, hi = 1.0;
-    double x = 1.0 - cbrt(mu * (1.0 / 3.0));
+    double x = (x0 > 0.0 && x0 < 1.0) ? x0 : 1.0 - cbrt(mu * (1.0 / 3.0));
     for (int it = 0; it < 200; ++it) {
         const double omx = 1.0 - x;
         const double ix = rcp_fast(x), io = rcp_fast(omx);
@@ -150,7 +191,8 @@ __device__ inline double xl1_solve(double q)
     return x;
 }
 
-__device__ inline int roche_init(Roche& R, double q)
+// qp (nullable) receives q's table patch for later lookups (bspot)
+__device__ inline int roche_init(Roche& R, double q, QPatch* qp = nullptr)
 {
     if (!(q > 0.0) || !isfinite(q)) return ST_BAD_Q;
     R.q = q;
@@ -158,7 +200,9 @@ __device__ inline int roche_init(Roche& R, double q)
     R.cA = 2.0 * i1q;
     R.cB = q * R.cA;
     R.mu = q * i1q;
-    R.xl1 = xl1_solve(q);
+    const QPatch p = q_patch(q);
+    if (qp) *qp = p;
+    R.xl1 = xl1_solve(q, p.iq >= 0 ? q_series(kStXl1, p) : -1.0);
     R.pl1 = rpot(R, R.xl1, 0.0, 0.0);
     R.Rs = 1.0 - R.xl1;
     R.Rs2 = R.Rs * R.Rs;
@@ -761,21 +805,6 @@ __constant__ const double kStCoef[LFG_ST_NQ * LFG_ST_NS * 3 * (LFG_ST_DQ + 1) * 
 constexpr double kStSb[LFG_ST_NS + 1] = LFG_ST_SB;
 constexpr int ST_PATCH = (LFG_ST_DQ + 1) * (LFG_ST_DS + 1);
 
-// Clenshaw sum of c[0..n-1] T_k(x)
-template <int N>
-__device__ __forceinline__ double clenshaw(const double* c, double x)
-{
-    const double x2 = x + x;
-    double b1 = 0.0, b2 = 0.0;
-#pragma unroll
-    for (int k = N - 1; k >= 1; --k) {
-        const double t = fma(x2, b1, c[k] - b2);
-        b2 = b1;
-        b1 = t;
-    }
-    return fma(x, b1, c[0] - b2);
-}
-
 // one output of a patch: sum_i T_i(xq) sum_j c[i][j] T_j(xs); the DQ + 1 inner
 // sums are independent chains (13 levels), then one 10-level chain
 __device__ __forceinline__ double st_patch(const double* c, double xq, double xs)
@@ -790,17 +819,16 @@ __device__ __forceinline__ double st_patch(const double* c, double xq, double xs
 // (trm.roche.bspot).  VEL = false leaves out[2..3] unset: the hot path
 // needs the impact point only.
 template <bool VEL = true>
-__device__ inline int bspot(const Roche& R, double rad, double out[4])
+__device__ inline int bspot(const Roche& R, double rad, double out[4], const QPatch* qp = nullptr)
 {
     if (!(rad > 0.0) || !(rad < R.xl1)) return ST_BAD_STREAM;
-    if (!(R.q >= LFG_ST_QLO && R.q <= LFG_ST_QHI))
-        return bspot_rk4(R, rad, out);
-    const double fq = (log(R.q) - LFG_ST_LQLO) * (1.0 / LFG_ST_LQW);
-    const int iq = min(max(int(fq), 0), LFG_ST_NQ - 1);
-    const double xq = 2.0 * (fq - iq) - 1.0;
+    const QPatch p = qp ? *qp : q_patch(R.q);
+    if (p.iq < 0) return bspot_rk4(R, rad, out);
+    const int iq = p.iq;
+    const double xq = p.xq;
     const StreamState s0 = stream_start(R);
     const double r0 = sqrt(s0.x * s0.x + s0.y * s0.y);
-    const double rmin = exp(clenshaw<LFG_ST_DR + 1>(kStRmin + iq * (LFG_ST_DR + 1), xq));
+    const double rmin = exp(q_series(kStRmin, p));
     if (!(rad > rmin) || !(rad < r0)) return ST_BAD_STREAM;  // misses the disc / starts inside rad
     const double s = sqrt((rad - rmin) / (r0 - rmin));
     if (!(s <= LFG_ST_STOP)) return bspot_rk4(R, rad, out);
