@@ -283,13 +283,13 @@ def run(args):
                 evs[i] = h.value
         return evs
 
-    def timed_half(pos, lnp, half, a, seed, step, q, zfac, naccept, lnp_new=None):
-        """the single-process path: lfg_stretch_step_half with the events"""
+    def timed_half(pos, lnp, half, a, seed, step, q, zfac, naccept, lnp_new=None, spec=False):
+        """the single-process path: lfg_stretch_step_half(_spec) with the events"""
         evs = None
         if sampled():
             evs = make_evs()
             events.append((evs, q.shape[0]))
-        ev.step_half(pos, lnp, half, a, seed, step, q, zfac, naccept, lnp_new=lnp_new, events=evs)
+        ev.step_half(pos, lnp, half, a, seed, step, q, zfac, naccept, lnp_new=lnp_new, events=evs, spec=spec)
 
     def timed_shard(pos, half, a, seed, step, lo, q, zfac, lnp_sh):
         """the multi-rank path: this rank's lfg_stretch_step_shard with the events"""

@@ -228,6 +228,28 @@ int lfg_stretch_step_half(double* pos, double* lnp, int W, int half, double a,
                           size_t ws_bytes, void* stream, void* const* ev);
 
 /*
+ * lfg_stretch_step_half with the next half's setup formed speculatively.
+ * The proposal of walker k of the next half uses its partner j's position
+ * after this half's Metropolis step: j's current position or j's proposal.
+ * With spec_out = 1, this call's k_elements also runs the next half's k_setup
+ * lanes for both cases (the chip is mostly idle in k_setup, which is bound by
+ * dependent FP64 latency), and k_lnlike records which moves it accepted.
+ * With spec_in = 1 the call skips k_setup: k_elements takes each pair's
+ * candidate for the partner's actual fate.  spec_in = 1 is valid only when
+ * the previous call on this workspace was this sampler's other half (the
+ * step before for half 0) with spec_out = 1, and pos / lnp were not changed
+ * in between; the chain is bit-identical to lfg_stretch_step_half's.  The
+ * workspace must come from lfg_workspace_size_tree (it holds the candidates).
+ */
+int lfg_stretch_step_half_spec(double* pos, double* lnp, int W, int half,
+                               double a, unsigned long long seed,
+                               unsigned long long step, double* q,
+                               double* zfac, const lfg_tree* tree,
+                               int* naccept, double* lnp_new, int spec_in,
+                               int spec_out, void* ws, size_t ws_bytes,
+                               void* stream, void* const* ev);
+
+/*
  * The half-step of one rank when the walkers of each half are sharded over
  * ranks (the replacement of the reference's pool.map over walkers,
  * mcmcfit.py:273-288).  lfg_stretch_step_shard forms the proposals of

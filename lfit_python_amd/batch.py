@@ -173,6 +173,7 @@ class LnProbEvaluator:
             p('gp_gather'), p('gp_base'), p('gp_ecl'), int(tree.fixed_invalid), p('prior_c'))
         self._ws = None
         self._ws_walkers = 0
+        self._spec_key = None  # step_half(spec=True): what the workspace's candidates are for
         # bumped whenever the workspace is reallocated: a captured HIP graph
         # holds the old pointer (sampler.EnsembleSampler re-captures on change)
         self.generation = 0
@@ -210,6 +211,7 @@ class LnProbEvaluator:
         if nd != self.tree.ndim:
             raise ValueError("walker vectors have %d entries, the tree has %d" % (nd, self.tree.ndim))
         self._ensure(W)
+        self._spec_key = None  # lfg_lnprob's workspace layout overlaps the candidates
         if out is None:
             out = torch.empty(W, dtype=torch.float64, device=self.device)
         rc = self.L.lfg_lnprob(ctypes.c_void_p(walkers.data_ptr()), W, ctypes.byref(self.ctree),
@@ -227,22 +229,47 @@ class LnProbEvaluator:
         lnp and naccept of half `half` in place."""
         W = pos.shape[0]
         self._ensure(W // 2)
+        self._spec_key = None
         vp = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
         rc = self.L.lfg_stretch_lnprob_accept(vp(pos), vp(lnp), W, half, vp(q), vp(zfac), ctypes.byref(self.ctree),
                                               seed, step, vp(naccept), vp(lnp_new), vp(self._ws), self._ws.numel(),
                                               _native.stream_ptr(self.device), events)
         _native.check(rc, "lfg_stretch_lnprob_accept")
 
-    def step_half(self, pos, lnp, half, a, seed, step, q, zfac, naccept, lnp_new=None, events=None):
+    def step_half(self, pos, lnp, half, a, seed, step, q, zfac, naccept, lnp_new=None, events=None, spec=False):
         """A whole stretch-move half-step (lfg_stretch_step_half): propose half
-        `half` into q / zfac, evaluate, accept; pos, lnp, naccept in place."""
+        `half` into q / zfac, evaluate, accept; pos, lnp, naccept in place.
+        spec=True (lfg_stretch_step_half_spec): this call also forms the next
+        half's setup for both fates of each partner, and skips its own k_setup
+        when the previous call on this evaluator left exactly this half's
+        candidates (same ensemble tensors, seed, a, the preceding half, and no
+        other entry point since; the caller clears it with invalidate_spec()
+        when it changes pos / lnp itself)."""
         W = pos.shape[0]
+        gen = self.generation
         self._ensure(W // 2)
         vp = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
-        rc = self.L.lfg_stretch_step_half(vp(pos), vp(lnp), W, half, a, seed, step, vp(q), vp(zfac),
-                                          ctypes.byref(self.ctree), vp(naccept), vp(lnp_new), vp(self._ws),
-                                          self._ws.numel(), _native.stream_ptr(self.device), events)
-        _native.check(rc, "lfg_stretch_step_half")
+        if not spec:
+            self._spec_key = None
+            rc = self.L.lfg_stretch_step_half(vp(pos), vp(lnp), W, half, a, seed, step, vp(q), vp(zfac),
+                                              ctypes.byref(self.ctree), vp(naccept), vp(lnp_new), vp(self._ws),
+                                              self._ws.numel(), _native.stream_ptr(self.device), events)
+            _native.check(rc, "lfg_stretch_step_half")
+            return
+        ens = (W, pos.data_ptr(), lnp.data_ptr(), q.data_ptr(), zfac.data_ptr(), seed, float(a))
+        spec_in = gen == self.generation and self._spec_key == ens + (half, step)
+        self._spec_key = None
+        rc = self.L.lfg_stretch_step_half_spec(vp(pos), vp(lnp), W, half, a, seed, step, vp(q), vp(zfac),
+                                               ctypes.byref(self.ctree), vp(naccept), vp(lnp_new),
+                                               int(spec_in), 1, vp(self._ws), self._ws.numel(),
+                                               _native.stream_ptr(self.device), events)
+        _native.check(rc, "lfg_stretch_step_half_spec")
+        self._spec_key = ens + (1 - half, step + half)
+
+    def invalidate_spec(self):
+        """Forget the speculative candidates (the ensemble was changed outside
+        step_half)."""
+        self._spec_key = None
 
     def step_shard(self, pos, half, a, seed, step, lo, q, zfac, lnp_new, events=None):
         """This rank's part of a sharded half-step (lfg_stretch_step_shard):
@@ -250,6 +277,7 @@ class LnProbEvaluator:
         lnp_new.numel()) into q / zfac and their ln_prob into lnp_new."""
         W, n = pos.shape[0], lnp_new.shape[0]
         self._ensure(n)
+        self._spec_key = None
         vp = lambda t: ctypes.c_void_p(t.data_ptr())
         rc = self.L.lfg_stretch_step_shard(vp(pos), W, half, a, seed, step, lo, n, vp(q), vp(zfac),
                                            ctypes.byref(self.ctree), vp(lnp_new), vp(self._ws), self._ws.numel(),
@@ -263,6 +291,7 @@ class LnProbEvaluator:
             walkers = walkers.to(device=self.device, dtype=torch.float64).contiguous()
         W = walkers.shape[0]
         self._ensure(W)
+        self._spec_key = None
         if out is None:
             out = torch.empty(W, dtype=torch.float64, device=self.device)
         rc = self.L.lfg_lnprior(ctypes.c_void_p(walkers.data_ptr()), W, ctypes.byref(self.ctree),

@@ -31,7 +31,7 @@ constexpr int SETUP_BLOCK = 64;
 #endif
 constexpr int ELEM_BLOCK = LFG_ELEM_BLOCK;
 #ifndef ELEM_MINW
-#define ELEM_MINW 1  // minimum waves per SIMD of k_elements
+#define ELEM_MINW 5  // minimum waves per SIMD of k_elements (94 VGPRs: the speculative setup lanes spill to fit)
 #endif
 // per-pair weight block written by k_elements: disc ring weights, the disc
 // total 2 pi [P(rdisc) - P(rin)], spot element weights
@@ -62,12 +62,23 @@ struct Ws {
     double* lle;
     int* done;      // [W] eclipses finished per walker (k_lnlike's fused combine, E > 1)
     double* res;    // [pairs][gp_n] GP trees: residuals y - flux (k_lnlike<2> -> k_gp_like)
+    // speculative setup (lfg_stretch_step_half_spec): per half parity h and
+    // candidate c (the partner's move rejected / accepted) the k_setup
+    // outputs of the next half, formed inside the previous half's k_elements
+    double* geoC;   // [2][2][pairs][NGEO]
+    int* statusC;   // [2][2][pairs]
+    int* bstatusC;  // [2][2][pairs]
+    double* priorC; // [2][2][W]
+    double* qC;     // [2][2][W][ndim]
+    double* zfC;    // [2][2][W]
+    int* jk;        // [2][W] the partner (in the other half) of walker w's proposal
+    int* accflag;   // [W] 1: walker w's move was accepted in the last half
     size_t total;
 };
 
 inline size_t align256(size_t v) { return (v + 255) & ~size_t(255); }
 
-Ws carve(void* base, int W, int E, int gp_n = 0)
+Ws carve(void* base, int W, int E, int gp_n = 0, int ndim_spec = 0)
 {
     const size_t pairs = size_t(W) * size_t(E);
     Ws ws{};
@@ -84,6 +95,16 @@ Ws carve(void* base, int W, int E, int gp_n = 0)
     ws.lle = reinterpret_cast<double*>(take(pairs * sizeof(double)));
     ws.done = reinterpret_cast<int*>(take(size_t(W) * sizeof(int)));
     ws.res = gp_n > 0 ? reinterpret_cast<double*>(take(pairs * size_t(gp_n) * sizeof(double))) : nullptr;
+    if (ndim_spec > 0) {
+        ws.geoC = reinterpret_cast<double*>(take(4 * pairs * LFG_NGEO * sizeof(double)));
+        ws.statusC = reinterpret_cast<int*>(take(4 * pairs * sizeof(int)));
+        ws.bstatusC = reinterpret_cast<int*>(take(4 * pairs * sizeof(int)));
+        ws.priorC = reinterpret_cast<double*>(take(4 * size_t(W) * sizeof(double)));
+        ws.qC = reinterpret_cast<double*>(take(4 * size_t(W) * ndim_spec * sizeof(double)));
+        ws.zfC = reinterpret_cast<double*>(take(4 * size_t(W) * sizeof(double)));
+        ws.jk = reinterpret_cast<int*>(take(2 * size_t(W) * sizeof(int)));
+        ws.accflag = reinterpret_cast<int*>(take(size_t(W) * sizeof(int)));
+    }
     ws.total = off;
     return ws;
 }
@@ -126,32 +147,55 @@ struct SetupArgs {
     int lo, ns;
     int fixed_invalid;  // lfg_tree.fixed_invalid: every prior lane gives -inf
     const double* prior_c;  // lfg_tree.prior_c (nullable): [ndim][2] Prior.ln_prob constants
+    // speculative setup of the next half (lfg_stretch_step_half_spec): cand 1
+    // forms the proposal from the partner's own proposal of the half before
+    // (step_prev, the other half), i.e. as if the partner's move is accepted;
+    // cand 0 from the partner's current position.  jkout: the partner index.
+    int cand;
+    unsigned long long step_prev;
+    int* jkout;
 };
 
 // where a lane reads walker w's parameters: the walker row, or the
-// stretch-move proposal s + z (c_j - s) ... written as k_propose writes it
+// stretch-move proposal s + z (c_j - s) ... written as k_propose writes it;
+// with ci the partner's position is itself the proposal cj + zj (ci - cj)...
+// of the half before (speculative setup, candidate 1)
 struct Prop {
     const double* s;
     const double* cj;
     double z;
+    const double* ci;
+    double zj;
 };
 
 __device__ inline Prop make_prop(const SetupArgs& A, int w)
 {
-    if (!A.pos) return Prop{A.walkers + size_t(w) * A.ndim, nullptr, 0.0};
+    if (!A.pos) return Prop{A.walkers + size_t(w) * A.ndim, nullptr, 0.0, nullptr, 0.0};
     const int ns = A.ns, i = A.lo + w;  // walker i of the half, as k_propose's lane i
     const uint4 r = draw(A.seed, A.step, A.half, 0, i);
     const double u = u53(r.x, r.y);
     const double zr = (A.a - 1.0) * u + 1.0;
     const int j = int(__umulhi(r.z, unsigned(ns)));
-    return Prop{A.pos + size_t(A.half * ns + i) * A.ndim, A.pos + size_t((1 - A.half) * ns + j) * A.ndim,
-                zr * zr / A.a};
+    if (A.jkout && A.cand == 0) A.jkout[w] = j;
+    Prop P{A.pos + size_t(A.half * ns + i) * A.ndim, A.pos + size_t((1 - A.half) * ns + j) * A.ndim,
+           zr * zr / A.a, nullptr, 0.0};
+    if (A.cand) {  // partner j's proposal in the other half (step_prev), as its own make_prop forms it
+        const int hp = 1 - A.half;
+        const uint4 rj = draw(A.seed, A.step_prev, hp, 0, j);
+        const double zrj = (A.a - 1.0) * u53(rj.x, rj.y) + 1.0;
+        const int ij = int(__umulhi(rj.z, unsigned(ns)));
+        P.ci = A.pos + size_t(A.half * ns + ij) * A.ndim;
+        P.zj = zrj * zrj / A.a;
+    }
+    return P;
 }
 
 __device__ __forceinline__ double gather_par(const SetupArgs& A, const Prop& P, int g)
 {
     if (g < 0) return A.consts[-1 - g];
-    return P.cj ? fma(P.s[g] - P.cj[g], P.z, P.cj[g]) : P.s[g];
+    if (!P.cj) return P.s[g];
+    const double cj = P.ci ? fma(P.cj[g] - P.ci[g], P.zj, P.ci[g]) : P.cj[g];
+    return fma(P.s[g] - cj, P.z, cj);
 }
 
 // Diagnostic build only (-DLFG_PROFILE_SETUP): s_memtime cycle counts of the
@@ -315,9 +359,10 @@ __device__ inline void prior_lane(const SetupArgs& A, int w)
 #endif
 }
 
-__global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
+// one lane of k_setup: t < npairs setup lanes, then W prior lanes, then
+// npairs stream lanes
+__device__ __forceinline__ void setup_any(const SetupArgs& A, int t)
 {
-    const int t = blockIdx.x * SETUP_BLOCK + threadIdx.x;
     const int npairs = A.W * A.E;
     if (t >= 2 * npairs + A.W) return;
 #if defined(LFG_EXP_SETUP_EMPTY)  // experiment build: the launch alone (every pair fails)
@@ -430,6 +475,11 @@ __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
     LFG_CY(3, t, tl);
 }
 
+__global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
+{
+    setup_any(A, blockIdx.x * SETUP_BLOCK + threadIdx.x);
+}
+
 // ------------------------------------------------------------- k_elements
 // One lane per symmetry-unique element.  The WD/disc grids are mirror
 // symmetric under y -> -y and the donor grid under y -> -y and z -> -z; the
@@ -478,10 +528,45 @@ __device__ inline double bs_weight(int j, const double* G)
     return exp(G[G_EXP1] * log(uk) - pow(uk, G[G_EXP2]) - G[G_LNPK]);
 }
 
-__global__ __launch_bounds__(ELEM_BLOCK, ELEM_MINW) void k_elements(const double* __restrict__ geo, int* status, int npairs,
+// k_elements' side jobs in lfg_stretch_step_half_spec:
+//  - sel: this half's k_setup outputs were formed speculatively inside the
+//    previous half's k_elements for both fates of each walker's partner;
+//    the pair takes candidate c = accflag[jk[w]] and its first block copies
+//    it into the standard workspace slots k_lnlike reads
+//  - spec: the leading nspecblk blocks run the k_setup lanes of the next half
+//    for both candidates (setup_any on S[0], S[1])
+struct ElemSpec {
+    const int* jk;  // nullptr: no selection
+    const int* accflag;
+    const double* geoC;
+    const int* statusC;
+    const int* bstatusC;
+    const double* priorC;
+    const double* qC;
+    const double* zfC;
+    double* prior;
+    double* q;
+    double* zf;
+    int* done;
+    int* bstatus;
+    int E, ndim;
+    SetupArgs S[2];
+    int nspec;     // lanes per candidate (0: no speculative setup)
+    int nspecblk;  // leading blocks that run them
+};
+
+__global__ __launch_bounds__(ELEM_BLOCK) __attribute__((amdgpu_waves_per_eu(ELEM_MINW))) void k_elements(const double* __restrict__ geo, int* status, int npairs,
                                                          double2* __restrict__ AB, double* __restrict__ DON,
-                                                         double* __restrict__ WT, const int* __restrict__ bstatus)
+                                                         double* __restrict__ WT, const int* __restrict__ bstatus,
+                                                         ElemSpec X)
 {
+    if (int(blockIdx.x) < X.nspecblk) {  // speculative setup lanes of the next half
+        const int t = int(blockIdx.x) * int(blockDim.x) + int(threadIdx.x);
+        const int c = t < X.nspec ? 0 : 1;
+        if (t < 2 * X.nspec) setup_any(X.S[c], t - c * X.nspec);
+        return;
+    }
+    const unsigned bid = blockIdx.x - unsigned(X.nspecblk);
     // blocks cover the NUNIQ unique items of every pair in chunks of
     // blockDim.x (the spot items fill the last chunk); block b takes pair
     // b % npairs, so that (with npairs a multiple of 8 and blocks dealt
@@ -489,8 +574,34 @@ __global__ __launch_bounds__(ELEM_BLOCK, ELEM_MINW) void k_elements(const double
     // L2 k_lnlike block `pair` reads them from -- speed only.  Item 0 folds
     // the stream lanes' status into the pair status (MODEL_SPEC 6 order:
     // setup failures first); every item skips a pair that failed either.
-    const int pair = int(blockIdx.x % unsigned(npairs));
-    const int v = int(blockIdx.x / unsigned(npairs)) * int(blockDim.x) + int(threadIdx.x);
+    const int pair = int(bid % unsigned(npairs));
+    const int v = int(bid / unsigned(npairs)) * int(blockDim.x) + int(threadIdx.x);
+    const double* G = geo + size_t(pair) * LFG_NGEO;
+    int st0, bst;
+    if (X.jk) {
+        const int w = pair / X.E, e = pair - w * X.E;
+        const size_t cp = size_t(X.accflag[X.jk[w]]) * npairs + pair;  // candidate slot of the pair
+        G = X.geoC + cp * LFG_NGEO;
+        st0 = X.statusC[cp];
+        bst = X.bstatusC[cp];
+        if (bid < unsigned(npairs)) {  // the pair's first block: the selected candidate into the standard slots
+            const int l = int(threadIdx.x);
+            double* Gd = const_cast<double*>(geo) + size_t(pair) * LFG_NGEO;
+            if (l < LFG_NGEO) Gd[l] = G[l];
+            if (l == LFG_NGEO) status[pair] = (st0 != ST_OK) ? st0 : bst;
+            if (l == LFG_NGEO + 1) X.bstatus[pair] = bst;
+            if (e == 0) {
+                const size_t cw = size_t(X.accflag[X.jk[w]]) * (npairs / X.E) + w;
+                for (int d = l; d < X.ndim; d += int(blockDim.x)) X.q[size_t(w) * X.ndim + d] = X.qC[cw * X.ndim + d];
+                if (l == LFG_NGEO + 2) X.prior[w] = X.priorC[cw];
+                if (l == LFG_NGEO + 3) X.zf[w] = X.zfC[cw];
+                if (l == LFG_NGEO + 4 && X.done) X.done[w] = 0;
+            }
+        }
+    } else {
+        st0 = status[pair];
+        bst = bstatus[pair];
+    }
     if (v >= NUNIQ) return;
 #ifndef LFG_EXP_OLDORDER
     // launch order WD, disc, spot, donor: the last chunk, dispatched last,
@@ -507,13 +618,11 @@ __global__ __launch_bounds__(ELEM_BLOCK, ELEM_MINW) void k_elements(const double
 #elif defined(LFG_EXP_ONLYWD)
     if (u >= U_WD) return;
 #endif
-    const int st0 = status[pair], bst = bstatus[pair];
     if (st0 != ST_OK) return;
     if (bst != ST_OK) {
-        if (u == 0) status[pair] = bst;
+        if (u == 0 && !X.jk) status[pair] = bst;
         return;
     }
-    const double* G = geo + size_t(pair) * LFG_NGEO;
     const Roche R{G[G_Q], G[G_CA], G[G_CB], G[G_MU], G[G_XL1], G[G_PL1], G[G_RS], G[G_RS2]};
     const double s = G[G_S], c = G[G_C];
 
@@ -726,6 +835,7 @@ struct LikeArgs {
     int* naccept;
     double* res;  // MODE 2: [pairs][N] residuals for k_gp_like
     const int* bstatus;  // fused element phase: the stream lanes' status (folded into status here)
+    int* accflag;        // nullable, [W]: 1 where the walker's move was accepted (speculative setup)
 };
 
 
@@ -760,6 +870,9 @@ __device__ inline void combine_walker(const LikeArgs& L, int w)
             for (int d = 0; d < L.ndim; ++d) p[d] = qi[d];
             L.lnp_ens[wg] = v;
             if (L.naccept) L.naccept[wg] += 1;
+            if (L.accflag) L.accflag[w] = 1;
+        } else if (L.accflag) {
+            L.accflag[w] = 0;
         }
     }
 }
@@ -1297,6 +1410,7 @@ __device__ inline void finish_walker(const LikeArgs& L, int pair, int tid, bool 
             if (L.naccept) L.naccept[wg] += 1;
         }
         sflag[0] = a ? 1 : 0;
+        if (L.accflag) L.accflag[pair] = a ? 1 : 0;
     }
     __syncthreads();
     if (sflag[0] && tid < L.ndim) L.pos[size_t(wg) * L.ndim + tid] = aq;
@@ -1987,7 +2101,8 @@ constexpr bool kFused = true;
 constexpr bool kFused = false;
 #endif
 
-int run_front(const SetupArgs& S, const Ws& ws, hipStream_t st, void* const* ev, bool elements = !kFused)
+int run_front(const SetupArgs& S, const Ws& ws, hipStream_t st, void* const* ev, bool elements = !kFused,
+              const ElemSpec* X = nullptr, bool setup = true)
 {
     auto mark = [&](int i) {
         if (ev && ev[i]) (void)hipEventRecord(static_cast<hipEvent_t>(ev[i]), st);
@@ -1995,13 +2110,17 @@ int run_front(const SetupArgs& S, const Ws& ws, hipStream_t st, void* const* ev,
     const int npairs = S.W * S.E;
     const int nlanes = 2 * npairs + S.W;
     mark(0);
-    hipLaunchKernelGGL(k_setup, dim3((nlanes + SETUP_BLOCK - 1) / SETUP_BLOCK), dim3(SETUP_BLOCK), 0, st, S);
-    if (launch_ok() != LFG_OK) return LFG_E_LAUNCH;
+    if (setup) {
+        hipLaunchKernelGGL(k_setup, dim3((nlanes + SETUP_BLOCK - 1) / SETUP_BLOCK), dim3(SETUP_BLOCK), 0, st, S);
+        if (launch_ok() != LFG_OK) return LFG_E_LAUNCH;
+    }
     mark(1);
     if (elements) {
         constexpr int chunks = (NUNIQ + ELEM_BLOCK - 1) / ELEM_BLOCK;
-        hipLaunchKernelGGL(k_elements, dim3(unsigned(npairs) * chunks), dim3(ELEM_BLOCK), 0, st, ws.geo, ws.status,
-                           npairs, ws.ab, ws.donor, ws.wts, ws.bstatus);
+        ElemSpec none{};
+        const ElemSpec& XS = X ? *X : none;
+        hipLaunchKernelGGL(k_elements, dim3(unsigned(npairs) * chunks + unsigned(XS.nspecblk)), dim3(ELEM_BLOCK), 0,
+                           st, ws.geo, ws.status, npairs, ws.ab, ws.donor, ws.wts, ws.bstatus, XS);
         if (launch_ok() != LFG_OK) return LFG_E_LAUNCH;
     }
     mark(2);
@@ -2021,7 +2140,7 @@ size_t lfg_workspace_size(int W, int E)
 size_t lfg_workspace_size_tree(int W, const lfg_tree* T)
 {
     if (W <= 0 || !T || T->E <= 0) return 0;
-    return carve(nullptr, W, T->E, T->gp ? T->max_n : 0).total;
+    return carve(nullptr, W, T->E, T->gp ? T->max_n : 0, T->ndim).total;  // + lfg_stretch_step_half_spec's
 }
 
 int lfg_flux(const double* pars, int W, int P, const double* x, const double* w, int N, int nsub,
@@ -2067,12 +2186,18 @@ struct Propose {  // inline proposal of lfg_stretch_step_half / _shard
     int lo, ns;  // the batch: walkers lo .. lo + W - 1 of the ns-walker half
 };
 
+struct SpecCtl {  // lfg_stretch_step_half_spec
+    bool in;   // this half's setup candidates are in the workspace (skip k_setup)
+    bool out;  // form the next half's candidates inside this k_elements
+};
+
 static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* lnp, double* lnlike_e, void* wsp,
                        size_t ws_bytes, void* stream, void* const* ev, const Accept* acc = nullptr,
-                       const Propose* prop = nullptr)
+                       const Propose* prop = nullptr, const SpecCtl* sp = nullptr)
 {
     if (W <= 0 || !T || T->E <= 0 || T->ndim <= 0 || T->nsub < 1 || !walkers || (!lnp && !acc)) return LFG_E_ARGS;
-    Ws ws = carve(wsp, W, T->E, T->gp ? T->max_n : 0);
+    if (sp && (!prop || !acc || prop->lo != 0 || prop->ns != W)) return LFG_E_ARGS;
+    Ws ws = carve(wsp, W, T->E, T->gp ? T->max_n : 0, sp ? T->ndim : 0);
     if (!wsp || ws_bytes < ws.total) return LFG_E_WORKSPACE;
     hipStream_t st = static_cast<hipStream_t>(stream);
     auto mark = [&](int i) {
@@ -2095,7 +2220,50 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
         S.ns = prop->ns;
     }
     const int npairs = W * T->E;
-    int rc = run_front(S, ws, st, ev);
+    ElemSpec X{};
+    if (sp) {
+        const int h = prop->half, hn = 1 - prop->half;
+        const size_t P48 = size_t(npairs) * LFG_NGEO;
+        if (sp->in) {
+            X.jk = ws.jk + size_t(h) * W;
+            X.accflag = ws.accflag;
+            X.geoC = ws.geoC + 2 * h * P48;
+            X.statusC = ws.statusC + 2 * h * size_t(npairs);
+            X.bstatusC = ws.bstatusC + 2 * h * size_t(npairs);
+            X.priorC = ws.priorC + 2 * h * size_t(W);
+            X.qC = ws.qC + 2 * h * size_t(W) * T->ndim;
+            X.zfC = ws.zfC + 2 * h * size_t(W);
+            X.prior = ws.prior;
+            X.q = prop->q;
+            X.zf = prop->zfac;
+            X.done = ws.done;
+            X.bstatus = ws.bstatus;
+        }
+        X.E = T->E;
+        X.ndim = T->ndim;
+        if (sp->out) {
+            for (int c = 0; c < 2; ++c) {
+                SetupArgs& N = X.S[c];
+                N = S;
+                const size_t k = size_t(2 * hn + c);
+                N.half = hn;
+                N.step = hn == 0 ? prop->step + 1 : prop->step;
+                N.step_prev = prop->step;
+                N.cand = c;
+                N.geo = ws.geoC + k * P48;
+                N.status = ws.statusC + k * npairs;
+                N.bstatus = ws.bstatusC + k * npairs;
+                N.prior = ws.priorC + k * W;
+                N.qout = ws.qC + k * size_t(W) * T->ndim;
+                N.zfout = ws.zfC + k * W;
+                N.done = nullptr;
+                N.jkout = ws.jk + size_t(hn) * W;
+            }
+            X.nspec = 2 * npairs + W;
+            X.nspecblk = ((2 * X.nspec + ELEM_BLOCK - 1) / ELEM_BLOCK + 7) / 8 * 8;  // keeps the pair -> XCD map
+        }
+    }
+    int rc = run_front(S, ws, st, ev, !kFused, sp ? &X : nullptr, !(sp && sp->in));
     if (rc) return rc;
     double* lle = lnlike_e ? lnlike_e : ws.lle;
     LikeArgs L{ws.geo, ws.status, ws.ab, ws.donor, ws.wts, T->E, T->off, T->max_n, T->x, T->y, T->ye,
@@ -2104,6 +2272,7 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
                T->ndim, acc ? acc->half : 0, acc ? acc->seed : 0ull, acc ? acc->step : 0ull,
                acc ? acc->naccept : nullptr};
     L.bstatus = ws.bstatus;
+    L.accflag = sp ? ws.accflag : nullptr;
     if (T->gp) {
         L.res = ws.res;
         hipLaunchKernelGGL((k_lnlike<2, kFused>), dim3(npairs), dim3(LIKE_THREADS), 0, st, L);
@@ -2159,6 +2328,20 @@ int lfg_stretch_step_half(double* pos, double* lnp, int W, int half, double a, u
     const Accept acc{pos, lnp, zfac, half, seed, step, naccept};
     const Propose prop{pos, a, q, zfac, half, seed, step, 0, W / 2};
     return lnprob_impl(q, W / 2, T, lnp_new, nullptr, wsp, ws_bytes, stream, ev, &acc, &prop);
+}
+
+int lfg_stretch_step_half_spec(double* pos, double* lnp, int W, int half, double a, unsigned long long seed,
+                               unsigned long long step, double* q, double* zfac, const lfg_tree* T, int* naccept,
+                               double* lnp_new, int spec_in, int spec_out, void* wsp, size_t ws_bytes, void* stream,
+                               void* const* ev)
+{
+    if (W < 4 || (W & 1) || (half != 0 && half != 1) || !(a > 1.0) || !pos || !lnp || !q || !zfac || !T)
+        return LFG_E_ARGS;
+    const Accept acc{pos, lnp, zfac, half, seed, step, naccept};
+    const Propose prop{pos, a, q, zfac, half, seed, step, 0, W / 2};
+    const SpecCtl sp{spec_in != 0, spec_out != 0};
+    // the fused-element build has no k_elements to host the candidates: plain half-step
+    return lnprob_impl(q, W / 2, T, lnp_new, nullptr, wsp, ws_bytes, stream, ev, &acc, &prop, kFused ? nullptr : &sp);
 }
 
 int lfg_stretch_step_shard(const double* pos, int W, int half, double a, unsigned long long seed,

@@ -127,6 +127,11 @@ class EnsembleSampler:
         # the optional half_timer replaces evaluator.step_half (bench timing)
         self.fuse = hasattr(evaluator, "step_half") and isinstance(self.ops, HipStretchOps)
         self.half_timer = None
+        # speculative setup on the fused path (lfg_stretch_step_half_spec): each
+        # half's k_elements also forms the next half's k_setup outputs for both
+        # fates of every partner, so the next half skips k_setup (the evaluator
+        # tracks whether its workspace holds valid candidates)
+        self.spec = os.environ.get("LFG_SPEC", "1") != "0"
         # sharded fused path (N ranks, or forced on one for tests): proposal and
         # ln_prob of this rank's shard in three kernels (lfg_stretch_step_shard),
         # all_gather of ln_prob, acceptance re-forming the proposals
@@ -170,6 +175,8 @@ class EnsembleSampler:
 
     def set_state(self, p0, lnp0=None):
         import torch
+        if hasattr(self.ev, "invalidate_spec"):
+            self.ev.invalidate_spec()  # the candidates were formed from the old positions
         self.pos.copy_(torch.as_tensor(np.asarray(p0), dtype=torch.float64))
         if lnp0 is None:
             self.lnp.copy_(self.ln_prob(self.pos))
@@ -252,8 +259,9 @@ class EnsembleSampler:
         for half in (0, 1):
             if self.world == 1 and self.fuse and self.timer is None and not self.force_shard:
                 f = self.half_timer or self.ev.step_half
+                kw = dict(spec=True) if self.spec else {}
                 f(self.pos, self.lnp, half, self.a, self.seed, self.rng_step, self.q, self.zfac, self.naccept,
-                  lnp_new=self.lnp_new)
+                  lnp_new=self.lnp_new, **kw)
                 continue
             if (self.world > 1 or self.force_shard) and self.fuse_shard and self.timer is None:
                 self._shard_half(half)

@@ -123,11 +123,13 @@ def test_device_mcmc_runs():
 
 
 def test_fused_half_step_matches_separate_kernels():
-    """lfg_stretch_step_half (the default single-process path: proposal in
-    k_setup, acceptance in k_lnlike) gives the chain of lfg_stretch_propose +
-    lfg_lnprob + lfg_stretch_accept, bit for bit, across reset(); and so do
-    lfg_stretch_lnprob_accept and the sharded path (lfg_stretch_step_shard on
-    one or two shards + lfg_stretch_accept_regen)."""
+    """lfg_stretch_step_half_spec (the default single-process path: proposal
+    and setup formed speculatively in the previous half's k_elements,
+    acceptance in k_lnlike) and lfg_stretch_step_half give the chain of
+    lfg_stretch_propose + lfg_lnprob + lfg_stretch_accept, bit for bit, across
+    reset() and set_state(); and so do lfg_stretch_lnprob_accept and the
+    sharded path (lfg_stretch_step_shard on one or two shards +
+    lfg_stretch_accept_regen)."""
     import torch
     from lfit_python_amd import batch, sampler, synthetic
     out = []
@@ -143,9 +145,10 @@ def test_fused_half_step_matches_separate_kernels():
         init = sampler.initialise_walkers(p0, sampler.comp_scatter(m.dynasty_par_names, 0.1), W,
                                           lambda p: ev(torch.as_tensor(p, device="cuda")).cpu().numpy())
         res = []
-        for mode in ("separate", "step_half", "lnprob_accept", "shard1", "shard2"):
+        for mode in ("separate", "spec", "step_half", "lnprob_accept", "shard1", "shard2"):
             S = sampler.EnsembleSampler(W, t.ndim, ev, seed=21)
-            S.fuse = mode in ("step_half", "lnprob_accept")
+            S.fuse = mode in ("spec", "step_half", "lnprob_accept")
+            S.spec = mode == "spec"
             S.force_shard = mode.startswith("shard")
             if mode == "shard2":
                 # two ranks' shards of each half (lfg_stretch_step_shard with
@@ -163,7 +166,9 @@ def test_fused_half_step_matches_separate_kernels():
             S.run_mcmc(init, 4)
             S.reset()
             S.run_mcmc(None, 3)
-            res.append((S.chain.cpu().numpy(), S.lnprob_chain.cpu().numpy(), S.naccept.cpu().numpy()))
+            ch, lc = S.chain.cpu().numpy(), S.lnprob_chain.cpu().numpy()
+            S.run_mcmc(ch[1], 2)  # set_state: new positions drop the speculative candidates
+            res.append((ch, lc, S.chain.cpu().numpy(), S.naccept.cpu().numpy()))
         for other in res[1:]:
             for a, b in zip(res[0], other):
                 np.testing.assert_array_equal(a, b)
@@ -192,6 +197,35 @@ def test_graph_replay_matches_eager():
             assert S._graph is not None
     for a, b in zip(out[0], out[1]):
         np.testing.assert_array_equal(a, b)
+
+
+def test_spec_chain_with_interleaved_calls():
+    """The speculative path stays bit-identical to the plain half-step when
+    other entry points use the evaluator between steps (their workspace use
+    overlaps the candidates, so the next step recomputes its setup)."""
+    import torch
+    from lfit_python_amd import batch, sampler, synthetic
+    m = synthetic.config_single(300, flux_fn=_flux_fn)
+    t = batch.compile_tree(m)
+    ev = batch.LnProbEvaluator(t)
+    p0 = np.array(m.dynasty_par_vals)
+    init = sampler.initialise_walkers(p0, sampler.comp_scatter(m.dynasty_par_names, 0.1), 96,
+                                      lambda p: ev(torch.as_tensor(p, device="cuda")).cpu().numpy())
+    out = []
+    for spec in (False, True):
+        S = sampler.EnsembleSampler(96, t.ndim, ev, seed=5)
+        S.spec = spec
+        S.set_state(init)
+        rows = []
+        for i in range(6):
+            S.step()
+            if i == 2:
+                ev(S.pos[:64].contiguous())  # an lfg_lnprob call on the same workspace
+            rows.append((S.pos.cpu().numpy().copy(), S.lnp.cpu().numpy().copy()))
+        out.append(rows)
+    for (pa, la), (pb, lb) in zip(*out):
+        np.testing.assert_array_equal(pa, pb)
+        np.testing.assert_array_equal(la, lb)
 
 
 # ---------------------------------------------------------------- GP trees
@@ -239,6 +273,29 @@ def test_gp_tree_matches_reference():
     _same(got, d["ln_prob"], LNP_RTOL)
     fin = np.isfinite(d["ln_prior"])
     _same(lle.cpu().numpy().sum(1)[fin], d["ln_like"][fin], LNP_RTOL)
+
+
+def test_gp_tree_spec_chain():
+    """The speculative half-step on the shipped GP tree (87 parameters, 6
+    eclipses: acceptance through k_gp_like's per-walker combine) equals the
+    plain half-step bit for bit."""
+    import torch
+    from lfit_python_amd import batch, cvmodel, sampler
+    m = cvmodel.construct_model(os.path.join(GOLD, "ref_test_data", "mcmc_input.dat"))
+    t = batch.compile_tree(m)
+    ev = batch.LnProbEvaluator(t)
+    p0 = np.array(m.dynasty_par_vals)
+    W = 2 * len(p0) + 2
+    init = sampler.initialise_walkers(p0, sampler.comp_scatter(m.dynasty_par_names, 0.1), W,
+                                      lambda p: ev(torch.as_tensor(p, device="cuda")).cpu().numpy())
+    out = []
+    for spec in (False, True):
+        S = sampler.EnsembleSampler(W, t.ndim, ev, seed=9)
+        S.spec = spec
+        S.run_mcmc(init, 3)
+        out.append((S.chain.cpu().numpy(), S.lnprob_chain.cpu().numpy(), S.naccept.cpu().numpy()))
+    for a, b in zip(*out):
+        np.testing.assert_array_equal(a, b)
 
 
 def test_gp_leaf_scalar_path():
