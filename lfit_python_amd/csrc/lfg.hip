@@ -708,7 +708,8 @@ __global__ __launch_bounds__(ELEM_BLOCK) __attribute__((amdgpu_waves_per_eu(ELEM
     // [cone, ingress, egress], their per-wave maxima, fallbacks, items, eclipsed
     bool fb = false;
     int nit[3] = {0, 0, 0};
-    element_interval_fast(R, Px, Py, Pz, s, c, G[G_RCAL], G[G_REFF], a, b, &fb, nit);
+    double gs[2] = {0.0, 0.0};
+    element_interval_fast(R, Px, Py, Pz, s, c, G[G_RCAL], G[G_REFF], a, b, &fb, nit, gs);
     {
         const int reg = (u < U_WD) ? 0 : (u < U_WD + U_DISC ? 1 : 2);
         unsigned long long* C = g_iter_dbg + reg * 16;
@@ -722,6 +723,11 @@ __global__ __launch_bounds__(ELEM_BLOCK) __attribute__((amdgpu_waves_per_eu(ELEM
         atomicAdd(C + 6, fb ? 1ull : 0ull);
         atomicAdd(C + 7, 1ull);
         atomicAdd(C + 8, (a < b) ? 1ull : 0ull);
+        if (a < b && !fb) {  // initial-guess error of the tangency solves: bins < 1e-4, 1e-3, 1e-2, 3e-2, 1e-1, more
+            const double er = fmax(fabs(gs[0] - a * TWO_PI), fabs(gs[1] - b * TWO_PI));
+            const int bin = er < 1e-4 ? 0 : er < 1e-3 ? 1 : er < 1e-2 ? 2 : er < 3e-2 ? 3 : er < 1e-1 ? 4 : 5;
+            atomicAdd(C + 10 + bin, 1ull);
+        }
     }
 #else
     element_interval_fast(R, Px, Py, Pz, s, c, G[G_RCAL], G[G_REFF], a, b);
@@ -1467,16 +1473,7 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
     // off the tail of the block (combine_walker does it for E > 1)
     const bool acc1 = CHI && !GP && L.pos && L.E == 1;
     double aq = 0.0;
-    if (acc1) {
-        const int wg = L.half * L.npairs + pair;
-        if (tid < L.ndim) aq = L.qprop[size_t(pair) * L.ndim + tid];
-        if (tid == 0) {
-            const uint4 r = draw(L.seed, L.step, L.half, 1, pair);
-            sacc1[0] = log(u53(r.x, r.y));
-            sacc1[1] = L.zfac[pair];
-            sacc1[2] = L.lnp_ens[wg];
-        }
-    }
+    if (acc1 && tid < L.ndim) aq = L.qprop[size_t(pair) * L.ndim + tid];
     int st;
     double s, c, ul, td;
     double px = 0.0, pw = 0.0;  // tile-0 point of this thread (y, ye: read where chi^2 is formed)
@@ -1561,6 +1558,15 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
         if (tid >= NBS && tid < NBS + NWD_RINGS) wring = wd_ring_weight(tid - NBS, ul);
         else if (tid >= NBS + NWD_RINGS && tid < NBS + NWD_RINGS + NDISC_R)
             wring = Wt[WT_DISC + tid - NBS - NWD_RINGS];
+    }
+    // the acceptance draw by the block's last lane, after its prologue loads
+    // are in flight (in wave 0 the Philox rounds and the log delayed every
+    // load of that wave's prologue)
+    if (acc1 && tid == nt - 1) {
+        const uint4 r = draw(L.seed, L.step, L.half, 1, pair);
+        sacc1[0] = log(u53(r.x, r.y));
+        sacc1[1] = L.zfac[pair];
+        sacc1[2] = L.lnp_ens[L.half * L.npairs + pair];
     }
 
     if (st != ST_OK) {

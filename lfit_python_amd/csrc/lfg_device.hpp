@@ -411,10 +411,20 @@ __device__ __forceinline__ void rotate(double& cs, double& sn, double d)
 // 2-D Newton for one contact phase.  Tan holds the running angle th, its
 // cosine and sine (advanced by rotation), the distance t along the line of
 // sight and the state: 0 running, 1 converged to a tangency of the right kind
-// (ingress: g falling with theta), -1 failed.  Newton converges
-// quadratically, so once |dth| and |dt| are <= TH_LAST the step just taken
-// leaves an error ~TH_LAST^2 << TH_TOL and the solve stops there (MODEL_SPEC 7).
+// (ingress: g falling with theta), -1 failed.
+//
+// Each step is Newton on the envelope g(th) = min_t Phi - Phi_L1 evaluated
+// at one point: t moves to the ray's minimum of Phi (dt0 = -F2 / J22), which
+// lowers F1 by F2^2 / (2 J22), and th takes the Newton step of that corrected
+// F1 with the envelope slope J11 + J21 dt0; t then follows th along the
+// valley (dt = dt0 - J21 / J22 dth).  The t guess (closest approach to the
+// donor centre) is ~1e-2 off the tangent point; in the joint 2-D step that
+// error leaks into th at first order, here only at second order, so th
+// converges one step earlier (tools/newton_emul statistics in DESIGN.md).
+// Stop once |dth| <= TH_LAST (th error ~TH_LAST^2 after the step) and
+// |dt| <= T_LAST (t errors reach th squared): ~1e-14 rad (MODEL_SPEC 7).
 constexpr double TH_LAST = 3e-8;
+constexpr double T_LAST = 1e-5;
 
 struct Tan {
     double th, cs, sn, t;
@@ -428,17 +438,19 @@ __device__ __forceinline__ void tangency_step(const Roche& R, double Px, double 
     ConePt o;
     cone_point(R, Px, Py, Pz, s, c, T.cs, T.sn, T.t, o);
     const double F1 = o.phi - R.pl1;
-    const double J11 = T.t * o.gth, J12 = o.F2;
+    const double J11 = T.t * o.gth;
     const double J21 = T.t * o.etHe + o.gth, J22 = o.eHe;
-    const double det = J11 * J22 - J12 * J21;
-    const bool bad = !(det != 0.0);
-    const double idet = rcp_fast(det);
-    double dth = -(F1 * J22 - o.F2 * J12) * idet;
-    const double dt = -(J11 * o.F2 - J21 * F1) * idet;
+    const double iJ22 = rcp_fast(J22);
+    const double dt0 = -o.F2 * iJ22;
+    const double F1m = fma(0.5 * o.F2, dt0, F1);  // F1 - F2^2 / (2 J22)
+    const double den = fma(J21, dt0, J11);
+    const bool bad = !(J22 != 0.0) || !(den != 0.0);
+    double dth = -F1m * rcp_fast(den);
     dth = fmin(fmax(dth, -0.05), 0.05);
+    const double dt = fma(-J21 * iJ22, dth, dt0);
     T.th += dth;
     T.t += dt;
-    const bool conv = fmax(fabs(dth), fabs(dt)) <= TH_LAST;  // both Newton variables (t errs enter F1 squared)
+    const bool conv = fabs(dth) <= TH_LAST && fabs(dt) <= T_LAST;
     const bool good = J22 > 0.0 && ((J11 < 0.0) == ingress) && T.t > 0.0 && o.dX2 < R.Rs2;
     rotate(T.cs, T.sn, dth);
     T.st = bad ? -1 : (conv ? (good ? 1 : -1) : 0);
@@ -505,7 +517,7 @@ __device__ inline int cone_exists(const Roche& R, double Px, double Py, double P
 // WD-centre contact (initial guesses only).  Trig: one atan2 and one acos.
 __device__ inline bool element_interval_fast(const Roche& R, double Px, double Py, double Pz, double s,
                                              double c, double Rcal, double Reff, double& a, double& b,
-                                             bool* fallback = nullptr, int* nit = nullptr)
+                                             bool* fallback = nullptr, int* nit = nullptr, double* guess = nullptr)
 {
     // nit (diagnostic builds): iterations of the cone search, ingress and egress
     const double ux = 1.0 - Px, uy = -Py, uz = -Pz;
@@ -530,6 +542,7 @@ __device__ inline bool element_interval_fast(const Roche& R, double Px, double P
                 double co = cc * ce - sc * se, so = sc * ce + cc * se;
                 Tan In{thc - de, ci, si, s * (ux * ci - uy * si) + uz * c, 0};
                 Tan Out{thc + de, co, so, s * (ux * co - uy * so) + uz * c, 0};
+                if (guess) { guess[0] = In.th; guess[1] = Out.th; }  // diagnostic builds only
                 tangency_pair(R, Px, Py, Pz, s, c, In, Out, nit ? nit + 1 : nullptr);
                 const double Dm = (cosD <= -1.0) ? PI : acos(cosD);
                 if (In.st == 1 && Out.st == 1 && In.th < Out.th && In.th > thc - Dm && Out.th < thc + Dm) {

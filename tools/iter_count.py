@@ -46,4 +46,7 @@ for r, name in enumerate(("WD", "disc", "spot")):
     print("%-5s items %7d  iters/item cone %.2f in %.2f out %.2f | per-wave max cone %.2f in %.2f out %.2f"
           " | fallback %.4f eclipsed %.3f" % (name, n, C[0] / n, C[1] / n, C[2] / n, C[3] / waves, C[4] / waves,
                                               C[5] / waves, C[6] / n, C[8] / n))
+    h = C[10:16]
+    print("      initial-guess error (rad) <1e-4 %.3f <1e-3 %.3f <1e-2 %.3f <3e-2 %.3f <1e-1 %.3f more %.3f"
+          % tuple(h / max(h.sum(), 1)))
 print("status", np.bincount(st.cpu().numpy()))
