@@ -67,8 +67,8 @@ KERNELS = [("k_setup", 0, 1), ("k_elements", 1, 2), ("k_lnlike", 2, 3)]
 # walker ball): setup + stream + prior lanes, per element root (900
 # symmetry-unique roots per pair), and the direct-form accumulation per
 # element per point per sub-phase
-F_SETUP = 7555.0
-F_GEOM_ROOT = 1309.0
+F_SETUP = 1543.0
+F_GEOM_ROOT = 1109.0
 N_ROOTS = 900
 F_ACC_ECL, F_ACC_DON, F_POINT = 3.0, 6.0, 40.0
 N_ECL, N_DON = 1500, 400
@@ -291,13 +291,15 @@ def run(args):
             events.append((evs, q.shape[0]))
         ev.step_half(pos, lnp, half, a, seed, step, q, zfac, naccept, lnp_new=lnp_new, events=evs, spec=spec)
 
-    def timed_shard(pos, half, a, seed, step, lo, q, zfac, lnp_sh):
-        """the multi-rank path: this rank's lfg_stretch_step_shard with the events"""
+    def timed_shard(pos, half, a, seed, step, lo, q, zfac, lnp_sh, spec=False):
+        """the multi-rank path: this rank's lfg_stretch_step_shard(_spec) with the events"""
         evs = None
         if sampled():
             evs = make_evs()
             events.append((evs, lnp_sh.shape[0]))
-        ev.step_shard(pos, half, a, seed, step, lo, q, zfac, lnp_sh, events=evs)
+        ev.step_shard(pos, half, a, seed, step, lo, q, zfac, lnp_sh, events=evs, spec=spec)
+
+    timed_half.takes_spec = timed_shard.takes_spec = True
 
     def set_timing(on):
         if world == 1 and not args.shard_path:

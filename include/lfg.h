@@ -267,6 +267,35 @@ int lfg_stretch_step_shard(const double* pos, int W, int half, double a,
                            int lo, int n, double* q, double* zfac,
                            const lfg_tree* tree, double* lnp_new, void* ws,
                            size_t ws_bytes, void* stream, void* const* ev);
+
+/*
+ * The sharded half-step with the speculative setup of
+ * lfg_stretch_step_half_spec: this call's k_elements also forms the setup
+ * of walkers lo .. lo+n-1 of the next half for both fates of each partner
+ * (spec_out), and with spec_in the call skips k_setup and takes each pair's
+ * candidate by the acceptances lfg_stretch_accept_regen_spec recorded for the
+ * whole half.  spec_in = 1 is valid only right after lfg_stretch_step_shard_spec
+ * (other half, spec_out = 1, same lo / n / ensemble) and
+ * lfg_stretch_accept_regen_spec of that half on the same workspace, which must
+ * be sized for W/2 walkers (lfg_workspace_size_tree(W/2, tree)).
+ */
+int lfg_stretch_step_shard_spec(const double* pos, int W, int half, double a,
+                                unsigned long long seed, unsigned long long step,
+                                int lo, int n, double* q, double* zfac,
+                                const lfg_tree* tree, double* lnp_new,
+                                int spec_in, int spec_out, void* ws,
+                                size_t ws_bytes, void* stream, void* const* ev);
+
+/*
+ * lfg_stretch_accept_regen that also records each walker's acceptance in the
+ * workspace of the rank's lfg_stretch_step_shard_spec calls (n: their shard
+ * size), for the next half's candidate choice.
+ */
+int lfg_stretch_accept_regen_spec(double* pos, double* lnp, int W, int half,
+                                  double a, unsigned long long seed,
+                                  unsigned long long step, const double* lnp_new,
+                                  int* naccept, const lfg_tree* tree, int n,
+                                  void* ws, size_t ws_bytes, void* stream);
 int lfg_stretch_accept_regen(double* pos, double* lnp, int W, int ndim,
                              int half, double a, unsigned long long seed,
                              unsigned long long step, const double* lnp_new,

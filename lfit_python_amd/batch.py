@@ -271,18 +271,47 @@ class LnProbEvaluator:
         step_half)."""
         self._spec_key = None
 
-    def step_shard(self, pos, half, a, seed, step, lo, q, zfac, lnp_new, events=None):
+    def step_shard(self, pos, half, a, seed, step, lo, q, zfac, lnp_new, events=None, spec=False):
         """This rank's part of a sharded half-step (lfg_stretch_step_shard):
         the proposals of walkers lo .. lo + n - 1 of half `half` (n =
-        lnp_new.numel()) into q / zfac and their ln_prob into lnp_new."""
+        lnp_new.numel()) into q / zfac and their ln_prob into lnp_new.
+        spec=True (lfg_stretch_step_shard_spec): speculative setup as in
+        step_half; pair it with accept_regen() on this evaluator."""
         W, n = pos.shape[0], lnp_new.shape[0]
-        self._ensure(n)
-        self._spec_key = None
         vp = lambda t: ctypes.c_void_p(t.data_ptr())
-        rc = self.L.lfg_stretch_step_shard(vp(pos), W, half, a, seed, step, lo, n, vp(q), vp(zfac),
-                                           ctypes.byref(self.ctree), vp(lnp_new), vp(self._ws), self._ws.numel(),
-                                           _native.stream_ptr(self.device), events)
-        _native.check(rc, "lfg_stretch_step_shard")
+        if not spec:
+            self._ensure(n)
+            self._spec_key = None
+            rc = self.L.lfg_stretch_step_shard(vp(pos), W, half, a, seed, step, lo, n, vp(q), vp(zfac),
+                                               ctypes.byref(self.ctree), vp(lnp_new), vp(self._ws), self._ws.numel(),
+                                               _native.stream_ptr(self.device), events)
+            _native.check(rc, "lfg_stretch_step_shard")
+            return
+        gen = self.generation
+        self._ensure(W // 2)  # the acceptances of the whole half live here
+        ens = ("shard", W, pos.data_ptr(), q.data_ptr(), zfac.data_ptr(), seed, float(a), lo, n)
+        spec_in = gen == self.generation and self._spec_key == ens + (half, step, "accepted")
+        self._spec_key = None
+        rc = self.L.lfg_stretch_step_shard_spec(vp(pos), W, half, a, seed, step, lo, n, vp(q), vp(zfac),
+                                                ctypes.byref(self.ctree), vp(lnp_new), int(spec_in), 1, vp(self._ws),
+                                                self._ws.numel(), _native.stream_ptr(self.device), events)
+        _native.check(rc, "lfg_stretch_step_shard_spec")
+        self._spec_key = ens + (half, step, "pending")
+
+    def accept_regen(self, pos, lnp, half, a, seed, step, lnp_new, naccept, n):
+        """Metropolis step of the whole half after the gather
+        (lfg_stretch_accept_regen_spec), recording the acceptances for the
+        next step_shard(spec=True) of this rank (shard size n)."""
+        W = pos.shape[0]
+        self._ensure(W // 2)
+        key, self._spec_key = self._spec_key, None
+        vp = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
+        rc = self.L.lfg_stretch_accept_regen_spec(vp(pos), vp(lnp), W, half, a, seed, step, vp(lnp_new),
+                                                  vp(naccept), ctypes.byref(self.ctree), n, vp(self._ws),
+                                                  self._ws.numel(), _native.stream_ptr(self.device))
+        _native.check(rc, "lfg_stretch_accept_regen_spec")
+        if key is not None and key[-3:] == (half, step, "pending") and key[2] == pos.data_ptr() and key[8] == n:
+            self._spec_key = key[:-3] + (1 - half, step + half, "accepted")
 
     def ln_prior(self, walkers, out=None):
         """ln_prior alone (mcmcfit.ln_prior, mcmcfit.py:30-34) of walkers [W, ndim]."""

@@ -72,13 +72,14 @@ struct Ws {
     double* qC;     // [2][2][W][ndim]
     double* zfC;    // [2][2][W]
     int* jk;        // [2][W] the partner (in the other half) of walker w's proposal
-    int* accflag;   // [W] 1: walker w's move was accepted in the last half
+    int* accflag;   // [max(W, nacc)] 1: walker j of the last half accepted its move (a rank's
+                    // shard of W walkers needs every partner's: nacc = the half)
     size_t total;
 };
 
 inline size_t align256(size_t v) { return (v + 255) & ~size_t(255); }
 
-Ws carve(void* base, int W, int E, int gp_n = 0, int ndim_spec = 0)
+Ws carve(void* base, int W, int E, int gp_n = 0, int ndim_spec = 0, int nacc = 0)
 {
     const size_t pairs = size_t(W) * size_t(E);
     Ws ws{};
@@ -103,7 +104,7 @@ Ws carve(void* base, int W, int E, int gp_n = 0, int ndim_spec = 0)
         ws.qC = reinterpret_cast<double*>(take(4 * size_t(W) * ndim_spec * sizeof(double)));
         ws.zfC = reinterpret_cast<double*>(take(4 * size_t(W) * sizeof(double)));
         ws.jk = reinterpret_cast<int*>(take(2 * size_t(W) * sizeof(int)));
-        ws.accflag = reinterpret_cast<int*>(take(size_t(W) * sizeof(int)));
+        ws.accflag = reinterpret_cast<int*>(take(size_t(W > nacc ? W : nacc) * sizeof(int)));
     }
     ws.total = off;
     return ws;
@@ -1989,7 +1990,7 @@ __global__ void k_accept(double* __restrict__ pos, double* __restrict__ lnp, int
 // partner half is unchanged until this half is accepted
 __global__ void k_accept_regen(double* __restrict__ pos, double* __restrict__ lnp, int W, int ndim, int half,
                                double a, const double* __restrict__ lnp_new, unsigned long long seed,
-                               unsigned long long step, int* __restrict__ naccept)
+                               unsigned long long step, int* __restrict__ naccept, int* __restrict__ accflag)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int ns = W / 2;
@@ -2009,6 +2010,7 @@ __global__ void k_accept_regen(double* __restrict__ pos, double* __restrict__ ln
         lnp[w] = lnp_new[i];
         if (naccept) naccept[w] += 1;
     }
+    if (accflag) accflag[i] = (lu < diff) ? 1 : 0;  // the speculative setup's candidate choice
 }
 
 // ------------------------------------------------------ k_gp, k_wdphases
@@ -2202,8 +2204,8 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
                        const Propose* prop = nullptr, const SpecCtl* sp = nullptr)
 {
     if (W <= 0 || !T || T->E <= 0 || T->ndim <= 0 || T->nsub < 1 || !walkers || (!lnp && !acc)) return LFG_E_ARGS;
-    if (sp && (!prop || !acc || prop->lo != 0 || prop->ns != W)) return LFG_E_ARGS;
-    Ws ws = carve(wsp, W, T->E, T->gp ? T->max_n : 0, sp ? T->ndim : 0);
+    if (sp && (!prop || (acc && (prop->lo != 0 || prop->ns != W)))) return LFG_E_ARGS;
+    Ws ws = carve(wsp, W, T->E, T->gp ? T->max_n : 0, sp ? T->ndim : 0, prop ? prop->ns : 0);
     if (!wsp || ws_bytes < ws.total) return LFG_E_WORKSPACE;
     hipStream_t st = static_cast<hipStream_t>(stream);
     auto mark = [&](int i) {
@@ -2278,7 +2280,7 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
                T->ndim, acc ? acc->half : 0, acc ? acc->seed : 0ull, acc ? acc->step : 0ull,
                acc ? acc->naccept : nullptr};
     L.bstatus = ws.bstatus;
-    L.accflag = sp ? ws.accflag : nullptr;
+    L.accflag = (sp && acc) ? ws.accflag : nullptr;  // sharded: k_accept_regen records them
     if (T->gp) {
         L.res = ws.res;
         hipLaunchKernelGGL((k_lnlike<2, kFused>), dim3(npairs), dim3(LIKE_THREADS), 0, st, L);
@@ -2361,6 +2363,19 @@ int lfg_stretch_step_shard(const double* pos, int W, int half, double a, unsigne
     return lnprob_impl(q, n, T, lnp_new, nullptr, wsp, ws_bytes, stream, ev, nullptr, &prop);
 }
 
+int lfg_stretch_step_shard_spec(const double* pos, int W, int half, double a, unsigned long long seed,
+                                unsigned long long step, int lo, int n, double* q, double* zfac, const lfg_tree* T,
+                                double* lnp_new, int spec_in, int spec_out, void* wsp, size_t ws_bytes,
+                                void* stream, void* const* ev)
+{
+    if (W < 4 || (W & 1) || (half != 0 && half != 1) || !(a > 1.0) || !pos || !q || !zfac || !T || !lnp_new ||
+        n <= 0 || lo < 0 || lo + n > W / 2)
+        return LFG_E_ARGS;
+    const Propose prop{pos, a, q, zfac, half, seed, step, lo, W / 2};
+    const SpecCtl sp{spec_in != 0, spec_out != 0};
+    return lnprob_impl(q, n, T, lnp_new, nullptr, wsp, ws_bytes, stream, ev, nullptr, &prop, kFused ? nullptr : &sp);
+}
+
 int lfg_stretch_lnprob_accept(double* pos, double* lnp, int W, int half, const double* q, const double* zfac,
                               const lfg_tree* T, unsigned long long seed, unsigned long long step, int* naccept,
                               double* lnp_new, void* wsp, size_t ws_bytes, void* stream, void* const* ev)
@@ -2402,7 +2417,22 @@ int lfg_stretch_accept_regen(double* pos, double* lnp, int W, int ndim, int half
         return LFG_E_ARGS;
     const int ns = W / 2;
     hipLaunchKernelGGL(k_accept_regen, dim3((ns + 63) / 64), dim3(64), 0, static_cast<hipStream_t>(stream), pos,
-                       lnp, W, ndim, half, a, lnp_new, seed, step, naccept);
+                       lnp, W, ndim, half, a, lnp_new, seed, step, naccept, nullptr);
+    return launch_ok();
+}
+
+int lfg_stretch_accept_regen_spec(double* pos, double* lnp, int W, int half, double a, unsigned long long seed,
+                                  unsigned long long step, const double* lnp_new, int* naccept, const lfg_tree* T,
+                                  int n, void* wsp, size_t ws_bytes, void* stream)
+{
+    if (W < 4 || (W & 1) || (half != 0 && half != 1) || !(a > 1.0) || !pos || !lnp || !lnp_new || !T ||
+        T->ndim <= 0 || n <= 0 || n > W / 2)
+        return LFG_E_ARGS;
+    const Ws ws = carve(wsp, n, T->E, T->gp ? T->max_n : 0, T->ndim, W / 2);
+    if (!wsp || ws_bytes < ws.total) return LFG_E_WORKSPACE;
+    const int ns = W / 2;
+    hipLaunchKernelGGL(k_accept_regen, dim3((ns + 63) / 64), dim3(64), 0, static_cast<hipStream_t>(stream), pos,
+                       lnp, W, T->ndim, half, a, lnp_new, seed, step, naccept, ws.accflag);
     return launch_ok();
 }
 

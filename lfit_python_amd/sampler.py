@@ -259,7 +259,9 @@ class EnsembleSampler:
         for half in (0, 1):
             if self.world == 1 and self.fuse and self.timer is None and not self.force_shard:
                 f = self.half_timer or self.ev.step_half
-                kw = dict(spec=True) if self.spec else {}
+                # a replacement step_half (bench timing, tests) takes spec only if it says so
+                kw = dict(spec=True) if self.spec and (self.half_timer is None or
+                                                       getattr(self.half_timer, "takes_spec", False)) else {}
                 f(self.pos, self.lnp, half, self.a, self.seed, self.rng_step, self.q, self.zfac, self.naccept,
                   lnp_new=self.lnp_new, **kw)
                 continue
@@ -286,14 +288,20 @@ class EnsembleSampler:
             self._zf_sh = torch.empty(self.shard, **f64)
             self._lnp_sh = torch.empty(self.shard, **f64)
         f = self.shard_timer or self.ev.step_shard
+        spec = self.spec and hasattr(self.ev, "accept_regen") and (
+            self.shard_timer is None or getattr(self.shard_timer, "takes_spec", False))
         f(self.pos, half, self.a, self.seed, self.rng_step, self.rank * self.shard, self._q_sh, self._zf_sh,
-          self._lnp_sh)
+          self._lnp_sh, **(dict(spec=True) if spec else {}))
         if self.world > 1 or self.force_exchange:
             self._gather(self.lnp_new, self._lnp_sh)
         else:
             self.lnp_new.copy_(self._lnp_sh)
-        self.ops.accept_regen(self.pos, self.lnp, half, self.a, self.lnp_new, self.seed, self.rng_step,
-                              self.naccept)
+        if spec:  # records the acceptances for the next half's speculative setup
+            self.ev.accept_regen(self.pos, self.lnp, half, self.a, self.seed, self.rng_step, self.lnp_new,
+                                 self.naccept, self.shard)
+        else:
+            self.ops.accept_regen(self.pos, self.lnp, half, self.a, self.lnp_new, self.seed, self.rng_step,
+                                  self.naccept)
 
     def close(self):
         """Release the direct RCCL communicator (every rank, before the

@@ -145,10 +145,10 @@ def test_fused_half_step_matches_separate_kernels():
         init = sampler.initialise_walkers(p0, sampler.comp_scatter(m.dynasty_par_names, 0.1), W,
                                           lambda p: ev(torch.as_tensor(p, device="cuda")).cpu().numpy())
         res = []
-        for mode in ("separate", "spec", "step_half", "lnprob_accept", "shard1", "shard2"):
+        for mode in ("separate", "spec", "step_half", "lnprob_accept", "shard1", "shard1_spec", "shard2"):
             S = sampler.EnsembleSampler(W, t.ndim, ev, seed=21)
             S.fuse = mode in ("spec", "step_half", "lnprob_accept")
-            S.spec = mode == "spec"
+            S.spec = mode in ("spec", "shard1_spec")
             S.force_shard = mode.startswith("shard")
             if mode == "shard2":
                 # two ranks' shards of each half (lfg_stretch_step_shard with

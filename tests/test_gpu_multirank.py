@@ -1,0 +1,71 @@
+"""GPU: the multi-rank sampler path (walker shards, one all_gather of ln_prob
+per half-step, lfg_stretch_step_shard(_spec) + lfg_stretch_accept_regen(_spec))
+with two real ranks sharing cuda:0 over gloo, against the single-rank fused
+chain.  The reference's analogue is the pool.map fan-out of mcmcfit.py:273-288;
+the chains must be bit-identical whatever the rank count."""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _flux_fn(p, x, w, nsub):
+    from lfit_python_amd.lfit import flux_batch
+    f, st = flux_batch(np.asarray(p)[None, :], x, w, nsub=nsub)
+    return f[0].cpu().numpy()
+
+
+def _init(W):
+    from lfit_python_amd import synthetic
+    m = synthetic.config_single(300, flux_fn=None)
+    p0 = np.array(m.dynasty_par_vals)
+    rng = np.random.default_rng(17)
+    return p0 * (1.0 + 1e-3 * rng.standard_normal((W, p0.size)))
+
+
+def _chain(spec, world=1, rank=0):
+    import torch
+    from lfit_python_amd import batch, sampler, synthetic
+    m = synthetic.config_single(300, flux_fn=_flux_fn)
+    t = batch.compile_tree(m)
+    ev = batch.LnProbEvaluator(t, device=torch.device("cuda", 0))
+    W = 64
+    S = sampler.EnsembleSampler(W, t.ndim, ev, seed=23)
+    S.spec = spec
+    S.run_mcmc(_init(W), 4)
+    out = (S.chain.cpu().numpy(), S.lnprob_chain.cpu().numpy(), S.naccept.cpu().numpy())
+    S.close()
+    return out
+
+
+def _rank_main(rank, world, port, path, spec):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ch, lc, na = _chain(spec, world, rank)
+        np.savez(path % rank, chain=ch, lnp=lc, nacc=na)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("spec", [True, False])
+def test_two_ranks_match_one(spec):
+    import torch.multiprocessing as mp
+    ref = _chain(True)
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "rank%d.npz")
+        mp.spawn(_rank_main, args=(2, port, path, spec), nprocs=2, join=True)
+        for r in range(2):
+            got = np.load(path % r)
+            np.testing.assert_array_equal(got["chain"], ref[0])
+            np.testing.assert_array_equal(got["lnp"], ref[1])
+            np.testing.assert_array_equal(got["nacc"], ref[2])

@@ -65,6 +65,16 @@ def walkers(config, n, seed=20261015):
     return tree, init
 
 
+def prior_sum_flops(types, chunk=16):
+    """Prior.ln_prob sum of a prior lane from the tree's constants
+    (lfg_tree.prior_c; lfg.hip prior_lane): per parameter gauss
+    (v - p1) c1 and fma(-z/2, z, c0) = 5, plus the running add; log_uniform
+    one product multiply, mod_jeff also v + p1; per chunk one log and one sub."""
+    per = {0: 6, 1: 6, 2: 1, 3: 2, 4: 3}
+    n = len(types)
+    return float(sum(per.get(int(t), 1) for t in types) + 2 * ((n + chunk - 1) // chunk))
+
+
 def cv_pars(tree, walk, e):
     g = tree.gather[e]
     return np.array([[w[k] if k >= 0 else tree.consts[-1 - k] for k in g] for w in walk])
@@ -87,8 +97,7 @@ def main():
                 rows.append(out.copy())
     R = np.array(rows, dtype=np.float64)
     m = R.mean(0)
-    prior = np.mean([sum(lib.lfc_count_prior(int(t), a, b, nrm, v) for t, a, b, nrm, v in
-                         zip(tree.prior_type, tree.prior_p1, tree.prior_p2, tree.prior_norm, w)) for w in walk])
+    prior = prior_sum_flops(tree.prior_type)
     unit = np.zeros(8, np.int64)
     lib.lfc_unit_counts(unit.ctypes.data)
     E = tree.E

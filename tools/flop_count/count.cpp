@@ -5,6 +5,8 @@
 // and k_elements (lfg.hip) are restated around them, so the counts are those
 // of the kernels' own arithmetic, iteration by iteration, on given parameter
 // sets.  Built and driven by tools/flop_count.py; tooling only.
+#include <algorithm>
+
 #include "flop.hpp"
 #define double F64
 #include "lfg_device.hpp"
@@ -50,47 +52,54 @@ int lfc_count_pair(const double* pin, int np, long long* out)
     {
         F64 s, c;
         sincos(inc * DEG, &s, &c);
-        const F64 a1 = p[14], a2 = p[15];
-        const F64 upk = pow(a1 / a2, 1.0 / a2);
-        const F64 lnpk = a1 * log(upk) - pow(upk, a2);
         const F64 tilt = p[16] * DEG, psi = (p[10] - 90.0 + p[17]) * DEG;
         F64 st_, ct_, sp_, cp_, saz, caz;
         sincos(tilt, &st_, &ct_);
         sincos(psi, &sp_, &cp_);
         const F64 nmax = fabs(st_) * s + ct_ * c;
         sincos(p[10] * DEG, &saz, &caz);
-        const F64 umax = bs_umax(a1, a2, lnpk);
         const F64 bden = p[11] + (1.0 - p[11]) * fmax(nmax, 0.0);
         const F64 sce = s * cos(PI * p[5]);
         const F64 rcal = sqrt(1.0 - sce * sce);
         const F64 reff = eggleton(R.q);
         const F64 nb0 = st_ * cp_, nb1 = st_ * sp_;
-        (void)umax; (void)bden; (void)rcal; (void)reff; (void)nb0; (void)nb1;
+        (void)bden; (void)rcal; (void)reff; (void)nb0; (void)nb1;
     }
     out[0] = since(c0);
     out[1] = trans_since(c0);
 
-    // ---- k_setup stream lane
+    // ---- k_setup stream lane: the stream table (MODEL_SPEC 4.5), the
+    // azimuth prior's angle and the strip shape (MODEL_SPEC 5.3)
     c0 = snap();
     Roche Rb;
-    roche_init(Rb, p[4]);
+    QPatch qp;
+    roche_init(Rb, p[4], &qp);
     F64 bs[4];
-    if (bspot(Rb, p[6] * Rb.xl1, bs) != ST_OK) return 3;
+    if (bspot<false>(Rb, p[6] * Rb.xl1, bs, &qp) != ST_OK) return 3;
     {
         F64 alpha = atan2(bs[1], bs[0]) / DEG;
-        (void)alpha;
+        const F64 a1 = p[14], a2 = p[15];
+        const F64 upk = pow(a1 / a2, 1.0 / a2);
+        const F64 lnpk = a1 * log(upk) - pow(upk, a2);
+        const F64 umax = bs_umax(a1, a2, lnpk);
+        (void)alpha; (void)umax;
     }
     out[2] = since(c0);
     out[3] = trans_since(c0);
 
-    // ---- k_setup prior lane (LCModel findphi(q, 90) prior; Prior sums are
-    // counted per parameter by the caller)
+    // ---- k_setup prior lane: the LCModel dphi prior from the findphi(q, 90)
+    // series (Prior sums are counted per parameter by the caller)
     c0 = snap();
     {
-        Roche Rp;
-        roche_init(Rp, p[4]);
-        F64 maxphi;
-        findphi_fast(Rp, 90.0, maxphi);
+        const QPatch pq = q_patch(p[4]);
+        F64 maxphi = pq.iq >= 0 ? q_series(kStPhi90, pq) : F64(0.0);
+        if (pq.iq < 0) {
+            Roche Rp;
+            roche_init(Rp, p[4]);
+            findphi_fast(Rp, 90.0, maxphi);
+        }
+        const F64 lim = maxphi - DPHI_TOL;
+        (void)lim;
     }
     out[4] = since(c0);
     out[5] = trans_since(c0);

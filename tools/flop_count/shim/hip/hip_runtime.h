@@ -9,3 +9,5 @@
 #define __noinline__
 #define __builtin_amdgcn_rsq(x) lfg_rsq(x)
 #define __builtin_amdgcn_rcp(x) lfg_rcp(x)
+using std::max;  // integer min/max of the device code (HIP provides them on the device; count.cpp includes <algorithm> first)
+using std::min;
