@@ -891,7 +891,7 @@ __device__ inline void combine_walker(const LikeArgs& L, int w)
 // eclipse per walker and fused acceptance, thread 0 decides with the
 // prefetched draw and the copy of the accepted proposal is spread over the
 // first ndim lanes; otherwise thread 0 runs combine_after
-__device__ inline void finish_walker(const LikeArgs& L, int pair, int tid, bool acc1, double aq,
+__device__ inline void finish_walker(const LikeArgs& L, int pair, int tid, bool acc1, const double* sq,
                                      const double* sacc1, int* sflag);
 
 __device__ inline void combine_after(const LikeArgs& L, int pair)
@@ -921,6 +921,7 @@ __device__ inline void combine_after(const LikeArgs& L, int pair)
 // w |[a,b] n [lo,hi]| / (hi - lo) directly.  Sums are 2^-61 fixed point in
 // int64 so LDS atomics add them exactly, independent of order.
 constexpr int LIKE_THREADS = 512;
+constexpr int ACC_LDS = 32;  // proposal coordinates of the fused acceptance kept in LDS (the rest re-read)
 #ifndef LIKE_MINW
 #define LIKE_MINW 4  // minimum waves per SIMD: two 512-lane blocks per CU (<= 128 VGPRs; LDS < 80 KB)
 #endif
@@ -1391,7 +1392,7 @@ __device__ __forceinline__ int windows_unsorted(const LikeArgs& L, int o0, int n
 #define LIKE_STAMP(i)
 #endif
 
-__device__ inline void finish_walker(const LikeArgs& L, int pair, int tid, bool acc1, double aq,
+__device__ inline void finish_walker(const LikeArgs& L, int pair, int tid, bool acc1, const double* sq,
                                      const double* sacc1, int* sflag)
 {
     if (!acc1) {
@@ -1420,7 +1421,8 @@ __device__ inline void finish_walker(const LikeArgs& L, int pair, int tid, bool 
         if (L.accflag) L.accflag[pair] = a ? 1 : 0;
     }
     __syncthreads();
-    if (sflag[0] && tid < L.ndim) L.pos[size_t(wg) * L.ndim + tid] = aq;
+    if (sflag[0] && tid < L.ndim)
+        L.pos[size_t(wg) * L.ndim + tid] = (tid < ACC_LDS) ? sq[tid] : L.qprop[size_t(pair) * L.ndim + tid];
 }
 
 // MODE 0: flux (and components) only; 1: fused chi^2 -> ln_like; 2: GP
@@ -1473,8 +1475,10 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
     // (one per lane), the uniform draw and the old ln_prob are fetched here,
     // off the tail of the block (combine_walker does it for E > 1)
     const bool acc1 = CHI && !GP && L.pos && L.E == 1;
-    double aq = 0.0;
-    if (acc1 && tid < L.ndim) aq = L.qprop[size_t(pair) * L.ndim + tid];
+    // the proposal's coordinates wait in LDS (a register held through the
+    // whole block would be spilled: the kernel is at its 128-VGPR budget)
+    __shared__ double sq[ACC_LDS];
+    if (acc1 && tid < L.ndim && tid < ACC_LDS) sq[tid] = L.qprop[size_t(pair) * L.ndim + tid];
     int st;
     double s, c, ul, td;
     double px = 0.0, pw = 0.0;  // tile-0 point of this thread (y, ye: read where chi^2 is formed)
@@ -1578,7 +1582,7 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
         }
         if (CHI && !GP) {  // GP trees: k_gp_like sees the status and finishes the pair
             if (tid == 0) L.lle[pair] = -INFINITY;
-            finish_walker(L, pair, tid, acc1, aq, sacc1, sflag);
+            finish_walker(L, pair, tid, acc1, sq, sacc1, sflag);
         }
         return;
     }
@@ -1756,7 +1760,7 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
             for (int i = 0; i < nw; ++i) tot += red[0][i];
             L.lle[pair] = -0.5 * tot;
         }
-        finish_walker(L, pair, tid, acc1, aq, sacc1, sflag);
+        finish_walker(L, pair, tid, acc1, sq, sacc1, sflag);
     }
 }
 

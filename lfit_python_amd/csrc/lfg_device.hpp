@@ -530,7 +530,22 @@ __device__ inline bool element_interval_fast(const Roche& R, double Px, double P
         // theta_c = atan2(-uy, ux): closest approach of the line of sight to D
         const double cc = ux * iuxy, sc = -uy * iuxy;
         const double tc = s * uxy + uz * c;
-        const int ex = cone_exists(R, Px, Py, Pz, s, c, cc, sc, tc, nit);
+        // the closest approach to D inside the lobe decides at once (one
+        // potential, no gradient or Hessian); otherwise the cone search
+        int ex;
+        {
+            const double ex0 = s * cc, ey0 = -s * sc;
+            const double x = fma(tc, ex0, Px), y = fma(tc, ey0, Py), z = fma(tc, c, Pz);
+            const double dx = x - 1.0, xm = x - R.mu;
+            const double r2s = dx * dx + y * y + z * z;
+            const double phi = -R.cA * rsqrt_pos(x * x + y * y + z * z) - R.cB * rsqrt_pos(r2s) - xm * xm - y * y;
+            if (phi < R.pl1 && r2s < R.Rs2) {
+                ex = 1;
+                if (nit) ++nit[0];  // diagnostic builds: one cone step
+            } else {
+                ex = cone_exists(R, Px, Py, Pz, s, c, cc, sc, tc, nit);
+            }
+        }
         if (ex == 0) { a = 1.0; b = -1.0; return false; }
         if (ex == 1) {
             const double ce = (sqrt(fmax(uu - Rcal * Rcal, 0.0)) - c * uz) * iuxy / s;
@@ -544,8 +559,12 @@ __device__ inline bool element_interval_fast(const Roche& R, double Px, double P
                 Tan Out{thc + de, co, so, s * (ux * co - uy * so) + uz * c, 0};
                 if (guess) { guess[0] = In.th; guess[1] = Out.th; }  // diagnostic builds only
                 tangency_pair(R, Px, Py, Pz, s, c, In, Out, nit ? nit + 1 : nullptr);
-                const double Dm = (cosD <= -1.0) ? PI : acos(cosD);
-                if (In.st == 1 && Out.st == 1 && In.th < Out.th && In.th > thc - Dm && Out.th < thc + Dm) {
+                // both contacts within Dm of thc (where the ray meets the
+                // donor's sphere), tested as cos(th - thc) > cos Dm with the
+                // rotated cosines: no acos; the steps are clamped to 0.05 rad
+                // and the solve is short, so |th - thc| stays far below pi
+                const double cin = In.cs * cc + In.sn * sc, cout = Out.cs * cc + Out.sn * sc;
+                if (In.st == 1 && Out.st == 1 && In.th < Out.th && cin > cosD && cout > cosD) {
                     a = In.th * (1.0 / TWO_PI);
                     b = Out.th * (1.0 / TWO_PI);
                     return true;
