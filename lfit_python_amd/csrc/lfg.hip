@@ -603,7 +603,23 @@ __global__ __launch_bounds__(ELEM_BLOCK) __attribute__((amdgpu_waves_per_eu(ELEM
         st0 = status[pair];
         bst = bstatus[pair];
     }
-    if (v >= NUNIQ) return;
+    if (v >= NUNIQ) {
+        // the last chunk's spare lanes: the disc ring weights (MODEL_SPEC
+        // 5.2).  Lane NUNIQ + i holds the boundary term P(r_i), i = 0..NDISC_R;
+        // ring i's weight is the difference of neighbours: one pow per lane
+        // of one wave, instead of two in a ring-start lane of every disc wave
+        const int rb = v - NUNIQ;
+        if (rb > NDISC_R || st0 != ST_OK) return;
+        const double P = disc_boundary(rb, G);
+        const int lane = int(threadIdx.x) & 63, l0 = lane - rb;  // lane of P(r_0)
+        const double Pn = __shfl(P, min(lane + 1, l0 + NDISC_R), 64);
+        const double Pt = __shfl(P, l0 + NDISC_R, 64);
+        double* Wp = WT + size_t(pair) * WT_N;
+        if (rb < NDISC_R) Wp[WT_DISC + rb] = (TWO_PI / NDISC_AZ) * (Pn - P);
+        if (rb == 0) Wp[WT_TD] = TWO_PI * (Pt - P);
+        return;
+    }
+    static_assert((NUNIQ % ELEM_BLOCK) + NDISC_R + 1 <= ELEM_BLOCK, "ring-weight lanes fit in the last chunk");
 #ifndef LFG_EXP_OLDORDER
     // launch order WD, disc, spot, donor: the last chunk, dispatched last,
     // holds the cheap donor items (one 1-D root) instead of spot tangencies
@@ -685,11 +701,6 @@ __global__ __launch_bounds__(ELEM_BLOCK) __attribute__((amdgpu_waves_per_eu(ELEM
         km = NWD + ir * NDISC_AZ + NDISC_AZ - 1 - j;
         const double rin = G[G_RWD];
         const double rc = rin + (ir + 0.5) * ((G[G_RDISC] - rin) / NDISC_R);
-        if (j == 0) {
-            double* Wp = WT + size_t(pair) * WT_N;
-            Wp[WT_DISC + ir] = disc_ring_weight(ir, G);
-            if (ir == 0) Wp[WT_TD] = TWO_PI * (disc_boundary(NDISC_R, G) - disc_boundary(0, G));
-        }
         Px = rc * kDiscCos[j];
         Py = rc * kDiscSin[j];
         Pz = 0.0;
@@ -1105,12 +1116,29 @@ __device__ __forceinline__ int sweep_ring(int k)
     return r;
 }
 
+// v of the lane CTRL's DPP pattern names (0 where the source lane is outside
+// the row or the row is not in RM): two 32-bit DPP moves, no LDS round trip
+template <int CTRL, int RM>
+__device__ __forceinline__ long long dpp64(long long v)
+{
+    const int lo = __builtin_amdgcn_update_dpp(0, static_cast<int>(v), CTRL, RM, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, static_cast<int>(v >> 32), CTRL, RM, 0xf, false);
+    return (static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo);
+}
+
+// inclusive wave prefix sum: Hillis-Steele within each row of 16 lanes
+// (row_shr 1, 2, 4, 8), then row_bcast:15 into rows 1 and 3 and
+// row_bcast:31 into rows 2 and 3 (gfx9 DPP).  Six dependent VALU steps; the
+// ds_bpermute form waited an LDS round trip per step.
 __device__ __forceinline__ long long wave_scan_incl(long long v, int lane)
 {
-    for (int off = 1; off < 64; off <<= 1) {
-        const long long u = bperm64((lane_id_here() - off) << 2, v);  // lanes below off: ignored
-        if (lane >= off) v += u;
-    }
+    (void)lane;
+    v += dpp64<0x111, 0xf>(v);
+    v += dpp64<0x112, 0xf>(v);
+    v += dpp64<0x114, 0xf>(v);
+    v += dpp64<0x118, 0xf>(v);
+    v += dpp64<0x142, 0xa>(v);
+    v += dpp64<0x143, 0xc>(v);
     return v;
 }
 
@@ -1388,8 +1416,14 @@ __device__ __forceinline__ int windows_unsorted(const LikeArgs& L, int o0, int n
 #ifdef LFG_PROFILE_LIKE  // diagnostic build only: phase stamps (first tile) into spare geo slots 41..46
 #define LIKE_STAMP(i)                                                                                       \
     if (tid == 0 && t0 == 0) const_cast<double*>(G)[41 + (i)] = double(__builtin_amdgcn_s_memtime() - tstart)
+// prologue stamps of thread 0 (and of the block's last lane) per block: lfg_debug_like_cycles
+__device__ unsigned long long g_like_cyc[8][4096];
+#define LIKE_PRO(k)                                                                                 \
+    if ((tid == 0 || tid == LIKE_THREADS - 1) && blockIdx.x < 4096)                                  \
+        g_like_cyc[(k) + (tid ? 4 : 0)][blockIdx.x] = __builtin_amdgcn_s_memtime() - tstart
 #else
 #define LIKE_STAMP(i)
+#define LIKE_PRO(k)
 #endif
 
 __device__ inline void finish_walker(const LikeArgs& L, int pair, int tid, bool acc1, const double* sq,
@@ -1574,6 +1608,7 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
         sacc1[2] = L.lnp_ens[L.half * L.npairs + pair];
     }
 
+    LIKE_PRO(0);
     if (st != ST_OK) {
         for (int p = tid; p < n; p += nt) {
             if (L.flux) L.flux[size_t(pair) * n + p] = NAN;
@@ -1609,14 +1644,27 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
     dn = wave_sum(dn);
     vs = wave_sum(vs);
     if (lane == 0) { red[0][wv] = tb; red[1][wv] = dn; red[2][wv] = vs; }
+    LIKE_PRO(1);
     __syncthreads();
-    if (tid == 0) {  // block-uniform normalisers live in LDS (read at use: no registers held)
-        tb = dn = vs = 0.0;
-        for (int i = 0; i < nw; ++i) { tb += red[0][i]; dn += red[1][i]; vs += red[2][i]; }
-        snorm[0] = 1.0 / tb;
-        snorm[1] = 1.0 / vs;
-        snorm[2] = dn;
-        snorm[3] = vs;
+    LIKE_PRO(2);
+    if (wv == 0) {  // block-uniform normalisers live in LDS (read at use: no registers held)
+        // the nw wave partials: lanes 0..nw-1 read them at once and a
+        // 3-step xor butterfly sums them (a serial loop in one lane waited
+        // on every LDS read in turn)
+        double p0 = 0.0, p1 = 0.0, p2 = 0.0;
+        if (lane < nw) { p0 = red[0][lane]; p1 = red[1][lane]; p2 = red[2][lane]; }
+        static_assert(nw == 8, "partials butterfly");
+        for (int off = 4; off > 0; off >>= 1) {
+            p0 += __longlong_as_double(bperm64((lane_id_here() ^ off) << 2, __double_as_longlong(p0)));
+            p1 += __longlong_as_double(bperm64((lane_id_here() ^ off) << 2, __double_as_longlong(p1)));
+            p2 += __longlong_as_double(bperm64((lane_id_here() ^ off) << 2, __double_as_longlong(p2)));
+        }
+        if (lane == 0) {
+            snorm[0] = 1.0 / p0;
+            snorm[1] = 1.0 / p2;
+            snorm[2] = p1;
+            snorm[3] = p2;
+        }
     }
     const double twd = TWO_PI * ((1.0 - ul) * 0.5 + ul / 3.0);  // 2 pi [F(1) - F(0)]
     if (tid >= NBS && tid < NBS + NWD_RINGS + NDISC_R)  // visible to the sweep after the pass barrier
@@ -1645,8 +1693,11 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
         for (int j = 0; j < S; ++j) {
             const double ph = wrap_phase(ph0 - wk + (2 * j + 1) * h);
             if (tid == 0) { sflag[0] = 0; sflag[1] = 0; }
+            // S = 1: the sub-bin window is the point's own window (ph = phc,
+            // h = wk), so the spot sweep reuses TA's windows and cells
+            const bool one = S == 1;
             int flA = (j == 0) ? put_window(TA, tid, own, phc, wk) : 0;
-            int flB = put_window(TB, tid, own, ph, h);
+            int flB = one ? 0 : put_window(TB, tid, own, ph, h);
             if (own) sph[tid] = ph;
             for (int i = (j == 0) ? 0 : 2; i < 6; ++i) sacc[i][tid] = 0ull;
             if (tid == 0)
@@ -1657,9 +1708,9 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
                 if (flA) atomicOr(&sflag[0], flA);
                 build_cells(TA.lo, m, TA.cell, tid);
             }
-            flB |= check_sorted(TB, tid, own) | ((own && tid && sph[tid] < sph[tid - 1]) ? 4 : 0);
+            flB |= (one ? flA : check_sorted(TB, tid, own)) | ((own && tid && sph[tid] < sph[tid - 1]) ? 4 : 0);
             if (flB) atomicOr(&sflag[1], flB);
-            build_cells(TB.lo, m, TB.cell, tid);
+            if (!one) build_cells(TB.lo, m, TB.cell, tid);
             build_cells(sph, m, scp, tid);
             __syncthreads();
             const bool swA = (j == 0) && sflag[0] == 0, swB = sflag[1] == 0;  // sweep, else direct
@@ -1685,8 +1736,13 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
             }
             LIKE_STAMP(2);
             if (swB) {
-                const PhaseIndex XW = phase_index(TB.lo, TB.cell, m), XP = phase_index(sph, scp, m);
-                sweep_spot_donor(tid, XW, TB, XP, sab, sbw, snorm[0], sdq, snorm[1], sacc + 2);
+                const PhaseIndex XP = phase_index(sph, scp, m);
+                if (one)
+                    sweep_spot_donor(tid, phase_index(TA.lo, TA.cell, m), TA, XP, sab, sbw, snorm[0], sdq, snorm[1],
+                                     sacc + 2);
+                else
+                    sweep_spot_donor(tid, phase_index(TB.lo, TB.cell, m), TB, XP, sab, sbw, snorm[0], sdq, snorm[1],
+                                     sacc + 2);
             }
             __syncthreads();
             LIKE_STAMP(3);
@@ -2543,6 +2599,14 @@ int lfg_gp_lnlike(const double* x, const double* ye, const double* res, int W, i
                        lnlike);
     return launch_ok();
 }
+
+#ifdef LFG_PROFILE_LIKE
+// diagnostic build only: k_lnlike prologue stamps
+int lfg_debug_like_cycles(unsigned long long* host)
+{
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_like_cyc), sizeof(g_like_cyc)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 #ifdef LFG_PROFILE_SETUP
 // diagnostic build only: copy the k_setup lane stamps to the host

@@ -789,6 +789,7 @@ __device__ inline int bspot_rk4(const Roche& R, double rad, double out[4])
     StreamState s = stream_start(R);
     double r2c = s.x * s.x + s.y * s.y;
     const double rad2 = rad * rad;
+    if (!(rad2 < r2c)) return ST_BAD_STREAM;  // the stream starts inside rad (as the table path)
     for (int n = 0; n < STREAM_MAXSTEP_FINE; ++n) {
         // r^(3/2) = r2 (r2 (r2)^(-1/2))^(-1/2): two v_rsq steps
         const double r32 = r2c * rsqrt_pos(r2c * rsqrt_pos(r2c));

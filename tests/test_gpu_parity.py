@@ -36,6 +36,40 @@ def test_roche_primitives(oracle):
             np.testing.assert_allclose(roche.bspot(q, rad), oracle.bspot(q, rad), rtol=1e-9, atol=1e-11)
 
 
+def test_stream_table_matches_oracle(oracle):
+    """bspot over the stream table's whole domain (MODEL_SPEC 4.5): random
+    (q, s) with s near periastron and toward the start point, and q outside
+    the table (the fine RK4).  Kernels and oracle evaluate the same
+    coefficients, so they agree to rounding."""
+    from lfit_python_amd import roche
+    rng = np.random.default_rng(31)
+    qs = np.concatenate([np.exp(rng.uniform(np.log(0.002), np.log(5.0), 24)), [0.0015, 6.0]])
+    for q in qs:
+        x1 = oracle.xl1(q)
+        grid = x1 * np.arange(1, 400) / 400.0
+        ok = []
+        for r in grid:
+            try:
+                oracle.bspot(q, r)
+                ok.append(r)
+            except ValueError:
+                pass
+        assert ok, q
+        r_lo, r_hi = min(ok), max(ok)  # within a grid step of r_min and r0
+        rads = np.concatenate([r_lo + (r_hi - r_lo) * np.array([0.0, 1e-4, 0.01, 0.3, 0.7, 0.99, 1.0]),
+                               [0.5 * r_lo, r_hi + 0.5 * (x1 - r_hi)]])
+        for rad in rads:
+            try:
+                ref = oracle.bspot(q, rad)
+            except ValueError:
+                with pytest.raises(roche.RocheError):
+                    roche.bspot(q, rad)
+                continue
+            got = roche.bspot(q, rad)
+            np.testing.assert_allclose(got[:2], ref[:2], rtol=0, atol=1e-12)
+            np.testing.assert_allclose(got[2:], ref[2:], rtol=0, atol=1e-10)
+
+
 def test_roche_errors():
     from lfit_python_amd import roche
     with pytest.raises(roche.RocheError):

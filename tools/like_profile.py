@@ -48,3 +48,8 @@ sh = (hw >> 12) & 1
 se = (hw >> 13) & 0x7
 key = se * 32 + sh * 16 + cu
 print('distinct (se, sh, cu) slots in use: %d of %d blocks' % (len(np.unique(key)), len(key)))
+cyc = np.zeros((8, 4096), dtype=np.uint64)
+L.lfg_debug_like_cycles(ctypes.c_void_p(cyc.ctypes.data))
+cyc = cyc[:, :W].astype(np.float64)[:, ok]
+for k, nm in enumerate(['status known', 'wave sums (before barrier)', 'after the barrier']):
+    print('prologue %-28s thread 0 mean %7.0f | last lane mean %7.0f' % (nm, cyc[k].mean(), cyc[4 + k].mean()))
