@@ -213,6 +213,11 @@ def pmc_row(kernel):
 
 
 def run(args):
+    # stdout carries exactly one JSON line: libraries that print to stdout
+    # (RCCL's version banner at communicator init) are sent to stderr
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -460,7 +465,7 @@ def run(args):
             "acceptance_fraction": acc,
             "cpu_baseline": cpu,
         }
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=json_out, flush=True)
     S.close()
     if dist:
         dist.destroy_process_group()
