@@ -36,14 +36,27 @@ constexpr int ELEM_BLOCK = LFG_ELEM_BLOCK;
 // per-pair weight block written by k_elements: disc ring weights, the disc
 // total 2 pi [P(rdisc) - P(rin)], spot element weights
 constexpr int WT_DISC = 0, WT_TD = NDISC_R, WT_BS = 24, WT_N = WT_BS + NBS;
-// WD/disc eclipse intervals are stored in sweep order: slot g of a pair's
-// interval table holds element sweep_item(g) (stride-37 permutation: a wave's
-// 64 lanes sweep elements of different rings, so their LDS atomics spread),
-// and k_lnlike reads its items as coalesced rows; slot_of inverts it
-// (37 * 1173 = 1 mod 1400).  Spot elements keep their own slots.
-__device__ __forceinline__ int sweep_item(int g) { return g < NWD + NDISC ? (g * 37) % (NWD + NDISC) : g; }
-__device__ __forceinline__ int slot_of(int k) { return k < NWD + NDISC ? (k * 1173) % (NWD + NDISC) : k; }
-static_assert(NWD + NDISC == 1400 && (37 * 1173) % 1400 == 1, "sweep permutation inverse");
+// Eclipse intervals are stored once per mirror pair (MODEL_SPEC 5: the
+// mirrored element's interval is [-b, -a]): NU_WDD symmetry-unique WD/disc
+// items, then the NBS spot elements, NELU (a, b) pairs per pair in all.  The
+// WD/disc slots are in sweep order: slot g holds unique item uitem(g), a
+// stride-37 permutation (a wave's lanes sweep items of different rings and
+// azimuths, so their LDS atomics spread), and k_lnlike's sweep element g in
+// [0, NWD + NDISC) is slot g mod NU_WDD, mirrored for g >= NU_WDD: it reads
+// its items as coalesced rows, half the bytes of a table of every element.
+constexpr int NU_WDD = (NWD + NDISC) / 2, NELU = NU_WDD + NBS;
+__device__ __forceinline__ int uitem(int g) { return (g * 37) % NU_WDD; }
+__device__ __forceinline__ int uslot(int u) { return (u * 473) % NU_WDD; }
+static_assert(NU_WDD == 700 && (37 * 473) % 700 == 1, "sweep permutation inverse");
+__device__ __forceinline__ double2 mirror_ab(double2 ab)
+{
+    return (ab.x < ab.y) ? make_double2(-ab.y, -ab.x) : make_double2(1.0, -1.0);
+}
+// sweep element g of a pair's table (g < NWD + NDISC)
+__device__ __forceinline__ double2 sweep_ab(const double2* __restrict__ AB, int g)
+{
+    return (g < NU_WDD) ? AB[g] : mirror_ab(AB[g - NU_WDD]);
+}
 // per unique donor tile: vx, vy, vz, arc centre, arc half-width (phase units)
 constexpr int DON_STRIDE = 5;
 
@@ -55,7 +68,7 @@ struct Ws {
     double* geo;
     int* status;
     int* bstatus;   // [pairs] stream status (k_setup stream lanes), folded into status by k_elements
-    double2* ab;    // [pairs][NEL] eclipse intervals (a, b)
+    double2* ab;    // [pairs][NELU] eclipse intervals (a, b) of the symmetry-unique elements
     double* donor;  // [pairs][NDONOR/4][DON_STRIDE] symmetry-unique donor tiles
     double* wts;    // [pairs][WT_N] ring / spot weights
     double* prior;
@@ -89,7 +102,7 @@ Ws carve(void* base, int W, int E, int gp_n = 0, int ndim_spec = 0, int nacc = 0
     ws.geo = reinterpret_cast<double*>(take(pairs * LFG_NGEO * sizeof(double)));
     ws.status = reinterpret_cast<int*>(take(pairs * sizeof(int)));
     ws.bstatus = reinterpret_cast<int*>(take(pairs * sizeof(int)));
-    ws.ab = reinterpret_cast<double2*>(take(pairs * NEL * sizeof(double2)));
+    ws.ab = reinterpret_cast<double2*>(take(pairs * NELU * sizeof(double2)));
     ws.donor = reinterpret_cast<double*>(take(pairs * (NDONOR / 4) * DON_STRIDE * sizeof(double)));
     ws.wts = reinterpret_cast<double*>(take(pairs * WT_N * sizeof(double)));
     ws.prior = reinterpret_cast<double*>(take(size_t(W) * sizeof(double)));
@@ -679,15 +692,10 @@ __global__ __launch_bounds__(ELEM_BLOCK) __attribute__((amdgpu_waves_per_eu(ELEM
         return;
     }
 
+    // the element of unique item u (its mirror's interval is implied)
     double Px, Py, Pz;
-    int k, km;
     if (u < U_WD) {  // white dwarf tile (MODEL_SPEC 5.1), cos(psi) > 0 half
         const int ir = wd_ring_of(u);
-        const int nk = 4 * (2 * ir + 1), q4 = nk / 4, jj = u - 2 * ir * ir;
-        const int j = (jj < q4) ? jj : jj - q4 + 3 * q4;
-        const int jm = (j < nk / 2) ? nk / 2 - 1 - j : 3 * nk / 2 - 1 - j;
-        k = 4 * ir * ir + j;
-        km = 4 * ir * ir + jm;
         const double rc = kWdRc[ir], mu0 = kWdMu0[ir];
         const double cp = kWdCos[u], sp = kWdSin[u];
         const double rw = G[G_RWD];
@@ -697,8 +705,6 @@ __global__ __launch_bounds__(ELEM_BLOCK) __attribute__((amdgpu_waves_per_eu(ELEM
     } else if (u < U_WD + U_DISC) {  // disc (MODEL_SPEC 5.2), alpha in (0, pi)
         const int uu = u - U_WD;
         const int ir = uu / (NDISC_AZ / 2), j = uu - ir * (NDISC_AZ / 2);
-        k = NWD + ir * NDISC_AZ + j;
-        km = NWD + ir * NDISC_AZ + NDISC_AZ - 1 - j;
         const double rin = G[G_RWD];
         const double rc = rin + (ir + 0.5) * ((G[G_RDISC] - rin) / NDISC_R);
         Px = rc * kDiscCos[j];
@@ -706,7 +712,6 @@ __global__ __launch_bounds__(ELEM_BLOCK) __attribute__((amdgpu_waves_per_eu(ELEM
         Pz = 0.0;
     } else {  // bright-spot strip (MODEL_SPEC 5.3): no mirror partner
         const int j = u - U_MAIN;
-        k = km = NWD + NDISC + j;
         const double uk = (j + 0.5) * (G[G_UMAX] / NBS);
         WT[size_t(pair) * WT_N + WT_BS + j] = bs_weight(j, G);
         const double off = G[G_L] * (uk - G[G_UPK]);
@@ -744,12 +749,34 @@ __global__ __launch_bounds__(ELEM_BLOCK) __attribute__((amdgpu_waves_per_eu(ELEM
 #else
     element_interval_fast(R, Px, Py, Pz, s, c, G[G_RCAL], G[G_REFF], a, b);
 #endif
-    const size_t o = size_t(pair) * NEL;
-    AB[o + slot_of(k)] = make_double2(a, b);
-    if (km != k) {
-        const bool ecl = a < b;
-        AB[o + slot_of(km)] = ecl ? make_double2(-b, -a) : make_double2(1.0, -1.0);
+    AB[size_t(pair) * NELU + (u >= U_MAIN ? NU_WDD + (u - U_MAIN) : uslot(u))] = make_double2(a, b);
+}
+
+// interval of element k (MODEL_SPEC 5 numbering) from a pair's table: the
+// unique item of k's mirror pair, mirrored when k is the partner
+__device__ inline double2 elem_ab(const double2* __restrict__ AB, int k)
+{
+    if (k >= NWD + NDISC) return AB[NU_WDD + (k - NWD - NDISC)];
+    int u;
+    bool mir;
+    if (k < NWD) {  // ring ir holds 4 (2 ir + 1) tiles; j in [0, q4) u [3 q4, nk) are the unique ones
+        int ir = int(sqrt(k * 0.25));
+        if (4 * (ir + 1) * (ir + 1) <= k) ++ir;
+        if (4 * ir * ir > k) --ir;
+        const int nk = 4 * (2 * ir + 1), q4 = nk / 4;
+        int j = k - 4 * ir * ir;
+        mir = j >= q4 && j < 3 * q4;
+        if (mir) j = (j < nk / 2) ? nk / 2 - 1 - j : 3 * nk / 2 - 1 - j;
+        u = 2 * ir * ir + ((j < q4) ? j : j - 2 * q4);
+    } else {
+        const int ir = (k - NWD) / NDISC_AZ;
+        int j = k - NWD - ir * NDISC_AZ;
+        mir = j >= NDISC_AZ / 2;
+        if (mir) j = NDISC_AZ - 1 - j;
+        u = U_WD + ir * (NDISC_AZ / 2) + j;
     }
+    const double2 ab = AB[uslot(u)];
+    return mir ? mirror_ab(ab) : ab;
 }
 
 // test/inspection only: per-element weights and the full 400-tile donor
@@ -761,7 +788,7 @@ __global__ void k_expand(const double* __restrict__ geo, const int* __restrict__
     const int pair = int(t / NEL), k = int(t - long(pair) * NEL);
     if (pair >= npairs || status[pair] != ST_OK) return;
     const double* G = geo + size_t(pair) * LFG_NGEO;
-    const double2 ab = AB[size_t(pair) * NEL + slot_of(k)];
+    const double2 ab = elem_ab(AB + size_t(pair) * NELU, k);
     if (A) A[size_t(pair) * NEL + k] = ab.x;
     if (B) B[size_t(pair) * NEL + k] = ab.y;
     double w;
@@ -932,7 +959,7 @@ __device__ inline void combine_after(const LikeArgs& L, int pair)
 // w |[a,b] n [lo,hi]| / (hi - lo) directly.  Sums are 2^-61 fixed point in
 // int64 so LDS atomics add them exactly, independent of order.
 constexpr int LIKE_THREADS = 512;
-constexpr int ACC_LDS = 32;  // proposal coordinates of the fused acceptance kept in LDS (the rest re-read)
+constexpr int ACC_LDS = 24;  // proposal coordinates of the fused acceptance kept in LDS (the rest re-read)
 #ifndef LIKE_MINW
 #define LIKE_MINW 4  // minimum waves per SIMD: two 512-lane blocks per CU (<= 128 VGPRs; LDS < 80 KB)
 #endif
@@ -1054,6 +1081,9 @@ __device__ __forceinline__ long long to_fx(double x) { return static_cast<long l
 
 __device__ __forceinline__ void fx_add(unsigned long long* acc, int p, long long q)
 {
+#ifdef LFG_EXP_ATOM_TID  // timing experiment only (wrong sums): every lane its own address
+    p = threadIdx.x;
+#endif
     atomicAdd(acc + p, static_cast<unsigned long long>(q));
 }
 
@@ -1101,18 +1131,14 @@ __device__ __forceinline__ void apply_runs(const Runs& R, double a, double b, do
     }
 }
 
-// WD/disc element of sweep slot g: a stride-37 permutation of [0, NWD + NDISC)
-// so that the lanes of a wave take elements of different rings and azimuths
-// (their runs start at different points: fewer same-address LDS atomics)
-
-// ring of WD/disc element k: WD ring r holds 4 r^2 <= k < 4 (r + 1)^2, disc
-// rings follow (NDISC_AZ elements each)
-__device__ __forceinline__ int sweep_ring(int k)
+// ring of unique WD/disc item u: WD ring r holds 2 r^2 <= u < 2 (r + 1)^2,
+// disc rings follow (NDISC_AZ / 2 items each)
+__device__ __forceinline__ int uring(int u)
 {
-    if (k >= NWD) return NWD_RINGS + (k - NWD) / NDISC_AZ;
-    int r = int(sqrtf(float(k) * 0.25f));
-    r += (4 * (r + 1) * (r + 1) <= k) ? 1 : 0;
-    r -= (4 * r * r > k) ? 1 : 0;
+    if (u >= U_WD) return NWD_RINGS + (u - U_WD) / (NDISC_AZ / 2);
+    int r = int(sqrtf(float(u) * 0.5f));
+    r += (2 * (r + 1) * (r + 1) <= u) ? 1 : 0;
+    r -= (2 * r * r > u) ? 1 : 0;
     return r;
 }
 
@@ -1256,14 +1282,16 @@ __device__ __noinline__ double2 direct_wd_disc(const double2* __restrict__ AB, c
 {
     double ewd = 0.0, ed = 0.0;
     const double lo = phc - wk, hi = phc + wk;
-    for (int ring = 0; ring < NWD_RINGS + NDISC_R; ++ring) {
-        const int k0 = ring < NWD_RINGS ? 4 * ring * ring : NWD + (ring - NWD_RINGS) * NDISC_AZ;
-        const int k1 = ring < NWD_RINGS ? 4 * (ring + 1) * (ring + 1) : k0 + NDISC_AZ;
+    auto cover = [&](double2 ab) {
+        return (wk > 0.0) ? fmax(fmin(ab.y, hi) - fmax(ab.x, lo), 0.0) : ((phc > ab.x && phc < ab.y) ? 1.0 : 0.0);
+    };
+    for (int ring = 0; ring < NWD_RINGS + NDISC_R; ++ring) {  // each unique item and its mirror
+        const int u0 = ring < NWD_RINGS ? 2 * ring * ring : U_WD + (ring - NWD_RINGS) * (NDISC_AZ / 2);
+        const int u1 = ring < NWD_RINGS ? 2 * (ring + 1) * (ring + 1) : u0 + NDISC_AZ / 2;
         double acc = 0.0;
-        for (int k = k0; k < k1; ++k) {
-            const double2 ab = AB[slot_of(k)];
-            acc += (wk > 0.0) ? fmax(fmin(ab.y, hi) - fmax(ab.x, lo), 0.0)
-                              : ((phc > ab.x && phc < ab.y) ? 1.0 : 0.0);
+        for (int u = u0; u < u1; ++u) {
+            const double2 ab = AB[uslot(u)];
+            acc += cover(ab) + cover(mirror_ab(ab));
         }
         if (ring < NWD_RINGS) ewd = fma(swr[ring], acc, ewd); else ed = fma(swr[ring], acc, ed);
     }
@@ -1340,14 +1368,8 @@ __device__ __noinline__ void element_item(int u, const double* __restrict__ G, d
         return;
     }
     double Px, Py, Pz;
-    int k, km;
     if (u < U_WD) {  // white dwarf tile (MODEL_SPEC 5.1), cos(psi) > 0 half
         const int ir = wd_ring_of(u);
-        const int nk = 4 * (2 * ir + 1), q4 = nk / 4, jj = u - 2 * ir * ir;
-        const int j = (jj < q4) ? jj : jj - q4 + 3 * q4;
-        const int jm = (j < nk / 2) ? nk / 2 - 1 - j : 3 * nk / 2 - 1 - j;
-        k = 4 * ir * ir + j;
-        km = 4 * ir * ir + jm;
         const double rc = kWdRc[ir], mu0 = kWdMu0[ir];
         const double cp = kWdCos[u], sp = kWdSin[u];
         const double rw = G[G_RWD];
@@ -1357,8 +1379,6 @@ __device__ __noinline__ void element_item(int u, const double* __restrict__ G, d
     } else if (u < U_WD + U_DISC) {  // disc (MODEL_SPEC 5.2), alpha in (0, pi)
         const int uu = u - U_WD;
         const int ir = uu / (NDISC_AZ / 2), j = uu - ir * (NDISC_AZ / 2);
-        k = NWD + ir * NDISC_AZ + j;
-        km = NWD + ir * NDISC_AZ + NDISC_AZ - 1 - j;
         const double rin = G[G_RWD];
         const double rc = rin + (ir + 0.5) * ((G[G_RDISC] - rin) / NDISC_R);
         if (j == 0) {
@@ -1370,7 +1390,6 @@ __device__ __noinline__ void element_item(int u, const double* __restrict__ G, d
         Pz = 0.0;
     } else {  // bright-spot strip (MODEL_SPEC 5.3): no mirror partner
         const int j = u - U_MAIN;
-        k = km = NWD + NDISC + j;
         const double uk = (j + 0.5) * (G[G_UMAX] / NBS);
         sbw[j] = bs_weight(j, G);
         const double off = G[G_L] * (uk - G[G_UPK]);
@@ -1380,18 +1399,13 @@ __device__ __noinline__ void element_item(int u, const double* __restrict__ G, d
     }
     double a, b;
     element_interval_fast(R, Px, Py, Pz, s, c, G[G_RCAL], G[G_REFF], a, b);
-    if (k >= NWD + NDISC) {
-        sab[k - NWD - NDISC] = make_double2(a, b);
-        if (ABg) ABg[k] = make_double2(a, b);
+    if (u >= U_MAIN) {
+        sab[u - U_MAIN] = make_double2(a, b);
+        if (ABg) ABg[NU_WDD + (u - U_MAIN)] = make_double2(a, b);
         return;
     }
-    const double2 mir = (a < b) ? make_double2(-b, -a) : make_double2(1.0, -1.0);
-    stage[slot_of(k)] = make_double2(a, b);
-    stage[slot_of(km)] = mir;
-    if (ABg) {
-        ABg[slot_of(k)] = make_double2(a, b);
-        ABg[slot_of(km)] = mir;
-    }
+    stage[uslot(u)] = make_double2(a, b);
+    if (ABg) ABg[uslot(u)] = make_double2(a, b);
 }
 
 // does every exposure window of the pair's points come in sorted order
@@ -1502,7 +1516,7 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
     const int n = L.off ? L.off[e + 1] - o0 : L.N;
     const double* G = L.geo + size_t(pair) * LFG_NGEO;
     const double* Wt = L.WT + size_t(pair) * WT_N;
-    const double2* AB = L.AB + size_t(pair) * NEL;
+    const double2* AB = L.AB + size_t(pair) * NELU;
     const double* DONp = L.DON + size_t(pair) * U_DON * DON_STRIDE;
 
     // fused acceptance with one eclipse per walker: the proposal's coordinates
@@ -1513,11 +1527,19 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
     // whole block would be spilled: the kernel is at its 128-VGPR budget)
     __shared__ double sq[ACC_LDS];
     if (acc1 && tid < L.ndim && tid < ACC_LDS) sq[tid] = L.qprop[size_t(pair) * L.ndim + tid];
+    // each thread's own data point y, ye: fetched with the prologue's loads
+    // into this thread's LDS slot (no registers held through the passes, and
+    // no memory round trip where chi^2 is formed)
+    __shared__ double sy[CHI ? LIKE_TILE : 1], sye[CHI ? LIKE_TILE : 1];
+    if (CHI && tid < n) {
+        sy[tid] = L.y[o0 + tid];
+        if (!GP) sye[tid] = L.ye[o0 + tid];
+    }
     int st;
     double s, c, ul, td;
     double px = 0.0, pw = 0.0;  // tile-0 point of this thread (y, ye: read where chi^2 is formed)
     // this thread's sweep items, held in registers for every tile: WD/disc
-    // elements sweep_item(tid + i nt) with their ring weights, spot element
+    // elements tid + i nt (sweep_ab) with their ring weights, spot element
     // tid (< NBS), donor tile (last NDONOR lanes)
     constexpr int NI = (NWD + NDISC + nt - 1) / nt;
     double2 abk[NI];
@@ -1552,7 +1574,7 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
             __syncthreads();
             for (int i = 0; i < NI; ++i) {
                 const int g = tid + i * nt;
-                abk[i] = (g < NWD + NDISC) ? stage[g] : make_double2(1.0, -1.0);
+                abk[i] = (g < NWD + NDISC) ? sweep_ab(stage, g) : make_double2(1.0, -1.0);
             }
             if (tid < NBS) {
                 abB = sab[tid];
@@ -1583,10 +1605,10 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
         }
         for (int i = 0; i < NI; ++i) {
             const int g = tid + i * nt;
-            abk[i] = (g < NWD + NDISC) ? AB[g] : make_double2(1.0, -1.0);
+            abk[i] = (g < NWD + NDISC) ? sweep_ab(AB, g) : make_double2(1.0, -1.0);
         }
         if (tid < NBS) {
-            abB = AB[NWD + NDISC + tid];
+            abB = AB[NU_WDD + tid];
             wB = Wt[WT_BS + tid];
         } else if (tid >= nt - NDONOR) {
             const int t = tid - (nt - NDONOR);
@@ -1683,6 +1705,10 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
         if (t0 > 0 && own) {
             px = L.x[p];
             pw = L.w ? L.w[p] : 0.0;
+            if (CHI) {
+                sy[tid] = L.y[p];
+                if (!GP) sye[tid] = L.ye[p];
+            }
         }
         const double wk = own ? pw : 0.0;
         const double ph0 = own ? px - SG[G_PHI0] : 0.0;
@@ -1729,9 +1755,10 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
 #pragma unroll
                 for (int i = 0; i < NI; ++i)
                     if (abk[i].x < abk[i].y) {
-                        const int k = sweep_item(tid + i * nt);
+                        const int g = tid + i * nt;
+                        const int u = uitem(g < NU_WDD ? g : g - NU_WDD);
                         apply_runs(Runs{Jb[2 * i], J[2 * i], Jb[2 * i + 1], J[2 * i + 1]}, abk[i].x, abk[i].y,
-                                   swn[sweep_ring(k)], X, TA.hi, TA.iw, sacc[(k < NWD) ? 0 : 1]);
+                                   swn[uring(u)], X, TA.hi, TA.iw, sacc[(u < U_WD) ? 0 : 1]);
                     }
             }
             LIKE_STAMP(2);
@@ -1800,10 +1827,10 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
                 L.comps[(size_t(3) * L.npairs + pair) * n + pi] = fr;
             }
             if (CHI && !GP) {
-                const double r = (L.y[p] - f) / L.ye[p];  // loaded here: no registers held over the passes
+                const double r = (sy[tid] - f) / sye[tid];
                 chi += isnan(f) ? INFINITY : r * r;
             }
-            if (GP) L.res[size_t(pair) * L.N + pi] = L.y[p] - f;  // the filter runs in k_gp_like
+            if (GP) L.res[size_t(pair) * L.N + pi] = sy[tid] - f;  // the filter runs in k_gp_like
         }
         LIKE_STAMP(5);
     }

@@ -423,8 +423,12 @@ __device__ __forceinline__ void rotate(double& cs, double& sn, double d)
 // converges one step earlier (tools/newton_emul statistics in DESIGN.md).
 // Stop once |dth| <= TH_LAST (th error ~TH_LAST^2 after the step) and
 // |dt| <= T_LAST (t errors reach th squared): ~1e-14 rad (MODEL_SPEC 7).
-constexpr double TH_LAST = 3e-8;
-constexpr double T_LAST = 1e-5;
+#ifndef LFG_TH_LAST  // experiment builds may override (tools/build_exp.sh)
+#define LFG_TH_LAST 3e-8
+#define LFG_T_LAST 1e-5
+#endif
+constexpr double TH_LAST = LFG_TH_LAST;
+constexpr double T_LAST = LFG_T_LAST;
 
 struct Tan {
     double th, cs, sn, t;

@@ -21,3 +21,13 @@ for k, v in sorted(d.items()):
         v = sorted(v); print('  %-22s grid %8s n %3d median %7.1f us' % (k[0], k[1], len(v), v[len(v)//2] / 1e3))
 PY
 done
+python3 - $R/gpurun_out <<'PY'
+import glob, os, sys, numpy as np
+d = sys.argv[1]
+ref = np.load(os.path.join(d, "kt_lnp_hip.npy")) if os.path.exists(os.path.join(d, "kt_lnp_hip.npy")) else None
+for f in sorted(glob.glob(os.path.join(d, "kt_lnp_*.npy"))):
+    v = np.load(f)
+    if ref is not None:
+        ok = np.isfinite(ref) & np.isfinite(v)
+        print("  %-28s max |dlnp| vs main %.3g  finite-pattern same %s" % (os.path.basename(f), np.abs(v[ok] - ref[ok]).max(), bool((np.isfinite(ref) == np.isfinite(v)).all())))
+PY

@@ -35,3 +35,5 @@ for _ in range(int(sys.argv[1]) if len(sys.argv) > 1 else 30):
     ev(x, out=out)
 torch.cuda.synchronize()
 print("lnp mean", float(out[torch.isfinite(out)].mean()))
+tag = os.path.basename(os.environ.get("LFG_LIB", "main")).replace("liblfg_", "").replace(".so", "")
+np.save(os.path.join(os.path.dirname(cache), "kt_lnp_%s.npy" % tag), out.cpu().numpy())
