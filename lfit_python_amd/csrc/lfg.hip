@@ -1275,9 +1275,10 @@ __device__ __forceinline__ void sweep_spot_donor(int tid, const PhaseIndex& XW, 
 }
 
 // direct (point-major) WD and disc eclipse fractions of one window: the
-// fallback for unsorted or mixed windows (out of line: it must not add to the
-// sweep's register budget)
-__device__ __noinline__ double2 direct_wd_disc(const double2* __restrict__ AB, const double* __restrict__ swr,
+// fallback for unsorted or mixed windows.  Inlined: k_lnlike takes it as a
+// whole pass of its own, where little is live (an out-of-line call anywhere
+// in the kernel spilled ~14 live values to scratch in every block)
+__device__ __forceinline__ double2 direct_wd_disc(const double2* __restrict__ AB, const double* __restrict__ swr,
                                                double phc, double wk, double twd, double td)
 {
     double ewd = 0.0, ed = 0.0;
@@ -1299,18 +1300,23 @@ __device__ __noinline__ double2 direct_wd_disc(const double2* __restrict__ AB, c
     return make_double2(ewd * nrm * (1.0 / twd), ed * nrm * (1.0 / td));
 }
 
-// direct (point-major) spot eclipse fraction and donor sum for one point
-__device__ __noinline__ double2 direct_spot_donor(const double2* ABs, const double* sbw, const double* DONp, double ph,
-                                                  double h, double e0, double e1, double c, double itb)
+// direct (point-major) spot eclipse fraction of one window
+__device__ __forceinline__ double direct_spot(const double2* ABs, const double* sbw, double ph, double h, double itb)
 {
-    double eb = 0.0, D = 0.0;
+    double eb = 0.0;
     const double l2 = ph - h, h2 = ph + h;
     for (int k = 0; k < NBS; ++k) {
         const double2 ab = ABs[k];
         eb = fma(sbw[k], (h > 0.0) ? fmax(fmin(ab.y, h2) - fmax(ab.x, l2), 0.0)
                                    : ((ph > ab.x && ph < ab.y) ? 1.0 : 0.0), eb);
     }
-    eb *= ((h > 0.0) ? 1.0 / (2.0 * h) : 1.0) * itb;
+    return eb * ((h > 0.0) ? 1.0 / (2.0 * h) : 1.0) * itb;
+}
+
+// direct donor sum for one line of sight e = (e0, e1, c)
+__device__ __forceinline__ double direct_donor(const double* DONp, double e0, double e1, double c)
+{
+    double D = 0.0;
     for (int q = 0; q < U_DON; ++q) {
         // max(A + Y, 0) + max(A - Y, 0) = max(A + max(Y, A), 0), A = vx e0 +- vz c
         const double* d5 = DONp + q * DON_STRIDE;
@@ -1318,7 +1324,7 @@ __device__ __noinline__ double2 direct_spot_donor(const double2* ABs, const doub
         const double A1 = fma(d5[0], e0, z), A2 = fma(d5[0], e0, -z);
         D += fmax(A1 + fmax(y, A1), 0.0) + fmax(A2 + fmax(y, A2), 0.0);
     }
-    return make_double2(eb, D);
+    return D;
 }
 
 
@@ -1428,8 +1434,17 @@ __device__ __forceinline__ int windows_unsorted(const LikeArgs& L, int o0, int n
 }
 
 #ifdef LFG_PROFILE_LIKE  // diagnostic build only: phase stamps (first tile) into spare geo slots 41..46
+// (thread 0), and the earliest / latest wave of each block per phase (g_like_wav)
+__device__ unsigned long long g_like_wav[2][6][4096];
 #define LIKE_STAMP(i)                                                                                       \
-    if (tid == 0 && t0 == 0) const_cast<double*>(G)[41 + (i)] = double(__builtin_amdgcn_s_memtime() - tstart)
+    if (t0 == 0) {                                                                                          \
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime() - tstart;                             \
+        if (tid == 0) const_cast<double*>(G)[41 + (i)] = double(now_);                                       \
+        if (lane == 0 && blockIdx.x < 4096) {                                                                \
+            atomicMin(&g_like_wav[0][i][blockIdx.x], now_);                                                  \
+            atomicMax(&g_like_wav[1][i][blockIdx.x], now_);                                                  \
+        }                                                                                                   \
+    }
 // prologue stamps of thread 0 (and of the block's last lane) per block: lfg_debug_like_cycles
 __device__ unsigned long long g_like_cyc[8][4096];
 #define LIKE_PRO(k)                                                                                 \
@@ -1511,7 +1526,7 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
     constexpr int nt = LIKE_THREADS, nw = LIKE_THREADS / 64;
     const int pair = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int e = pair % L.E;
+    const int e = (L.E == 1) ? 0 : pair % L.E;  // (one eclipse: no division constants held)
     const int o0 = L.off ? L.off[e] : 0;
     const int n = L.off ? L.off[e + 1] - o0 : L.N;
     const double* G = L.geo + size_t(pair) * LFG_NGEO;
@@ -1739,69 +1754,76 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
             if (!one) build_cells(TB.lo, m, TB.cell, tid);
             build_cells(sph, m, scp, tid);
             __syncthreads();
-            const bool swA = (j == 0) && sflag[0] == 0, swB = sflag[1] == 0;  // sweep, else direct
+            // any unsorted / mixed window (or invalid width) of the tile: the
+            // whole pass goes point-major (every element against each point)
+            const bool dir = (j == 0 && sflag[0] != 0) || sflag[1] != 0;
             LIKE_STAMP(1);
-            if (swA) {
-                const PhaseIndex X = phase_index(TA.lo, TA.cell, m);
-                double qx[2 * NI];
-                int J[2 * NI], Jb[2 * NI];
-#pragma unroll
-                for (int i = 0; i < NI; ++i) {
-                    qx[2 * i] = abk[i].x;
-                    qx[2 * i + 1] = abk[i].y;
-                }
-                count_lt_multi<2 * NI>(X, qx, J);
-                count_le_back_multi<2 * NI>(TA.hi, qx, J, Jb);
-#pragma unroll
-                for (int i = 0; i < NI; ++i)
-                    if (abk[i].x < abk[i].y) {
-                        const int g = tid + i * nt;
-                        const int u = uitem(g < NU_WDD ? g : g - NU_WDD);
-                        apply_runs(Runs{Jb[2 * i], J[2 * i], Jb[2 * i + 1], J[2 * i + 1]}, abk[i].x, abk[i].y,
-                                   swn[uring(u)], X, TA.hi, TA.iw, sacc[(u < U_WD) ? 0 : 1]);
+            double eb = 0.0, R3 = 0.0, R4 = 0.0, R5 = 0.0;
+            if (dir) {
+                if (own) {
+                    if (j == 0) {
+                        const double ulg = SG[G_ULIMB];
+                        const double2 f2 = direct_wd_disc(AB, swr, phc, wk, TWO_PI * ((1.0 - ulg) * 0.5 + ulg / 3.0),
+                                                          FUSED ? swt[WT_TD] : Wt[WT_TD]);
+                        fw = f2.x;
+                        fd = f2.y;
                     }
-            }
-            LIKE_STAMP(2);
-            if (swB) {
-                const PhaseIndex XP = phase_index(sph, scp, m);
-                if (one)
-                    sweep_spot_donor(tid, phase_index(TA.lo, TA.cell, m), TA, XP, sab, sbw, snorm[0], sdq, snorm[1],
-                                     sacc + 2);
-                else
-                    sweep_spot_donor(tid, phase_index(TB.lo, TB.cell, m), TB, XP, sab, sbw, snorm[0], sdq, snorm[1],
-                                     sacc + 2);
-            }
-            __syncthreads();
-            LIKE_STAMP(3);
-            long long r[6] = {0, 0, 0, 0, 0, 0};
-            if (j == 0) block_scan<6>(sacc, spart, tid, r);
-            else block_scan<4>(sacc + 2, spart + 2, tid, r + 2);  // sub-bin passes: spot and donor only
-            LIKE_STAMP(4);
-            if (j == 0) {
-                if (swA) {
+                    eb = direct_spot(sab, sbw, ph, h, snorm[0]);
+                }
+                __syncthreads();  // every wave has read sflag before the next pass resets it
+            } else {
+                if (j == 0) {
+                    const PhaseIndex X = phase_index(TA.lo, TA.cell, m);
+                    double qx[2 * NI];
+                    int J[2 * NI], Jb[2 * NI];
+#pragma unroll
+                    for (int i = 0; i < NI; ++i) {
+                        qx[2 * i] = abk[i].x;
+                        qx[2 * i + 1] = abk[i].y;
+                    }
+                    count_lt_multi<2 * NI>(X, qx, J);
+                    count_le_back_multi<2 * NI>(TA.hi, qx, J, Jb);
+#pragma unroll
+                    for (int i = 0; i < NI; ++i)
+                        if (abk[i].x < abk[i].y) {
+                            const int g = tid + i * nt;
+                            const int u = uitem(g < NU_WDD ? g : g - NU_WDD);
+                            apply_runs(Runs{Jb[2 * i], J[2 * i], Jb[2 * i + 1], J[2 * i + 1]}, abk[i].x, abk[i].y,
+                                       swn[uring(u)], X, TA.hi, TA.iw, sacc[(u < U_WD) ? 0 : 1]);
+                        }
+                }
+                LIKE_STAMP(2);
+                {
+                    const PhaseIndex XP = phase_index(sph, scp, m);
+                    if (one)
+                        sweep_spot_donor(tid, phase_index(TA.lo, TA.cell, m), TA, XP, sab, sbw, snorm[0], sdq,
+                                         snorm[1], sacc + 2);
+                    else
+                        sweep_spot_donor(tid, phase_index(TB.lo, TB.cell, m), TB, XP, sab, sbw, snorm[0], sdq,
+                                         snorm[1], sacc + 2);
+                }
+                __syncthreads();
+                LIKE_STAMP(3);
+                long long r[6] = {0, 0, 0, 0, 0, 0};
+                if (j == 0) block_scan<6>(sacc, spart, tid, r);
+                else block_scan<4>(sacc + 2, spart + 2, tid, r + 2);  // sub-bin passes: spot and donor only
+                LIKE_STAMP(4);
+                if (j == 0) {
                     fw = double(r[0]) * FX_INV;
                     fd = double(r[1]) * FX_INV;
-                } else if (own) {  // unsorted / mixed widths: every element against this point
-                    const double ulg = SG[G_ULIMB];
-                    const double2 f2 = direct_wd_disc(AB, swr, phc, wk, TWO_PI * ((1.0 - ulg) * 0.5 + ulg / 3.0),
-                                                      FUSED ? swt[WT_TD] : Wt[WT_TD]);
-                    fw = f2.x;
-                    fd = f2.y;
                 }
+                eb = double(r[2]) * FX_INV;
+                R3 = double(r[3]);
+                R4 = double(r[4]);
+                R5 = double(r[5]);
             }
             const double2 scp2 = sincospi_ool(2.0 * ph);  // |2 ph| <= 1: cheap exact reduction
             const double sn = scp2.x, cs = scp2.y;
             const double sg = SG[G_S], cg = SG[G_C];
             const double e0 = sg * cs, e1 = -sg * sn;
-            double eb = 0.0, D = 0.0;
-            if (swB) {
-                eb = double(r[2]) * FX_INV;
-                D = (e0 * double(r[3]) + e1 * double(r[4]) + cg * double(r[5])) * (FX_INV * snorm[3]);
-            } else if (own) {
-                const double2 ed2 = direct_spot_donor(sab, sbw, sdq, ph, h, e0, e1, cg, snorm[0]);
-                eb = ed2.x;
-                D = ed2.y;
-            }
+            double D = 0.0;
+            if (!dir) D = (e0 * R3 + e1 * R4 + cg * R5) * (FX_INV * snorm[3]);
+            else if (own) D = direct_donor(sdq, e0, e1, cg);
             double beam = 0.0;
             const double bden = SG[G_BDEN], fis = SG[G_FIS];
             if (bden > 0.0)
@@ -2632,6 +2654,18 @@ int lfg_gp_lnlike(const double* x, const double* ye, const double* res, int W, i
 int lfg_debug_like_cycles(unsigned long long* host)
 {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_like_cyc), sizeof(g_like_cyc)) == hipSuccess ? 0 : -1;
+}
+
+// per-wave phase stamps: host [2][6][4096] (min, max over the block's waves);
+// reset (host == nullptr): min slots to ~0, max slots to 0
+int lfg_debug_like_waves(unsigned long long* host)
+{
+    static unsigned long long buf[2][6][4096];
+    if (!host) {
+        for (int i = 0; i < 6 * 4096; ++i) { (&buf[0][0][0])[i] = ~0ull; (&buf[1][0][0])[i] = 0ull; }
+        return hipMemcpyToSymbol(HIP_SYMBOL(g_like_wav), buf, sizeof(buf)) == hipSuccess ? 0 : -1;
+    }
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_like_wav), sizeof(g_like_wav)) == hipSuccess ? 0 : -1;
 }
 #endif
 

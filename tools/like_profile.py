@@ -19,6 +19,7 @@ flux = torch.empty((W, len(x)), dtype=torch.float64, device=dev)
 st = torch.empty(W, dtype=torch.int32, device=dev)
 ws = torch.empty(L.lfg_workspace_size(W, 1), dtype=torch.uint8, device=dev)
 vp = lambda t: ctypes.c_void_p(t.data_ptr())
+L.lfg_debug_like_waves(None)
 for _ in range(3):
     rc = L.lfg_flux(vp(pars), W, 18, vp(X), vp(Wd), len(x), NSUB, vp(flux), None, vp(st), vp(ws), ws.numel(),
                     _native.stream_ptr())
@@ -53,3 +54,10 @@ L.lfg_debug_like_cycles(ctypes.c_void_p(cyc.ctypes.data))
 cyc = cyc[:, :W].astype(np.float64)[:, ok]
 for k, nm in enumerate(['status known', 'wave sums (before barrier)', 'after the barrier']):
     print('prologue %-28s thread 0 mean %7.0f | last lane mean %7.0f' % (nm, cyc[k].mean(), cyc[4 + k].mean()))
+
+wv = np.zeros((2, 6, 4096), dtype=np.uint64)
+L.lfg_debug_like_waves(ctypes.c_void_p(wv.ctypes.data))
+wv = wv[:, :, :W].astype(np.float64)[:, :, ok]
+print('per-wave stamps (last launch overwrites max only; min is over all launches):')
+for i, nm in enumerate(names):
+    print('  %-8s first wave mean %8.0f   last wave mean %8.0f   spread %6.0f' % (nm, wv[0, i].mean(), wv[1, i].mean(), (wv[1, i] - wv[0, i]).mean()))
