@@ -1647,7 +1647,7 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
 
     LIKE_PRO(0);
     if (st != ST_OK) {
-        for (int p = tid; p < n; p += nt) {
+        for (int p = tid; p < n && !CHI; p += nt) {  // flux outputs: MODE 0 only (the tree paths pass none)
             if (L.flux) L.flux[size_t(pair) * n + p] = NAN;
             if (L.comps)
                 for (int m = 0; m < 4; ++m) L.comps[(size_t(m) * L.npairs + pair) * n + p] = NAN;
@@ -1711,13 +1711,15 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
     // loads of G would hold ~13 doubles in VGPRs through every pass)
     const double* SG = sgeo;
     const int S = L.nsub;
-    double chi = 0.0;
     for (int t0 = 0; t0 < n; t0 += LIKE_TILE) {
+        double chi = 0.0;  // this tile's chi^2 (summed per wave into red[1] at the tile's end)
         const int m = min(LIKE_TILE, n - t0);
         LIKE_STAMP(0);
         const bool own = tid < m;
-        const int p = o0 + t0 + tid;
         if (t0 > 0 && own) {
+            // the point index re-formed from a fresh (volatile) read of the
+            // offset: o0 + tid would otherwise be held, spilled, over the tiles
+            const int p = (L.off ? *reinterpret_cast<const volatile int*>(L.off + e) : 0) + t0 + tid;
             px = L.x[p];
             pw = L.w ? L.w[p] : 0.0;
             if (CHI) {
@@ -1841,8 +1843,8 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
             const double fb = SG[G_SF] * sbs / S, fr = SG[G_RSF] * srs / S;
             const double f = fwv + fdv + fb + fr;
             const int pi = t0 + tid;
-            if (L.flux) L.flux[size_t(pair) * n + pi] = f;
-            if (L.comps) {
+            if (!CHI && L.flux) L.flux[size_t(pair) * n + pi] = f;
+            if (!CHI && L.comps) {
                 L.comps[(size_t(0) * L.npairs + pair) * n + pi] = fwv;
                 L.comps[(size_t(1) * L.npairs + pair) * n + pi] = fdv;
                 L.comps[(size_t(2) * L.npairs + pair) * n + pi] = fb;
@@ -1854,15 +1856,17 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
             }
             if (GP) L.res[size_t(pair) * L.N + pi] = sy[tid] - f;  // the filter runs in k_gp_like
         }
+        if (CHI && !GP) {  // red[1] is free after the prologue; each wave owns its slot
+            chi = wave_sum(chi);
+            if (lane == 0) red[1][wv] = (t0 == 0) ? chi : red[1][wv] + chi;
+        }
         LIKE_STAMP(5);
     }
     if (CHI && !GP) {
-        chi = wave_sum(chi);
-        if (lane == 0) red[0][wv] = chi;
         __syncthreads();
         if (tid == 0) {
             double tot = 0.0;
-            for (int i = 0; i < nw; ++i) tot += red[0][i];
+            for (int i = 0; i < nw; ++i) tot += red[1][i];
             L.lle[pair] = -0.5 * tot;
         }
         finish_walker(L, pair, tid, acc1, sq, sacc1, sflag);
