@@ -1169,14 +1169,18 @@ __device__ __forceinline__ long long wave_scan_incl(long long v, int lane)
 }
 
 // inclusive prefix of NA difference arrays at index tid (one entry per thread)
+// (ext, nullable: second copies of arrays 0 and 1, summed in; the integer
+// sums are exact, so the split changes no bit of the result)
 template <int NA>
 __device__ __forceinline__ void block_scan(unsigned long long (*acc)[LIKE_TILE + 1], long long (*part)[LIKE_THREADS / 64],
-                                           int tid, long long* out)
+                                           int tid, long long* out,
+                                           const unsigned long long (*ext)[LIKE_TILE + 1] = nullptr)
 {
     const int lane = tid & 63, wv = tid >> 6;
     constexpr int NW = LIKE_THREADS / 64;
     for (int i = 0; i < NA; ++i) {
-        out[i] = wave_scan_incl(static_cast<long long>(acc[i][tid]), lane);
+        const unsigned long long a = acc[i][tid] + ((ext && i < 2) ? ext[i][tid] : 0ull);
+        out[i] = wave_scan_incl(static_cast<long long>(a), lane);
         if (lane == 63) part[i][wv] = out[i];
     }
     __syncthreads();
@@ -1514,7 +1518,17 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
     __shared__ double sacc1[3];                   // fused acceptance: ln u, zfac, old ln_prob
     __shared__ double snorm[4];                   // 1 / spot total, 1 / donor |v| sum, donor norm, |v| sum
     __shared__ double sgeo[LFG_NGEO];             // the pair's geometry record, read at use in the tile loop
-    __shared__ TileBufs TA, TB;      // WD/disc windows; spot windows of the current sub-bin
+    // TA: WD/disc windows.  TB: the spot windows of the current sub-bin when
+    // S > 1; at S = 1 (spot windows = TA's) its space holds second copies of
+    // the WD and disc difference arrays, taken by the odd lanes of the sweep:
+    // half the same-address LDS atomics where contacts cluster (four WD
+    // copies measured no faster: more arrays to zero and scan)
+    __shared__ TileBufs TA;
+    __shared__ union TBU_ {
+        TileBufs B;
+        unsigned long long X[2][LIKE_TILE + 1];
+    } TBU;
+    TileBufs& TB = TBU.B;
     __shared__ double sph[LIKE_TILE];  // sub-bin centre phases (donor)
     __shared__ int scp[LIKE_NC + 1];
     __shared__ unsigned long long sacc[6][LIKE_TILE + 1];
@@ -1743,6 +1757,10 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
             int flB = one ? 0 : put_window(TB, tid, own, ph, h);
             if (own) sph[tid] = ph;
             for (int i = (j == 0) ? 0 : 2; i < 6; ++i) sacc[i][tid] = 0ull;
+            if (one) {
+                TBU.X[0][tid] = 0ull;
+                TBU.X[1][tid] = 0ull;
+            }
             if (tid == 0)
                 for (int i = (j == 0) ? 0 : 2; i < 6; ++i) sacc[i][nt] = 0ull;
             __syncthreads();
@@ -1791,7 +1809,8 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
                             const int g = tid + i * nt;
                             const int u = uitem(g < NU_WDD ? g : g - NU_WDD);
                             apply_runs(Runs{Jb[2 * i], J[2 * i], Jb[2 * i + 1], J[2 * i + 1]}, abk[i].x, abk[i].y,
-                                       swn[uring(u)], X, TA.hi, TA.iw, sacc[(u < U_WD) ? 0 : 1]);
+                                       swn[uring(u)], X, TA.hi, TA.iw,
+                                       ((one && (lane & 1)) ? TBU.X : sacc)[(u < U_WD) ? 0 : 1]);
                         }
                 }
                 LIKE_STAMP(2);
@@ -1807,7 +1826,7 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
                 __syncthreads();
                 LIKE_STAMP(3);
                 long long r[6] = {0, 0, 0, 0, 0, 0};
-                if (j == 0) block_scan<6>(sacc, spart, tid, r);
+                if (j == 0) block_scan<6>(sacc, spart, tid, r, one ? TBU.X : nullptr);
                 else block_scan<4>(sacc + 2, spart + 2, tid, r + 2);  // sub-bin passes: spot and donor only
                 LIKE_STAMP(4);
                 if (j == 0) {
