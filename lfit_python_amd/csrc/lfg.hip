@@ -633,7 +633,15 @@ __global__ __launch_bounds__(ELEM_BLOCK) __attribute__((amdgpu_waves_per_eu(ELEM
         return;
     }
     static_assert((NUNIQ % ELEM_BLOCK) + NDISC_R + 1 <= ELEM_BLOCK, "ring-weight lanes fit in the last chunk");
-#ifndef LFG_EXP_OLDORDER
+#if defined(LFG_EXP_ORDER2)  // experiment: spot, disc, WD, donor
+    const int u = (v < U_BS) ? U_MAIN + v
+                : (v < U_BS + U_DISC) ? U_WD + (v - U_BS)
+                : (v < U_BS + U_DISC + U_WD) ? v - U_BS - U_DISC : v - U_BS;
+#elif defined(LFG_EXP_ORDER3)  // experiment: disc, spot, WD, donor
+    const int u = (v < U_DISC) ? U_WD + v
+                : (v < U_DISC + U_BS) ? U_MAIN + (v - U_DISC)
+                : (v < U_DISC + U_BS + U_WD) ? v - U_DISC - U_BS : v - U_BS;
+#elif !defined(LFG_EXP_OLDORDER)
     // launch order WD, disc, spot, donor: the last chunk, dispatched last,
     // holds the cheap donor items (one 1-D root) instead of spot tangencies
     constexpr int V_BS = U_WD + U_DISC;

@@ -577,7 +577,11 @@ __device__ inline bool element_interval_fast(const Roche& R, double Px, double P
         }
     }
     if (fallback) *fallback = true;
+#ifdef LFG_EXP_NOFALLBACK  // timing experiment only: no nested-solver fallback
+    a = 1.0; b = -1.0; return false;
+#else
     return element_interval(R, Px, Py, Pz, s, c, Reff, a, b);
+#endif
 }
 
 // findphi / findi with the same 2-D tangency Newton, nested solver fallback
