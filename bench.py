@@ -76,13 +76,15 @@ F_GP_POINT = 150.0   # one Kalman step (MODEL_SPEC 10.4)
 
 # builder's intermediate tables per (walker, eclipse) pair:
 # what each kernel reads and writes of the tables the kernels hand each other
-NEL, U_DON, DON_STRIDE = 1500, 100, 5
+# (intervals: the 700 symmetry-unique WD/disc elements + 100 spot, 16 B each;
+# k_lnlike also reads each point's x, w, y, ye: shared by the eclipse's pairs)
+NELU, U_DON, DON_STRIDE = 800, 100, 5
 GEO_SETUP, GEO_BSPOT, GEO_READ = 41, 5, 40
 WT_N = 124
 MATERIALISED_PER_PAIR = {
     "k_setup": 18 * 8 + GEO_SETUP * 8 + 4 + 3 * 8 + GEO_BSPOT * 8 + 4,
-    "k_elements": GEO_READ * 8 + 8 + NEL * 16 + U_DON * DON_STRIDE * 8 + WT_N * 8,
-    "k_lnlike": GEO_READ * 8 + 4 + NEL * 16 + U_DON * DON_STRIDE * 8 + WT_N * 8 + 8,
+    "k_elements": GEO_READ * 8 + 8 + NELU * 16 + U_DON * DON_STRIDE * 8 + WT_N * 8,
+    "k_lnlike": GEO_READ * 8 + 4 + NELU * 16 + U_DON * DON_STRIDE * 8 + WT_N * 8 + 8,
 }
 
 CONFIGS = {

@@ -828,28 +828,40 @@ __global__ void k_expand(const double* __restrict__ geo, const int* __restrict__
 }
 
 // --------------------------------------------------------------- k_lnlike
-// Cross-lane moves by ds_bpermute with the lane address formed at each use:
-// __shfl_xor / __shfl_up hoist one address VGPR per offset out of every loop
-// and keep them live through k_lnlike (the volatile mbcnt is not hoisted).
-__device__ __forceinline__ int lane_id_here()
+// Cross-lane sums and scans by DPP (no LDS round trips; __shfl_xor /
+// __shfl_up would also hoist one address VGPR per offset out of every loop
+// and keep it live through k_lnlike).
+// v of the lane CTRL's DPP pattern names (0 where the source lane is outside
+// the row or the row is not in RM): two 32-bit DPP moves, no LDS round trip
+template <int CTRL, int RM>
+__device__ __forceinline__ long long dpp64(long long v)
 {
-    int l;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
-    return l;
-}
-
-__device__ __forceinline__ long long bperm64(int addr, long long v)
-{
-    const int lo = __builtin_amdgcn_ds_bpermute(addr, static_cast<int>(v));
-    const int hi = __builtin_amdgcn_ds_bpermute(addr, static_cast<int>(v >> 32));
+    const int lo = __builtin_amdgcn_update_dpp(0, static_cast<int>(v), CTRL, RM, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, static_cast<int>(v >> 32), CTRL, RM, 0xf, false);
     return (static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo);
 }
 
+template <int CTRL, int RM>
+__device__ __forceinline__ double dppd(double v)
+{
+    return __longlong_as_double(dpp64<CTRL, RM>(__double_as_longlong(v)));
+}
+
+// sum over the wave, the same value in every lane: the DPP inclusive scan
+// (row_shr 1, 2, 4, 8, row_bcast:15, row_bcast:31; no LDS round trips, the
+// bpermute butterfly waited one per step) and lane 63's total read back
 __device__ __forceinline__ double wave_sum(double v)
 {
-    for (int off = 32; off > 0; off >>= 1)
-        v += __longlong_as_double(bperm64((lane_id_here() ^ off) << 2, __double_as_longlong(v)));
-    return v;
+    v += dppd<0x111, 0xf>(v);
+    v += dppd<0x112, 0xf>(v);
+    v += dppd<0x114, 0xf>(v);
+    v += dppd<0x118, 0xf>(v);
+    v += dppd<0x142, 0xa>(v);
+    v += dppd<0x143, 0xc>(v);
+    const long long t = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane(static_cast<int>(t), 63);
+    const int hi = __builtin_amdgcn_readlane(static_cast<int>(t >> 32), 63);
+    return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
 }
 
 struct LikeArgs {
@@ -1148,16 +1160,6 @@ __device__ __forceinline__ int uring(int u)
     r += (2 * (r + 1) * (r + 1) <= u) ? 1 : 0;
     r -= (2 * r * r > u) ? 1 : 0;
     return r;
-}
-
-// v of the lane CTRL's DPP pattern names (0 where the source lane is outside
-// the row or the row is not in RM): two 32-bit DPP moves, no LDS round trip
-template <int CTRL, int RM>
-__device__ __forceinline__ long long dpp64(long long v)
-{
-    const int lo = __builtin_amdgcn_update_dpp(0, static_cast<int>(v), CTRL, RM, 0xf, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, static_cast<int>(v >> 32), CTRL, RM, 0xf, false);
-    return (static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo);
 }
 
 // inclusive wave prefix sum: Hillis-Steele within each row of 16 lanes
@@ -1707,17 +1709,14 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
     __syncthreads();
     LIKE_PRO(2);
     if (wv == 0) {  // block-uniform normalisers live in LDS (read at use: no registers held)
-        // the nw wave partials: lanes 0..nw-1 read them at once and a
-        // 3-step xor butterfly sums them (a serial loop in one lane waited
-        // on every LDS read in turn)
+        // the nw wave partials: lanes 0..nw-1 read them at once and three
+        // independent DPP wave sums add them (a serial loop in one lane
+        // waited on every LDS read in turn)
         double p0 = 0.0, p1 = 0.0, p2 = 0.0;
         if (lane < nw) { p0 = red[0][lane]; p1 = red[1][lane]; p2 = red[2][lane]; }
-        static_assert(nw == 8, "partials butterfly");
-        for (int off = 4; off > 0; off >>= 1) {
-            p0 += __longlong_as_double(bperm64((lane_id_here() ^ off) << 2, __double_as_longlong(p0)));
-            p1 += __longlong_as_double(bperm64((lane_id_here() ^ off) << 2, __double_as_longlong(p1)));
-            p2 += __longlong_as_double(bperm64((lane_id_here() ^ off) << 2, __double_as_longlong(p2)));
-        }
+        p0 = wave_sum(p0);
+        p1 = wave_sum(p1);
+        p2 = wave_sum(p2);
         if (lane == 0) {
             snorm[0] = 1.0 / p0;
             snorm[1] = 1.0 / p2;
