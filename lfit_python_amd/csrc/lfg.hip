@@ -985,6 +985,9 @@ constexpr int ACC_LDS = 24;  // proposal coordinates of the fused acceptance kep
 #endif
 constexpr int LIKE_TILE = LIKE_THREADS;  // one point per thread per tile
 constexpr int LIKE_NC = 2 * LIKE_TILE;   // cells of the phase index
+#ifndef LFG_WALK
+#define LFG_WALK 2  // unrolled forward steps of the cell walk before the loop
+#endif
 constexpr double FX_SCALE = 2305843009213693952.0;  // 2^61
 constexpr double FX_INV = 1.0 / FX_SCALE;
 
@@ -1011,7 +1014,7 @@ __device__ __forceinline__ int count_below(const PhaseIndex& X, double x)
     const int last = X.m - 1;
     bool adv = false;
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < LFG_WALK; ++k) {
         const double vj = X.v[min(j, last)];
         adv = (j <= last) & (LE ? (vj <= x) : (vj < x));
         j += adv ? 1 : 0;
@@ -1030,7 +1033,7 @@ __device__ __forceinline__ void count_lt_multi(const PhaseIndex& X, const double
     for (int q = 0; q < Q; ++q) j[q] = X.cell[cell_of(X, x[q])];
     bool adv[Q];
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < LFG_WALK; ++k) {
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             const double vj = X.v[min(j[q], last)];
@@ -1194,19 +1197,22 @@ __device__ __forceinline__ void block_scan(unsigned long long (*acc)[LIKE_TILE +
         if (lane == 63) part[i][wv] = out[i];
     }
     __syncthreads();
-    // exclusive prefix over the waves, one (array, wave) per thread, in
-    // place after a second barrier: each thread then reads one word per array
-    // (summing all earlier waves' totals in every thread holds NA x NW of
-    // them in registers at once)
-    long long pre = 0;
-    if (tid < NA * NW) {
-        const int i = tid / NW, k = tid - (tid / NW) * NW;
-        for (int q = 0; q < k; ++q) pre += part[i][q];
+    // exclusive prefix over the waves, formed by every wave for itself (one
+    // barrier, not three): lanes 0..NW-1 read the NW wave totals of an array
+    // in one LDS read, a 3-step DPP row scan sums them, and lane wv - 1's
+    // inclusive prefix is this wave's offset
+    static_assert(NW == 8, "wave totals fit one DPP row");
+    for (int i = 0; i < NA; ++i) {
+        long long t = (lane < NW) ? part[i][lane] : 0;
+        t += dpp64<0x111, 0xf>(t);
+        t += dpp64<0x112, 0xf>(t);
+        t += dpp64<0x114, 0xf>(t);
+        if (wv > 0) {
+            const int lo = __builtin_amdgcn_readlane(static_cast<int>(t), wv - 1);
+            const int hi = __builtin_amdgcn_readlane(static_cast<int>(t >> 32), wv - 1);
+            out[i] += (static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo);
+        }
     }
-    __syncthreads();
-    if (tid < NA * NW) part[tid / NW][tid - (tid / NW) * NW] = pre;
-    __syncthreads();
-    for (int i = 0; i < NA; ++i) out[i] += part[i][wv];
 }
 
 __device__ __forceinline__ double wrap_phase(double ph) { return ph - floor(ph + 0.5); }
@@ -1450,11 +1456,16 @@ __device__ __forceinline__ int windows_unsorted(const LikeArgs& L, int o0, int n
 #ifdef LFG_PROFILE_LIKE  // diagnostic build only: phase stamps (first tile) into spare geo slots 41..46
 // (thread 0), and the earliest / latest wave of each block per phase (g_like_wav)
 __device__ unsigned long long g_like_wav[2][6][4096];
+#ifdef LFG_PROFILE_LIKE_WAVES  // per-wave stamps (global atomics: they perturb the timing)
+constexpr bool LIKE_WAVES = true;
+#else
+constexpr bool LIKE_WAVES = false;
+#endif
 #define LIKE_STAMP(i)                                                                                       \
     if (t0 == 0) {                                                                                          \
         const unsigned long long now_ = __builtin_amdgcn_s_memtime() - tstart;                             \
         if (tid == 0) const_cast<double*>(G)[41 + (i)] = double(now_);                                       \
-        if (lane == 0 && blockIdx.x < 4096) {                                                                \
+        if (LIKE_WAVES && lane == 0 && blockIdx.x < 4096) {                                                  \
             atomicMin(&g_like_wav[0][i][blockIdx.x], now_);                                                  \
             atomicMax(&g_like_wav[1][i][blockIdx.x], now_);                                                  \
         }                                                                                                   \
