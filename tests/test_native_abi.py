@@ -65,7 +65,8 @@ def test_argument_errors_without_gpu():
     L = _native.lib()
     assert L.lfg_workspace_size(0, 1) == 0
     ws1 = L.lfg_workspace_size(1024, 1)
-    assert ws1 > 1024 * (2 * 1500 + 3 * 100) * 8  # intervals + unique donor tiles
+    # symmetry-unique intervals (700 WD/disc + 100 spot, a and b) + unique donor tiles
+    assert ws1 > 1024 * (2 * 800 + 5 * 100) * 8
     assert L.lfg_workspace_size(2048, 1) > ws1
     assert L.lfg_flux(None, 0, 18, None, None, 10, 1, None, None, None, None, 0, None) == -1
     assert L.lfg_flux(ctypes.c_void_p(8), 4, 15, None, None, 10, 1, None, None, None, None, 0, None) == -1
