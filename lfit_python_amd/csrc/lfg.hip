@@ -489,6 +489,9 @@ __device__ __forceinline__ void setup_any(const SetupArgs& A, int t)
     LFG_CY(3, t, tl);
 }
 
+#ifdef LFG_ELEM_OOL
+__device__ __noinline__ void setup_any_ool(const SetupArgs& A, int t) { setup_any(A, t); }
+#endif
 __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
 {
     setup_any(A, blockIdx.x * SETUP_BLOCK + threadIdx.x);
@@ -542,6 +545,19 @@ __device__ inline double bs_weight(int j, const double* G)
     return exp(G[G_EXP1] * log(uk) - pow(uk, G[G_EXP2]) - G[G_LNPK]);
 }
 
+// A walker whose ln_prior is -inf (a Prior.ln_prob term, the LCModel dphi
+// check, or a Roche prior of this eclipse) has ln_prob = -inf whatever its
+// likelihood: Node.ln_prob never calls ln_like for it (model.py:476-498).
+// Tree calls skip such pairs in k_elements, k_lnlike and k_gp_like alike, so
+// that no kernel reads tables the others did not write.  (Stretch proposals
+// outside the prior box are common: in a long config-2 chain most of the
+// proposals that sent element solves to the nested fallback were of this
+// kind, tools/fallback_hunt.py.)
+__device__ __forceinline__ bool prior_rejects(double lprior, const double* G)
+{
+    return !(lprior + G[G_RPRIOR] + G[G_RPRIOR_BS] > -INFINITY);
+}
+
 // k_elements' side jobs in lfg_stretch_step_half_spec:
 //  - sel: this half's k_setup outputs were formed speculatively inside the
 //    previous half's k_elements for both fates of each walker's partner;
@@ -564,6 +580,7 @@ struct ElemSpec {
     int* done;
     int* bstatus;
     int E, ndim;
+    const double* lprior;  // tree calls: the batch's Prior sums (k_setup), prior_rejects skips; nullptr: none
     SetupArgs S[2];
     int nspec;     // lanes per candidate (0: no speculative setup)
     int nspecblk;  // leading blocks that run them
@@ -577,7 +594,11 @@ __global__ __launch_bounds__(ELEM_BLOCK) __attribute__((amdgpu_waves_per_eu(ELEM
     if (int(blockIdx.x) < X.nspecblk) {  // speculative setup lanes of the next half
         const int t = int(blockIdx.x) * int(blockDim.x) + int(threadIdx.x);
         const int c = t < X.nspec ? 0 : 1;
+#ifdef LFG_ELEM_OOL
+        if (t < 2 * X.nspec) setup_any_ool(X.S[c], t - c * X.nspec);
+#else
         if (t < 2 * X.nspec) setup_any(X.S[c], t - c * X.nspec);
+#endif
         return;
     }
     const unsigned bid = blockIdx.x - unsigned(X.nspecblk);
@@ -660,6 +681,11 @@ __global__ __launch_bounds__(ELEM_BLOCK) __attribute__((amdgpu_waves_per_eu(ELEM
     if (bst != ST_OK) {
         if (u == 0 && !X.jk) status[pair] = bst;
         return;
+    }
+    if (X.lprior) {  // the walker's ln_prior is -inf: nothing to evaluate (k_lnlike skips it too)
+        const int w = pair / X.E;
+        const double lp = X.jk ? X.priorC[size_t(X.accflag[X.jk[w]]) * (npairs / X.E) + w] : X.lprior[w];
+        if (prior_rejects(lp, G)) return;
     }
     const Roche R{G[G_Q], G[G_CA], G[G_CB], G[G_MU], G[G_XL1], G[G_PL1], G[G_RS], G[G_RS2]};
     const double s = G[G_S], c = G[G_C];
@@ -746,6 +772,10 @@ __global__ __launch_bounds__(ELEM_BLOCK) __attribute__((amdgpu_waves_per_eu(ELEM
         }
         if ((threadIdx.x & 63) == 0) atomicAdd(C + 9, 1ull);
         atomicAdd(C + 6, fb ? 1ull : 0ull);
+        if (fb) {  // slots 48..63: count, then up to 15 (pair << 16 | item) records
+            const unsigned long long k = atomicAdd(g_iter_dbg + 48, 1ull);
+            if (k < 15) g_iter_dbg[49 + k] = (static_cast<unsigned long long>(pair) << 16) | unsigned(u);
+        }
         atomicAdd(C + 7, 1ull);
         atomicAdd(C + 8, (a < b) ? 1ull : 0ull);
         if (a < b && !fb) {  // initial-guess error of the tangency solves: bins < 1e-4, 1e-3, 1e-2, 3e-2, 1e-1, more
@@ -1568,6 +1598,11 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
     const double* Wt = L.WT + size_t(pair) * WT_N;
     const double2* AB = L.AB + size_t(pair) * NELU;
     const double* DONp = L.DON + size_t(pair) * U_DON * DON_STRIDE;
+    // tree calls: a walker whose ln_prior is -inf was not solved by k_elements
+    // (prior_rejects); the pair goes straight to the -inf finish (a local
+    // status value only: the status array keeps the model's own code)
+    constexpr int ST_PRIOR_SKIP = -1;
+    const bool prej = CHI && L.prior && prior_rejects(L.prior[L.E == 1 ? pair : pair / L.E], G);
 
     // fused acceptance with one eclipse per walker: the proposal's coordinates
     // (one per lane), the uniform draw and the old ln_prob are fetched here,
@@ -1614,6 +1649,7 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
             sflag[0] = 0;
             if (st != L.status[pair]) const_cast<int*>(L.status)[pair] = st;
         }
+        if (st == ST_OK && prej) st = ST_PRIOR_SKIP;
         __syncthreads();
         if (st == ST_OK) {
             if (windows_unsorted(L, o0, n, sgeo[G_PHI0], tid)) atomicOr(&sflag[0], 1);
@@ -1645,6 +1681,7 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
         // every global load of the prologue is issued before anything waits on
         // one (the status included): a single memory round trip
         st = L.status[pair];
+        if (st == ST_OK && prej) st = ST_PRIOR_SKIP;
         s = G[G_S];
         c = G[G_C];
         ul = G[G_ULIMB];
@@ -1937,7 +1974,7 @@ __global__ __launch_bounds__(GP_BLOCK) void k_gp_like(LikeArgs L)
     const int n = L.off ? L.off[e + 1] - o0 : L.N;
     const double* G = L.geo + size_t(pair) * LFG_NGEO;
     double lle = -INFINITY;
-    if (L.status[pair] == ST_OK && G[G_GP_OK] != 0.0) {
+    if (L.status[pair] == ST_OK && G[G_GP_OK] != 0.0 && !(L.prior && prior_rejects(L.prior[pair / L.E], G))) {
         const double ain = G[G_GP_AIN], aout = G[G_GP_AOUT], lam = G[G_GP_LAM];
         const double dcp = G[G_GP_DCP], phi0 = G[G_PHI0];
         const int e0 = L.gp_ecl[2 * e], e1 = L.gp_ecl[2 * e + 1];
@@ -2379,6 +2416,9 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
     }
     const int npairs = W * T->E;
     ElemSpec X{};
+    X.E = T->E;
+    X.ndim = T->ndim;
+    X.lprior = ws.prior;
     if (sp) {
         const int h = prop->half, hn = 1 - prop->half;
         const size_t P48 = size_t(npairs) * LFG_NGEO;
@@ -2397,8 +2437,6 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
             X.done = ws.done;
             X.bstatus = ws.bstatus;
         }
-        X.E = T->E;
-        X.ndim = T->ndim;
         if (sp->out) {
             for (int c = 0; c < 2; ++c) {
                 SetupArgs& N = X.S[c];
@@ -2421,7 +2459,7 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
             X.nspecblk = ((2 * X.nspec + ELEM_BLOCK - 1) / ELEM_BLOCK + 7) / 8 * 8;  // keeps the pair -> XCD map
         }
     }
-    int rc = run_front(S, ws, st, ev, !kFused, sp ? &X : nullptr, !(sp && sp->in));
+    int rc = run_front(S, ws, st, ev, !kFused, &X, !(sp && sp->in));
     if (rc) return rc;
     double* lle = lnlike_e ? lnlike_e : ws.lle;
     LikeArgs L{ws.geo, ws.status, ws.ab, ws.donor, ws.wts, T->E, T->off, T->max_n, T->x, T->y, T->ye,

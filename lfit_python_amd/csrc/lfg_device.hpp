@@ -312,7 +312,7 @@ __device__ inline bool element_interval(const Roche& R, double Px, double Py, do
     if (uu <= R.Rs2 || uxy <= 0.0 || s <= 0.0) return false;
     const double thc = atan2(-uy, ux);
     const double cosD = (sqrt(uu - R.Rs2) - c * uz) / (s * uxy);
-    if (cosD >= 1.0) return false;
+    if (!(cosD < 1.0)) return false;  // never eclipsed (or non-finite geometry: no Newton on NaN)
     const double Dm = (cosD <= -1.0) ? PI : acos(cosD);
     const double lo = thc - Dm, hi = thc + Dm;
 
@@ -352,6 +352,13 @@ __device__ inline bool element_interval(const Roche& R, double Px, double Py, do
 }
 
 // ---------------------------------------------------------------------------
+#ifdef LFG_ELEM_OOL
+__device__ __noinline__ bool element_interval_ool(const Roche& R, double Px, double Py, double Pz, double s, double c,
+                                                  double Reff, double& a, double& b)
+{
+    return element_interval(R, Px, Py, Pz, s, c, Reff, a, b);
+}
+#endif
 // Fast path for element_interval (same converged answer, ~10x less work).
 // The contact phases are the tangencies of the line of sight with the lobe
 // surface: F1 = Phi(X) - Phi_L1 = 0 and F2 = grad Phi(X).e = 0 at
@@ -530,7 +537,7 @@ __device__ inline bool element_interval_fast(const Roche& R, double Px, double P
     if (uu > R.Rs2 && uxy2 > 0.0 && s > 0.0) {
         const double iuxy = rsqrt(uxy2), uxy = uxy2 * iuxy;
         const double cosD = (sqrt(uu - R.Rs2) - c * uz) * iuxy / s;
-        if (cosD >= 1.0) { a = 1.0; b = -1.0; return false; }
+        if (!(cosD < 1.0)) { a = 1.0; b = -1.0; return false; }  // (non-finite geometry included)
         // theta_c = atan2(-uy, ux): closest approach of the line of sight to D
         const double cc = ux * iuxy, sc = -uy * iuxy;
         const double tc = s * uxy + uz * c;
@@ -580,7 +587,11 @@ __device__ inline bool element_interval_fast(const Roche& R, double Px, double P
 #ifdef LFG_EXP_NOFALLBACK  // timing experiment only: no nested-solver fallback
     a = 1.0; b = -1.0; return false;
 #else
+#ifdef LFG_ELEM_OOL  // experiment: the fallback out of line (its registers off the fast path)
+    return element_interval_ool(R, Px, Py, Pz, s, c, Reff, a, b);
+#else
     return element_interval(R, Px, Py, Pz, s, c, Reff, a, b);
+#endif
 #endif
 }
 
