@@ -73,7 +73,6 @@ struct Ws {
     double* wts;    // [pairs][WT_N] ring / spot weights
     double* prior;
     double* lle;
-    int* done;      // [W] eclipses finished per walker (k_lnlike's fused combine, E > 1)
     double* res;    // [pairs][gp_n] GP trees: residuals y - flux (k_lnlike<2> -> k_gp_like)
     // speculative setup (lfg_stretch_step_half_spec): per half parity h and
     // candidate c (the partner's move rejected / accepted) the k_setup
@@ -107,7 +106,6 @@ Ws carve(void* base, int W, int E, int gp_n = 0, int ndim_spec = 0, int nacc = 0
     ws.wts = reinterpret_cast<double*>(take(pairs * WT_N * sizeof(double)));
     ws.prior = reinterpret_cast<double*>(take(size_t(W) * sizeof(double)));
     ws.lle = reinterpret_cast<double*>(take(pairs * sizeof(double)));
-    ws.done = reinterpret_cast<int*>(take(size_t(W) * sizeof(int)));
     ws.res = gp_n > 0 ? reinterpret_cast<double*>(take(pairs * size_t(gp_n) * sizeof(double))) : nullptr;
     if (ndim_spec > 0) {
         ws.geoC = reinterpret_cast<double*>(take(4 * pairs * LFG_NGEO * sizeof(double)));
@@ -146,7 +144,6 @@ struct SetupArgs {
     int gp;        // GP likelihood: per-pair hyper-parameters and changepoints
     const int* gp_gather;
     const double* gp_base;
-    int* done;     // nullable: per-walker eclipse counters of k_lnlike, zeroed here
     // inline stretch-move proposal (lfg_stretch_step_half; pos nullptr: off):
     // walker w of the batch is the proposal for ensemble walker half * W + w,
     // formed from pos as k_propose does; the walker lanes store it in qout
@@ -366,7 +363,6 @@ __device__ inline void prior_lane(const SetupArgs& A, int w)
     }
     if (qo) A.zfout[w] = (A.ndim - 1.0) * log(P.z);
     A.prior[w] = A.fixed_invalid ? -INFINITY : lp;
-    if (A.done) A.done[w] = 0;
     LFG_CY(8, w, tl);
 #ifdef LFG_PROFILE_SETUP
     if (w < 4096) g_setup_cyc[9][w] = __builtin_amdgcn_s_memrealtime() - trl;
@@ -577,7 +573,6 @@ struct ElemSpec {
     double* prior;
     double* q;
     double* zf;
-    int* done;
     int* bstatus;
     int E, ndim;
     const double* lprior;  // tree calls: the batch's Prior sums (k_setup), prior_rejects skips; nullptr: none
@@ -630,7 +625,6 @@ __global__ __launch_bounds__(ELEM_BLOCK) __attribute__((amdgpu_waves_per_eu(ELEM
                 for (int d = l; d < X.ndim; d += int(blockDim.x)) X.q[size_t(w) * X.ndim + d] = X.qC[cw * X.ndim + d];
                 if (l == LFG_NGEO + 2) X.prior[w] = X.priorC[cw];
                 if (l == LFG_NGEO + 3) X.zf[w] = X.zfC[cw];
-                if (l == LFG_NGEO + 4 && X.done) X.done[w] = 0;
             }
         }
     } else {
@@ -916,7 +910,6 @@ struct LikeArgs {
     // fused k_combine (MODE 1, 2): ln_prob = ln_prior + sum_e ln_like_e
     const double* prior;  // [W] Prior.ln_prob sums + LCModel prior (k_setup)
     double* lnp;          // nullable, [W]
-    int* done;            // [W] counters zeroed by k_setup (E > 1)
     bool combine;         // form ln_prob at all
     // fused stretch-move acceptance (lfg_stretch_lnprob_accept; pos nullptr:
     // off): walker w of this batch is the proposal for ensemble walker
@@ -972,9 +965,6 @@ __device__ inline void combine_walker(const LikeArgs& L, int w)
     }
 }
 
-// called by thread 0 after it wrote lle[pair]: the walker's last finished
-// eclipse forms its ln_prob (E = 1: at once; E > 1: a device-scope counter,
-// with fences so that the other blocks' lle are visible across XCD L2s)
 // end of k_lnlike (all threads; lle[pair] written by thread 0): with one
 // eclipse per walker and fused acceptance, thread 0 decides with the
 // prefetched draw and the copy of the accepted proposal is spread over the
@@ -984,17 +974,9 @@ __device__ inline void finish_walker(const LikeArgs& L, int pair, int tid, bool 
 
 __device__ inline void combine_after(const LikeArgs& L, int pair)
 {
-    if (!L.combine) return;
-    const int w = pair / L.E;
-    if (L.E == 1) {
-        combine_walker(L, w);
-        return;
-    }
-    __threadfence();
-    if (atomicAdd(L.done + w, 1) == L.E - 1) {
-        __threadfence();
-        combine_walker(L, w);
-    }
+    // one eclipse per walker: at once; E > 1: k_combine_walkers does it
+    // after the launch (L.combine is false then)
+    if (L.combine) combine_walker(L, pair / L.E);
 }
 
 // ---- sweeps over phase-sorted tiles of points (MODEL_SPEC 6 restated) ----
@@ -2074,6 +2056,17 @@ __global__ __launch_bounds__(GP_BLOCK) void k_gp_like(LikeArgs L)
 }
 
 // -------------------------------------------------------------- k_combine
+// E > 1: ln_prob (and the fused acceptance) of every walker once all its
+// eclipses' ln_like are written, one lane per walker, in a launch of its own.
+// (The last-finishing block of each walker used to do it after a device-scope
+// fence: on MI355X that fence writes back the block's whole L2, and the 12 288
+// fences of a config-3 launch cost a third of k_lnlike: 898 -> 587 us.)
+__global__ void k_combine_walkers(LikeArgs L)
+{
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w < L.npairs / L.E) combine_walker(L, w);
+}
+
 __global__ void k_combine(int W, int E, const double* __restrict__ prior, const double* __restrict__ geo,
                           double* __restrict__ lle, double* __restrict__ lnp)
 {
@@ -2346,12 +2339,12 @@ int lfg_flux(const double* pars, int W, int P, const double* x, const double* w,
     if (!wsp || ws_bytes < ws.total) return LFG_E_WORKSPACE;
     hipStream_t st = static_cast<hipStream_t>(stream);
     SetupArgs S{pars, W, P, 1, P, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
-                ws.geo, ws.status, ws.prior, ws.bstatus, 0, nullptr, nullptr, nullptr};
+                ws.geo, ws.status, ws.prior, ws.bstatus, 0, nullptr, nullptr};
     int rc = run_front(S, ws, st, nullptr);
     if (rc) return rc;
     if (N > 0) {
         LikeArgs L{ws.geo, ws.status, ws.ab, ws.donor, ws.wts, 1, nullptr, N, x, nullptr, nullptr, w,
-                   nsub, flux, comps, nullptr, W, nullptr, nullptr, nullptr, nullptr, false, nullptr,
+                   nsub, flux, comps, nullptr, W, nullptr, nullptr, nullptr, false, nullptr,
                    nullptr, nullptr, nullptr, 0, 0, 0ull, 0ull, nullptr};
         L.bstatus = ws.bstatus;
         hipLaunchKernelGGL((k_lnlike<0, kFused>), dim3(W), dim3(LIKE_THREADS), 0, st, L);
@@ -2400,7 +2393,7 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
     };
     SetupArgs S{walkers, W, T->ndim, T->E, 18, T->gather, T->npars, T->consts, T->prior_type, T->prior_p1,
                 T->prior_p2, T->prior_norm, T->roche_priors, ws.geo, ws.status, ws.prior, ws.bstatus, T->gp,
-                T->gp_gather, T->gp_base, ws.done};
+                T->gp_gather, T->gp_base};
     S.fixed_invalid = T->fixed_invalid;
     S.prior_c = T->prior_c;
     if (prop) {
@@ -2434,7 +2427,6 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
             X.prior = ws.prior;
             X.q = prop->q;
             X.zf = prop->zfac;
-            X.done = ws.done;
             X.bstatus = ws.bstatus;
         }
         if (sp->out) {
@@ -2452,7 +2444,6 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
                 N.prior = ws.priorC + k * W;
                 N.qout = ws.qC + k * size_t(W) * T->ndim;
                 N.zfout = ws.zfC + k * W;
-                N.done = nullptr;
                 N.jkout = ws.jk + size_t(hn) * W;
             }
             X.nspec = 2 * npairs + W;
@@ -2463,12 +2454,13 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
     if (rc) return rc;
     double* lle = lnlike_e ? lnlike_e : ws.lle;
     LikeArgs L{ws.geo, ws.status, ws.ab, ws.donor, ws.wts, T->E, T->off, T->max_n, T->x, T->y, T->ye,
-               T->w, T->nsub, nullptr, nullptr, lle, npairs, T->gp ? T->gp_ecl : nullptr, ws.prior, lnp, ws.done,
+               T->w, T->nsub, nullptr, nullptr, lle, npairs, T->gp ? T->gp_ecl : nullptr, ws.prior, lnp,
                true, acc ? acc->pos : nullptr, acc ? acc->lnp : nullptr, walkers, acc ? acc->zfac : nullptr,
                T->ndim, acc ? acc->half : 0, acc ? acc->seed : 0ull, acc ? acc->step : 0ull,
                acc ? acc->naccept : nullptr};
     L.bstatus = ws.bstatus;
     L.accflag = (sp && acc) ? ws.accflag : nullptr;  // sharded: k_accept_regen records them
+    L.combine = T->E == 1;  // E > 1: k_combine_walkers after the likelihood kernels
     if (T->gp) {
         L.res = ws.res;
         hipLaunchKernelGGL((k_lnlike<2, kFused>), dim3(npairs), dim3(LIKE_THREADS), 0, st, L);
@@ -2478,6 +2470,10 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
         hipLaunchKernelGGL((k_lnlike<1, kFused>), dim3(npairs), dim3(LIKE_THREADS), 0, st, L);
     }
     if ((rc = launch_ok())) return rc;
+    if (T->E > 1) {
+        hipLaunchKernelGGL(k_combine_walkers, dim3((W + 255) / 256), dim3(256), 0, st, L);
+        if ((rc = launch_ok())) return rc;
+    }
     mark(3);
     return LFG_OK;
 }
@@ -2491,7 +2487,7 @@ int lfg_lnprior(const double* walkers, int W, const lfg_tree* T, double* lnprior
     hipStream_t st = static_cast<hipStream_t>(stream);
     SetupArgs S{walkers, W, T->ndim, T->E, 18, T->gather, T->npars, T->consts, T->prior_type, T->prior_p1,
                 T->prior_p2, T->prior_norm, T->roche_priors, ws.geo, ws.status, ws.prior, ws.bstatus, 0,
-                nullptr, nullptr, nullptr};
+                nullptr, nullptr};
     S.fixed_invalid = T->fixed_invalid;
     S.prior_c = T->prior_c;
     const int nlanes = 2 * W * T->E + W;
@@ -2682,7 +2678,7 @@ int lfg_elements(const double* pars, int W, int P, double* a, double* b, double*
     if (!wsp || ws_bytes < ws.total) return LFG_E_WORKSPACE;
     hipStream_t st = static_cast<hipStream_t>(stream);
     SetupArgs S{pars, W, P, 1, P, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
-                ws.geo, ws.status, ws.prior, ws.bstatus, 0, nullptr, nullptr, nullptr};
+                ws.geo, ws.status, ws.prior, ws.bstatus, 0, nullptr, nullptr};
     int rc = run_front(S, ws, st, nullptr, true);  // the white-box tables come from k_elements
     if (rc) return rc;
     if (a || b || wgt || donor) {

@@ -72,6 +72,47 @@ def test_lnprob_configs_match_oracle(oracle, cfg):
     _same(got, ref, LNP_RTOL)
 
 
+@pytest.mark.parametrize("cfg", ["c2_complex", "c3_tree"])
+def test_prior_rejected_walkers_skip_the_model(oracle, cfg):
+    """Walkers with ln_prior = -inf get -inf without the model being run
+    (Node.ln_prob, model.py:476-498): k_elements and k_lnlike skip them.  An
+    exp2 -> 0 proposal puts the bright-spot strip at ~1e270 (bs_umax), whose
+    elements once sent whole waves into ms-long nested solves."""
+    import time
+    import torch
+    from lfit_python_amd import batch, synthetic
+    if cfg == "c2_complex":
+        m, W = synthetic.config_single(300, flux_fn=_flux_fn), 512
+    else:
+        m, W = synthetic.config_tree(4, 300, flux_fn=_flux_fn), 96
+    t = batch.compile_tree(m)
+    names = m.dynasty_par_names
+    rng = np.random.default_rng(11)
+    p0 = np.array(m.dynasty_par_vals)
+    walk = p0 * (1.0 + 0.002 * rng.standard_normal((W, p0.size)))
+    bad = np.zeros(W, bool)
+    exp2 = [i for i, n in enumerate(names) if n.startswith("exp2")]
+    az = [i for i, n in enumerate(names) if n.startswith("az")]
+    walk[1::4, exp2[0]] = 3e-3      # prior uniform(0.5, 5): out, absurd strip
+    walk[3::8, az[0]] = 200.0       # prior uniform(50, 175): out
+    bad[1::4] = True
+    bad[3::8] = True
+    ev = batch.LnProbEvaluator(t)
+    x = torch.as_tensor(walk, device="cuda")
+    got = ev(x).cpu().numpy()
+    assert np.all(np.isneginf(got[bad]))
+    ref, _, _ = oracle.lnprob_batch(walk, t)
+    _same(got, ref, LNP_RTOL)
+    assert np.isfinite(got[~bad]).sum() >= (~bad).sum() // 2
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(5):
+        ev(x)
+    torch.cuda.synchronize()
+    per = (time.perf_counter() - t0) / 5
+    assert per < 2e-3, "ln_prob of %d walkers took %.2f ms" % (W, per * 1e3)
+
+
 def test_stretch_kernels_match_host_double():
     import torch
     from lfit_python_amd.sampler import HipStretchOps
