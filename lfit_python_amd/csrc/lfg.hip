@@ -2061,10 +2061,53 @@ __global__ __launch_bounds__(GP_BLOCK) void k_gp_like(LikeArgs L)
 // (The last-finishing block of each walker used to do it after a device-scope
 // fence: on MI355X that fence writes back the block's whole L2, and the 12 288
 // fences of a config-3 launch cost a third of k_lnlike: 898 -> 587 us.)
-__global__ void k_combine_walkers(LikeArgs L)
+// One wave per walker: the lanes fetch the E Roche priors and ln_like at
+// once (the walker's chain of 2E dependent-latency loads in one lane was 43 us
+// per config-3 launch), lane 0 adds them in combine_walker's order (the
+// same sums, bit for bit), and the lanes copy an accepted proposal.
+__global__ __launch_bounds__(256) void k_combine_walkers(LikeArgs L)
 {
-    const int w = blockIdx.x * blockDim.x + threadIdx.x;
-    if (w < L.npairs / L.E) combine_walker(L, w);
+    const int w = int(blockIdx.x) * 4 + int(threadIdx.x >> 6), lane = int(threadIdx.x & 63);
+    if (w >= L.npairs / L.E) return;
+    const size_t p0 = size_t(w) * L.E;
+    double lp = L.prior[w];
+    double ll = 0.0;
+    for (int e0 = 0; e0 < L.E; e0 += 64) {
+        const int e = e0 + lane;
+        double g = 0.0, l = 0.0;
+        if (e < L.E) {
+            const double* G = L.geo + (p0 + e) * LFG_NGEO;
+            g = G[G_RPRIOR] + G[G_RPRIOR_BS];
+            l = L.lle[p0 + e];
+        }
+        const int m = min(64, L.E - e0);
+        for (int k = 0; k < m; ++k) {  // in eclipse order, as combine_walker
+            lp += __shfl(g, k, 64);
+            ll += __shfl(l, k, 64);
+        }
+    }
+    double v;
+    if (!isfinite(lp)) {
+        for (int e = lane; e < L.E; e += 64) L.lle[p0 + e] = -INFINITY;
+        v = -INFINITY;
+    } else {
+        v = lp + ll;
+    }
+    if (L.lnp && lane == 0) L.lnp[w] = v;
+    if (!L.pos) return;
+    const int wg = L.half * L.npairs / L.E + w;  // ensemble index (npairs / E = batch walkers)
+    bool acc = false;
+    if (lane == 0) {
+        const uint4 r = draw(L.seed, L.step, L.half, 1, w);
+        acc = log(u53(r.x, r.y)) < L.zfac[w] + v - L.lnp_ens[wg];
+        if (acc) {
+            L.lnp_ens[wg] = v;
+            if (L.naccept) L.naccept[wg] += 1;
+        }
+        if (L.accflag) L.accflag[w] = acc ? 1 : 0;
+    }
+    if (__shfl(acc ? 1 : 0, 0, 64))
+        for (int d = lane; d < L.ndim; d += 64) L.pos[size_t(wg) * L.ndim + d] = L.qprop[size_t(w) * L.ndim + d];
 }
 
 __global__ void k_combine(int W, int E, const double* __restrict__ prior, const double* __restrict__ geo,
@@ -2471,7 +2514,7 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
     }
     if ((rc = launch_ok())) return rc;
     if (T->E > 1) {
-        hipLaunchKernelGGL(k_combine_walkers, dim3((W + 255) / 256), dim3(256), 0, st, L);
+        hipLaunchKernelGGL(k_combine_walkers, dim3((W + 3) / 4), dim3(256), 0, st, L);
         if ((rc = launch_ok())) return rc;
     }
     mark(3);
