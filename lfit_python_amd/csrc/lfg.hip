@@ -30,6 +30,9 @@ constexpr int SETUP_BLOCK = 64;
 #define LFG_ELEM_BLOCK 64  // one wave: the item chunks dispatch at wave granularity (36.0 vs 37.6 us at 256, 36.5 at 128)
 #endif
 constexpr int ELEM_BLOCK = LFG_ELEM_BLOCK;
+#ifndef LFG_ELEM_IPL
+#define LFG_ELEM_IPL 1  // items per k_elements lane
+#endif
 #ifndef ELEM_MINW
 #define ELEM_MINW 5  // minimum waves per SIMD of k_elements (94 VGPRs: the speculative setup lanes spill to fit)
 #endif
@@ -581,56 +584,12 @@ struct ElemSpec {
     int nspecblk;  // leading blocks that run them
 };
 
-__global__ __launch_bounds__(ELEM_BLOCK) __attribute__((amdgpu_waves_per_eu(ELEM_MINW))) void k_elements(const double* __restrict__ geo, int* status, int npairs,
-                                                         double2* __restrict__ AB, double* __restrict__ DON,
-                                                         double* __restrict__ WT, const int* __restrict__ bstatus,
-                                                         ElemSpec X)
+// one k_elements lane's item v of pair `pair` (v >= NUNIQ: the disc ring
+// weights of the last chunk's spare lanes)
+__device__ __forceinline__ void element_lane(int v, int pair, int npairs, const double* __restrict__ G, int st0, int bst,
+                                             int* status, double2* __restrict__ AB, double* __restrict__ DON,
+                                             double* __restrict__ WT, const ElemSpec& X)
 {
-    if (int(blockIdx.x) < X.nspecblk) {  // speculative setup lanes of the next half
-        const int t = int(blockIdx.x) * int(blockDim.x) + int(threadIdx.x);
-        const int c = t < X.nspec ? 0 : 1;
-#ifdef LFG_ELEM_OOL
-        if (t < 2 * X.nspec) setup_any_ool(X.S[c], t - c * X.nspec);
-#else
-        if (t < 2 * X.nspec) setup_any(X.S[c], t - c * X.nspec);
-#endif
-        return;
-    }
-    const unsigned bid = blockIdx.x - unsigned(X.nspecblk);
-    // blocks cover the NUNIQ unique items of every pair in chunks of
-    // blockDim.x (the spot items fill the last chunk); block b takes pair
-    // b % npairs, so that (with npairs a multiple of 8 and blocks dealt
-    // round-robin over the XCDs) a pair's tables are written on the XCD whose
-    // L2 k_lnlike block `pair` reads them from -- speed only.  Item 0 folds
-    // the stream lanes' status into the pair status (MODEL_SPEC 6 order:
-    // setup failures first); every item skips a pair that failed either.
-    const int pair = int(bid % unsigned(npairs));
-    const int v = int(bid / unsigned(npairs)) * int(blockDim.x) + int(threadIdx.x);
-    const double* G = geo + size_t(pair) * LFG_NGEO;
-    int st0, bst;
-    if (X.jk) {
-        const int w = pair / X.E, e = pair - w * X.E;
-        const size_t cp = size_t(X.accflag[X.jk[w]]) * npairs + pair;  // candidate slot of the pair
-        G = X.geoC + cp * LFG_NGEO;
-        st0 = X.statusC[cp];
-        bst = X.bstatusC[cp];
-        if (bid < unsigned(npairs)) {  // the pair's first block: the selected candidate into the standard slots
-            const int l = int(threadIdx.x);
-            double* Gd = const_cast<double*>(geo) + size_t(pair) * LFG_NGEO;
-            if (l < LFG_NGEO) Gd[l] = G[l];
-            if (l == LFG_NGEO) status[pair] = (st0 != ST_OK) ? st0 : bst;
-            if (l == LFG_NGEO + 1) X.bstatus[pair] = bst;
-            if (e == 0) {
-                const size_t cw = size_t(X.accflag[X.jk[w]]) * (npairs / X.E) + w;
-                for (int d = l; d < X.ndim; d += int(blockDim.x)) X.q[size_t(w) * X.ndim + d] = X.qC[cw * X.ndim + d];
-                if (l == LFG_NGEO + 2) X.prior[w] = X.priorC[cw];
-                if (l == LFG_NGEO + 3) X.zf[w] = X.zfC[cw];
-            }
-        }
-    } else {
-        st0 = status[pair];
-        bst = bstatus[pair];
-    }
     if (v >= NUNIQ) {
         // the last chunk's spare lanes: the disc ring weights (MODEL_SPEC
         // 5.2).  Lane NUNIQ + i holds the boundary term P(r_i), i = 0..NDISC_R;
@@ -782,6 +741,63 @@ __global__ __launch_bounds__(ELEM_BLOCK) __attribute__((amdgpu_waves_per_eu(ELEM
     element_interval_fast(R, Px, Py, Pz, s, c, G[G_RCAL], G[G_REFF], a, b);
 #endif
     AB[size_t(pair) * NELU + (u >= U_MAIN ? NU_WDD + (u - U_MAIN) : uslot(u))] = make_double2(a, b);
+}
+
+__global__ __launch_bounds__(ELEM_BLOCK) __attribute__((amdgpu_waves_per_eu(ELEM_MINW))) void k_elements(const double* __restrict__ geo, int* status, int npairs,
+                                                         double2* __restrict__ AB, double* __restrict__ DON,
+                                                         double* __restrict__ WT, const int* __restrict__ bstatus,
+                                                         ElemSpec X)
+{
+    if (int(blockIdx.x) < X.nspecblk) {  // speculative setup lanes of the next half
+        const int t = int(blockIdx.x) * int(blockDim.x) + int(threadIdx.x);
+        const int c = t < X.nspec ? 0 : 1;
+#ifdef LFG_ELEM_OOL
+        if (t < 2 * X.nspec) setup_any_ool(X.S[c], t - c * X.nspec);
+#else
+        if (t < 2 * X.nspec) setup_any(X.S[c], t - c * X.nspec);
+#endif
+        return;
+    }
+    const unsigned bid = blockIdx.x - unsigned(X.nspecblk);
+    // blocks cover the NUNIQ unique items of every pair in chunks of
+    // blockDim.x (the spot items fill the last chunk); block b takes pair
+    // b % npairs, so that (with npairs a multiple of 8 and blocks dealt
+    // round-robin over the XCDs) a pair's tables are written on the XCD whose
+    // L2 k_lnlike block `pair` reads them from -- speed only.  Item 0 folds
+    // the stream lanes' status into the pair status (MODEL_SPEC 6 order:
+    // setup failures first); every item skips a pair that failed either.
+    const int pair = int(bid % unsigned(npairs));
+    // LFG_ELEM_IPL items per lane, one after the other (chunks of
+    // ELEM_BLOCK * LFG_ELEM_IPL items)
+    const int v0 = int(bid / unsigned(npairs)) * (int(blockDim.x) * LFG_ELEM_IPL) + int(threadIdx.x);
+    const double* G = geo + size_t(pair) * LFG_NGEO;
+    int st0, bst;
+    if (X.jk) {
+        const int w = pair / X.E, e = pair - w * X.E;
+        const size_t cp = size_t(X.accflag[X.jk[w]]) * npairs + pair;  // candidate slot of the pair
+        G = X.geoC + cp * LFG_NGEO;
+        st0 = X.statusC[cp];
+        bst = X.bstatusC[cp];
+        if (bid < unsigned(npairs)) {  // the pair's first block: the selected candidate into the standard slots
+            const int l = int(threadIdx.x);
+            double* Gd = const_cast<double*>(geo) + size_t(pair) * LFG_NGEO;
+            if (l < LFG_NGEO) Gd[l] = G[l];
+            if (l == LFG_NGEO) status[pair] = (st0 != ST_OK) ? st0 : bst;
+            if (l == LFG_NGEO + 1) X.bstatus[pair] = bst;
+            if (e == 0) {
+                const size_t cw = size_t(X.accflag[X.jk[w]]) * (npairs / X.E) + w;
+                for (int d = l; d < X.ndim; d += int(blockDim.x)) X.q[size_t(w) * X.ndim + d] = X.qC[cw * X.ndim + d];
+                if (l == LFG_NGEO + 2) X.prior[w] = X.priorC[cw];
+                if (l == LFG_NGEO + 3) X.zf[w] = X.zfC[cw];
+            }
+        }
+    } else {
+        st0 = status[pair];
+        bst = bstatus[pair];
+    }
+#pragma unroll 1
+    for (int k = 0; k < LFG_ELEM_IPL; ++k)
+        element_lane(v0 + k * int(blockDim.x), pair, npairs, G, st0, bst, status, AB, DON, WT, X);
 }
 
 // interval of element k (MODEL_SPEC 5 numbering) from a pair's table: the
@@ -2347,7 +2363,7 @@ int run_front(const SetupArgs& S, const Ws& ws, hipStream_t st, void* const* ev,
     }
     mark(1);
     if (elements) {
-        constexpr int chunks = (NUNIQ + ELEM_BLOCK - 1) / ELEM_BLOCK;
+        constexpr int chunks = (NUNIQ + ELEM_BLOCK * LFG_ELEM_IPL - 1) / (ELEM_BLOCK * LFG_ELEM_IPL);
         ElemSpec none{};
         const ElemSpec& XS = X ? *X : none;
         hipLaunchKernelGGL(k_elements, dim3(unsigned(npairs) * chunks + unsigned(XS.nspecblk)), dim3(ELEM_BLOCK), 0,
