@@ -451,6 +451,10 @@ def run(args):
                 "basis": "counted algorithmic FP64 FLOPs per walker-eclipse eval x evals/s per GPU over the "
                          "whole step (MODEL_SPEC 11): F_setup + 900 roots x F_geom + N S (1500 x 3 + 400 x 6 + 40)",
                 "flops_per_walker_eval": f_eval,
+                "note": (None if tf <= FP64_PEAK_TFLOPS else
+                         "the direct-form count of SURVEY 8(d) exceeds the FP64 peak here: k_lnlike's sweep forms "
+                         "the same sums with O(N S + N_el) work per pair, so frac > 1 is not a utilisation "
+                         "(MODEL_SPEC 11)"),
                 "flops_per_pair": fpp,
                 "kernel": {"name": kname, "avg_launch_ms": avg_dom, "launches_timed": ncalls,
                            "alg_flops_per_launch": dom_flops, "achieved": dom_tf,
