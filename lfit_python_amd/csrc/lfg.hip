@@ -77,6 +77,8 @@ struct Ws {
     double* prior;
     double* lle;
     double* res;    // [pairs][gp_n] GP trees: residuals y - flux (k_lnlike<2> -> k_gp_like)
+    double* gpx;    // [pairs][gp_n] GP trees: e^{-lam dx} of each point (k_lnlike<2> -> k_gp_like)
+    int* gpb;       // [pairs][gp_n] GP trees: each point's changepoint block
     // speculative setup (lfg_stretch_step_half_spec): per half parity h and
     // candidate c (the partner's move rejected / accepted) the k_setup
     // outputs of the next half, formed inside the previous half's k_elements
@@ -110,6 +112,8 @@ Ws carve(void* base, int W, int E, int gp_n = 0, int ndim_spec = 0, int nacc = 0
     ws.prior = reinterpret_cast<double*>(take(size_t(W) * sizeof(double)));
     ws.lle = reinterpret_cast<double*>(take(pairs * sizeof(double)));
     ws.res = gp_n > 0 ? reinterpret_cast<double*>(take(pairs * size_t(gp_n) * sizeof(double))) : nullptr;
+    ws.gpx = gp_n > 0 ? reinterpret_cast<double*>(take(pairs * size_t(gp_n) * sizeof(double))) : nullptr;
+    ws.gpb = gp_n > 0 ? reinterpret_cast<int*>(take(pairs * size_t(gp_n) * sizeof(int))) : nullptr;
     if (ndim_spec > 0) {
         ws.geoC = reinterpret_cast<double*>(take(4 * pairs * LFG_NGEO * sizeof(double)));
         ws.statusC = reinterpret_cast<int*>(take(4 * pairs * sizeof(int)));
@@ -938,6 +942,8 @@ struct LikeArgs {
     unsigned long long seed, step;
     int* naccept;
     double* res;  // MODE 2: [pairs][N] residuals for k_gp_like
+    double* gpx;  // MODE 2: [pairs][N] e^{-lam dx} per point (the filter's transitions)
+    int* gpb;     // MODE 2: [pairs][N] changepoint block per point
     const int* bstatus;  // fused element phase: the stream lanes' status (folded into status here)
     int* accflag;        // nullable, [W]: 1 where the walker's move was accepted (speculative setup)
 };
@@ -1601,6 +1607,21 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
     // status value only: the status array keeps the model's own code)
     constexpr int ST_PRIOR_SKIP = -1;
     const bool prej = CHI && L.prior && prior_rejects(L.prior[L.E == 1 ? pair : pair / L.E], G);
+    if constexpr (GP) {
+        // the Kalman filter's state-independent factors of the pair's points
+        // (e^{-lam dx}, changepoint block), for k_gp_like: one point per
+        // thread here instead of ~60 instructions per point in the filter's
+        // serial lane (formed before the prologue: no registers held)
+        const double lam = G[G_GP_LAM], dcp = G[G_GP_DCP], ph0 = G[G_PHI0];
+        const int ge0 = L.gp_ecl[2 * e], ge1 = L.gp_ecl[2 * e + 1];
+        for (int p = tid; p < n; p += LIKE_THREADS) {
+            const double xp = L.x[o0 + p];
+            const double dx = xp - (p > 0 ? L.x[o0 + p - 1] : xp);
+            const size_t q = size_t(pair) * L.N + p;
+            L.gpx[q] = exp(-(lam * dx));
+            L.gpb[q] = gp_block(xp, ge0, ge1, dcp, ph0);
+        }
+    }
 
     // fused acceptance with one eclipse per walker: the proposal's coordinates
     // (one per lane), the uniform draw and the old ln_prob are fetched here,
@@ -1958,7 +1979,10 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
 // + n ln 2 pi) and, as k_lnlike does, ln_prob and the acceptance of the
 // walker once its last eclipse is in.
 constexpr int GP_BLOCK = 64;
-constexpr int GP_CHUNK = 8;
+#ifndef LFG_GP_CHUNK
+#define LFG_GP_CHUNK 8
+#endif
+constexpr int GP_CHUNK = LFG_GP_CHUNK;
 #ifndef GP_LANES
 #define GP_LANES 64  // pairs per wave (the other lanes idle)
 #endif
@@ -1977,8 +2001,11 @@ __global__ __launch_bounds__(GP_BLOCK) void k_gp_like(LikeArgs L)
         const double dcp = G[G_GP_DCP], phi0 = G[G_PHI0];
         const int e0 = L.gp_ecl[2 * e], e1 = L.gp_ecl[2 * e + 1];
         const double* r = L.res + size_t(pair) * L.N;
+        const double* gx = L.gpx + size_t(pair) * L.N;
+        const int* gb = L.gpb + size_t(pair) * L.N;
         const double* xs = L.x + o0;
         const double* yes = L.ye + o0;
+        (void)dcp; (void)phi0; (void)e0; (void)e1;
         // state (D = P - Pinf, MODEL_SPEC 10.4)
         double m0 = 0.0, m1 = 0.0, m2 = 0.0, m3 = 0.0;
         double d00 = 0.0, d01 = 0.0, d11 = 0.0, d22 = 0.0, d23 = 0.0, d33 = 0.0;
@@ -1989,35 +2016,38 @@ __global__ __launch_bounds__(GP_BLOCK) void k_gp_like(LikeArgs L)
         // points in chunks of GP_CHUNK: the chunk's loads are issued one
         // chunk ahead, its transitions and blocks computed side by side,
         // so that only the recursion itself is serial
-        double cx[GP_CHUNK], cy[GP_CHUNK], cr[GP_CHUNK];
-        auto fetch = [&](int p0, double* X, double* Y, double* Rr) {
+        double cx[GP_CHUNK], cy[GP_CHUNK], cr[GP_CHUNK], ce[GP_CHUNK];
+        int cb[GP_CHUNK];
+        auto fetch = [&](int p0) {
 #pragma unroll
             for (int k = 0; k < GP_CHUNK; ++k) {
                 const int q = min(p0 + k, n - 1);
-                X[k] = xs[q];
-                Y[k] = yes[q];
-                Rr[k] = r[q];
+                cx[k] = xs[q];
+                cy[k] = yes[q];
+                cr[k] = r[q];
+                ce[k] = gx[q];
+                cb[k] = gb[q];
             }
         };
-        if (n > 0) fetch(0, cx, cy, cr);
+        if (n > 0) fetch(0);
         for (int p0 = 0; p0 < n; p0 += GP_CHUNK) {
             double a00[GP_CHUNK], a01[GP_CHUNK], a10[GP_CHUNK], a11[GP_CHUNK], ye2[GP_CHUNK], rv[GP_CHUNK];
             int blk[GP_CHUNK];
 #pragma unroll
             for (int k = 0; k < GP_CHUNK; ++k) {
                 const double dd = cx[k] - (k ? cx[k - 1] : xprev);
-                const double u = lam * dd, ex = exp(-u);
+                const double u = lam * dd, ex = ce[k];  // e^{-u}, formed in k_lnlike<2>
                 a00[k] = ex * (1.0 + u);
                 a01[k] = ex * dd;
                 a10[k] = -ex * lam * u;
                 a11[k] = ex * (1.0 - u);
                 ye2[k] = cy[k] * cy[k];
                 rv[k] = cr[k];
-                blk[k] = gp_block(cx[k], e0, e1, dcp, phi0);
+                blk[k] = cb[k];
                 bad = bad || (p0 + k < n && p0 + k > 0 && !(dd >= 0.0)) || (p0 + k < n && !isfinite(cr[k]));
             }
             xprev = cx[GP_CHUNK - 1];
-            if (p0 + GP_CHUNK < n) fetch(p0 + GP_CHUNK, cx, cy, cr);  // in flight during the recursion
+            if (p0 + GP_CHUNK < n) fetch(p0 + GP_CHUNK);  // in flight during the recursion
             double prodS = 1.0;  // one log per chunk (S ~ ye^2: eight factors stay far from underflow)
 #pragma unroll
             for (int k = 0; k < GP_CHUNK; ++k) {
@@ -2522,6 +2552,8 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
     L.combine = T->E == 1;  // E > 1: k_combine_walkers after the likelihood kernels
     if (T->gp) {
         L.res = ws.res;
+        L.gpx = ws.gpx;
+        L.gpb = ws.gpb;
         hipLaunchKernelGGL((k_lnlike<2, kFused>), dim3(npairs), dim3(LIKE_THREADS), 0, st, L);
         if ((rc = launch_ok())) return rc;
         hipLaunchKernelGGL(k_gp_like, dim3((npairs + GP_LANES - 1) / GP_LANES), dim3(GP_BLOCK), 0, st, L);
