@@ -92,6 +92,19 @@ __device__ __forceinline__ double rcp_fast(double x)
     return fma(y, fma(-x, y, 1.0), y);
 }
 
+// 1/x for a Newton step's length only (the step's direction and size need a
+// few digits: the root is fixed by F = 0, and a relative error e in the
+// step leaves e |dth| after it, ~1e-7 x 3e-8 at the last step): the raw
+// v_rcp_f64.  LFG_STEP_RCP_EXACT restores rcp_fast (A/B).
+__device__ __forceinline__ double rcp_step(double x)
+{
+#ifdef LFG_STEP_RCP_EXACT
+    return rcp_fast(x);
+#else
+    return __builtin_amdgcn_rcp(x);
+#endif
+}
+
 __device__ __forceinline__ double rpot(const Roche& R, double x, double y, double z)
 {
     const double dx = x - 1.0;
@@ -451,12 +464,12 @@ __device__ __forceinline__ void tangency_step(const Roche& R, double Px, double 
     const double F1 = o.phi - R.pl1;
     const double J11 = T.t * o.gth;
     const double J21 = T.t * o.etHe + o.gth, J22 = o.eHe;
-    const double iJ22 = rcp_fast(J22);
+    const double iJ22 = rcp_step(J22);
     const double dt0 = -o.F2 * iJ22;
     const double F1m = fma(0.5 * o.F2, dt0, F1);  // F1 - F2^2 / (2 J22)
     const double den = fma(J21, dt0, J11);
     const bool bad = !(J22 != 0.0) || !(den != 0.0);
-    double dth = -F1m * rcp_fast(den);
+    double dth = -F1m * rcp_step(den);
     dth = fmin(fmax(dth, -0.05), 0.05);
     const double dt = fma(-J21 * iJ22, dth, dt0);
     T.th += dth;
