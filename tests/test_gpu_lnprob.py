@@ -113,6 +113,39 @@ def test_prior_rejected_walkers_skip_the_model(oracle, cfg):
     assert per < 2e-3, "ln_prob of %d walkers took %.2f ms" % (W, per * 1e3)
 
 
+def test_long_chain_keeps_its_pace():
+    """A config-2 chain (1024 walkers) must not slow down as it leaves the
+    starting ball: proposals outside the prior box once ran the nested
+    solver on non-finite geometry for milliseconds (tools/chain_drift.py).
+    Blocks of 30 steps after the first 60 (the failure set in from step
+    ~150): no block may take twice the fastest (the failure was 2.5-6x)."""
+    import time
+    import torch
+    from lfit_python_amd import batch, sampler, synthetic
+    m = synthetic.config_single(300, flux_fn=_flux_fn)
+    t = batch.compile_tree(m)
+    W = 1024
+    ev = batch.LnProbEvaluator(t, max_walkers=W)
+    p0 = np.array(m.dynasty_par_vals)
+    init = sampler.initialise_walkers(p0, sampler.comp_scatter(m.dynasty_par_names, 0.1), W,
+                                      lambda p: ev(torch.as_tensor(p, device="cuda")).cpu().numpy(), seed=7)
+    S = sampler.EnsembleSampler(W, t.ndim, ev, seed=7)
+    S.set_state(init)
+    for _ in range(60):
+        S.step()
+    blocks = []
+    for _ in range(8):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(30):
+            S.step()
+        torch.cuda.synchronize()
+        blocks.append(time.perf_counter() - t0)
+    S.close()
+    assert max(blocks) < 2.0 * min(blocks), "30-step blocks (ms): %s" % np.round(np.array(blocks) * 1e3, 2)
+    assert np.all(np.isfinite(S.lnp.cpu().numpy()))
+
+
 def test_stretch_kernels_match_host_double():
     import torch
     from lfit_python_amd.sampler import HipStretchOps
