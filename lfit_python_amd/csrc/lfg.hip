@@ -278,8 +278,12 @@ __device__ inline void bspot_lane(const SetupArgs& A, int t)
     if (a1 > 0.0 && a2 > 0.0 && isfinite(a1) && isfinite(a2)) {  // else the setup lane fails the pair
         const double upk = pow(a1 / a2, 1.0 / a2);
         const double lnpk = a1 * log(upk) - pow(upk, a2);
-        G[G_UPK] = upk; G[G_UMAX] = bs_umax(a1, a2, lnpk); G[G_LNPK] = lnpk;
+        const double umax = bs_umax(a1, a2, lnpk);
+        G[G_UPK] = upk; G[G_UMAX] = umax; G[G_LNPK] = lnpk;
         G[G_EXP1] = a1; G[G_EXP2] = a2;
+        // a profile that over- or underflows (exp2 -> 0) is bad geometry,
+        // checked after the stream as the oracle does (MODEL_SPEC 6)
+        if (st == ST_OK && !(isfinite(upk) && isfinite(lnpk) && isfinite(umax))) st = ST_BAD_GEOMETRY;
     }
     A.bstatus[t] = st;
     LFG_CY(7, t, tl);
