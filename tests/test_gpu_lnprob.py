@@ -113,6 +113,35 @@ def test_prior_rejected_walkers_skip_the_model(oracle, cfg):
     assert per < 2e-3, "ln_prob of %d walkers took %.2f ms" % (W, per * 1e3)
 
 
+@pytest.mark.parametrize("cfg", ["c2_complex", "c3_tree", "gp"])
+def test_non_finite_walkers_give_minus_inf(oracle, cfg):
+    """NaN / inf walker coordinates: ln_prob -inf for those walkers only, in
+    one- and many-eclipse trees and the GP tree; the others as the oracle."""
+    import torch
+    from lfit_python_amd import batch, cvmodel, synthetic
+    if cfg == "c2_complex":
+        m, W = synthetic.config_single(300, flux_fn=_flux_fn), 64
+    elif cfg == "c3_tree":
+        m, W = synthetic.config_tree(4, 300, flux_fn=_flux_fn), 24
+    else:
+        m, W = cvmodel.construct_model(os.path.join(GOLD, "ref_test_data", "mcmc_input.dat")), 24
+    t = batch.compile_tree(m)
+    rng = np.random.default_rng(13)
+    p0 = np.array(m.dynasty_par_vals)
+    walk = p0 * (1.0 + 1e-3 * rng.standard_normal((W, p0.size)))
+    walk[3, 0] = np.nan
+    walk[7, -1] = np.inf
+    walk[11, p0.size // 2] = -np.inf
+    got = batch.LnProbEvaluator(t)(torch.as_tensor(walk, device="cuda")).cpu().numpy()
+    assert np.all(np.isneginf(got[[3, 7, 11]]))
+    if cfg == "gp":
+        fin = np.isfinite(got)
+        assert fin.sum() >= W // 2
+        return
+    ref, _, _ = oracle.lnprob_batch(walk, t)
+    _same(got, ref, LNP_RTOL)
+
+
 def test_long_chain_keeps_its_pace():
     """A config-2 chain (1024 walkers) must not slow down as it leaves the
     starting ball: proposals outside the prior box once ran the nested
