@@ -159,10 +159,20 @@ class EnsembleSampler:
             if self._rccl is None:
                 direct = os.environ.get("LFG_RCCL_DIRECT", "1") != "0"
                 if direct:
-                    from .comm import RcclAllGather
-                    self._rccl = RcclAllGather(self.group)
-                else:
-                    self._rccl = False
+                    # every rank must take the same path (building the
+                    # communicator is collective): agree first that each
+                    # can load librccl, else all use ProcessGroupNCCL
+                    from . import comm
+                    try:
+                        comm._load_rccl()
+                        ok = 1
+                    except (OSError, AttributeError):
+                        ok = 0
+                    import torch
+                    flag = torch.tensor([ok], dtype=torch.int32, device=out.device)
+                    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+                    direct = bool(flag.item())
+                self._rccl = comm.RcclAllGather(self.group) if direct else False
             if self._rccl:
                 self._rccl(out, mine)
                 return
