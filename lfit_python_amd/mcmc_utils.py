@@ -7,6 +7,7 @@ device-resident EnsembleSampler: same names, arguments and file formats.
                                                                 mcmc_utils.py:135-183
   flatchain(chain, npars=None, nskip=0, thin=1)                 mcmc_utils.py:242-249
   readchain(file) / readchain_dask(file)                        mcmc_utils.py:252-300
+  readflatchain(file)                                           mcmc_utils.py:303-306
 
 The emcee RNG state the reference threads from the burn-in into production
 (`state` -> `rstate0`) is the sampler's Philox counter here
@@ -46,20 +47,26 @@ def batched_ln_prior(evaluator):
 
 def run_burnin(sampler, startPos, nSteps, storechain=False, progress=False):
     """Burn-in (mcmc_utils.py:114-132): returns (pos, prob, state), with
-    state the RNG counter to hand to run_mcmc_save."""
-    pos, prob = sampler.run_mcmc(startPos, nSteps, store=storechain)
-    return pos, prob, sampler.random_state
+    state the RNG counter to hand to run_mcmc_save.  The steps run back to
+    back on the device (EnsembleSampler.run_mcmc); the reference's
+    `for pos, prob, state in sampler.sample(...)` loop also works on the
+    sampler, one host copy per step."""
+    return sampler.run_mcmc(startPos, nSteps, storechain=storechain)
 
 
-def run_mcmc_save(sampler, startPos, nSteps, rState, file, col_names='', progress=False, chunk=None, lnp0=None):
+def run_mcmc_save(sampler, startPos, nSteps, rState, file, col_names='', progress=False, chunk=None,
+                  lnprob0=None, **kwargs):
     """Production run written to `file` (mcmc_utils.py:135-183): the header
     line col_names, then '{k:4d} {values} {ln_prob:f}' per walker per step.
     rState (from run_burnin) continues the burn-in's random stream; None
-    keeps the sampler's own."""
+    keeps the sampler's own.  Afterwards sampler.chain holds every step, as
+    (nwalkers, nSteps, npars) like emcee's.  With torch.distributed every rank
+    runs the steps (the ensemble is replicated) and rank 0 alone writes."""
     if rState is not None:
         sampler.random_state = rState
     W, ndim = sampler.W, sampler.ndim
-    if file:
+    writer = bool(file) and getattr(sampler, "rank", 0) == 0
+    if writer:
         with open(file, "w") as fh:
             fh.write(col_names)
             if col_names:
@@ -68,10 +75,10 @@ def run_mcmc_save(sampler, startPos, nSteps, rState, file, col_names='', progres
     done, first = 0, True
     while done < nSteps:
         k = min(chunk, nSteps - done)
-        sampler.run_mcmc(startPos if first else None, k, store=True, lnp0=lnp0 if first else None)
-        if file:
-            _sampler.write_chain(file, None, sampler.chain.cpu().numpy(), sampler.lnprob_chain.cpu().numpy(),
-                                 mode="a")
+        sampler.run_mcmc(startPos if first else None, k, storechain=True, lnprob0=lnprob0 if first else None)
+        if writer:
+            ch, lp = sampler.last_run()
+            _sampler.write_chain(file, None, ch.cpu().numpy(), lp.cpu().numpy(), mode="a")
         first = False
         done += k
     return sampler
@@ -80,6 +87,8 @@ def run_mcmc_save(sampler, startPos, nSteps, rState, file, col_names='', progres
 def flatchain(chain, npars=None, nskip=0, thin=1):
     """All walkers' samples as one [n, npars] array, skipping the first nskip
     steps and keeping every thin-th (mcmc_utils.py:242-249)."""
+    if hasattr(chain, "cpu"):  # a device tensor
+        chain = chain.cpu().numpy()
     chain = np.asarray(chain)
     if npars is None:
         npars = chain.shape[2]
@@ -96,3 +105,10 @@ def readchain_dask(file, **kwargs):
     """The reference's threaded reader (mcmc_utils.py:275-300) falls back to
     readchain when dask is absent; so does this one (same result)."""
     return readchain(file, **kwargs)
+
+
+def readflatchain(file):
+    """A whitespace-separated table read with no header row (e.g. a
+    flattened chain) as one array (mcmc_utils.py:303-306: pandas, header=None)."""
+    import pandas as pd
+    return np.array(pd.read_csv(file, header=None, sep=r"\s+", float_precision="round_trip"))

@@ -118,11 +118,11 @@ def run(input_file, quiet=False, debug=False, seed=0, chain_file="chain_prod.txt
     p0 = sampler.initialise_walkers(np.asarray(pars), s1, nwalkers, prior_fn, seed=rng_seed)
 
     say("\n\nExecuting the burn-in phase...")
-    pos, prob = S.run_mcmc(p0, rc["nburn"], store=False)
+    pos, prob, state = S.run_mcmc(p0, rc["nburn"], storechain=False)
     if rc["double_burnin"]:
         say("Executing the second burn-in phase")
         p0 = sampler.initialise_walkers(pos[np.argmax(prob)], s2, nwalkers, prior_fn, seed=rng_seed + 1)
-        pos, prob = S.run_mcmc(p0, rc["nburn"], store=False)
+        pos, prob, state = S.run_mcmc(p0, rc["nburn"], storechain=False)
 
     S.reset()  # clears the counters; the RNG stream carries on (emcee's rstate0=rState)
     say("Starting the main MCMC chain. Probably going to take a while!")
@@ -132,9 +132,10 @@ def run(input_file, quiet=False, debug=False, seed=0, chain_file="chain_prod.txt
     done = 0
     while done < nprod:
         k = min(chunk, nprod - done)
-        S.run_mcmc(None if not first else pos, k, store=True, lnp0=None if not first else prob)
+        S.run_mcmc(None if not first else pos, k, storechain=True, lnprob0=None if not first else prob)
         if rank == 0:
-            sampler.write_chain(chain_file, names, S.chain.cpu().numpy(), S.lnprob_chain.cpu().numpy(),
+            ch, lp = S.last_run()
+            sampler.write_chain(chain_file, names, ch.cpu().numpy(), lp.cpu().numpy(),
                                 mode="w" if first else "a")
         first = False
         done += k

@@ -40,6 +40,11 @@ def comp_scatter(names, scatter):
     return out
 
 
+def _host(t):
+    """a host copy of a tensor (never a view of device-side or live state)"""
+    return t.cpu().numpy() if t.device.type != "cpu" else t.numpy().copy()
+
+
 class HipStretchOps:
     """The stretch move's two device kernels (include/lfg.h)."""
 
@@ -119,8 +124,8 @@ class EnsembleSampler:
         # so the production run after reset() never replays burn-in draws
         # (the reference hands the burn-in RNG state on, mcmc_utils.py:135-183)
         self.rng_step = 0
-        self.chain = None
-        self.lnprob_chain = None
+        self._chunks = []  # stored chain: device (chain [n, W, ndim], lnprob [n, W]) per run
+        self._cat = None
         self.timer = None  # optional callable(walkers) -> lnp used instead of self.ev
         # one process, HIP moves, an evaluator with the fused entry: proposal,
         # ln_prob and acceptance in one launch sequence (lfg_stretch_step_half);
@@ -320,21 +325,114 @@ class EnsembleSampler:
             self._rccl.close()
         self._rccl = None
 
-    def run_mcmc(self, p0, nsteps, store=True, lnp0=None):
-        """emcee-style run; returns (pos, lnp) as numpy.  With store=True the
-        chain [nsteps, W, ndim] and ln_prob [nsteps, W] stay on the device."""
+    # ---- emcee 2.x surface (EnsembleSampler.sample / run_mcmc / chain /
+    # lnprobability / flatchain / reset), as the reference drives it:
+    # mcmc_utils.py:114-183 (sample generators), mcmcfit.py:313-341 (reset,
+    # chain as (nwalkers, nsteps, npars) into utils.flatchain(..., thin=10))
+    def _begin(self, p0, lnprob0, rstate0, iterations, thin, store):
+        """common start of sample() / run_mcmc(): state, RNG counter, and a
+        device chunk [iterations // thin, W, ndim] appended to the chain"""
         import torch
+        if rstate0 is not None:
+            self.random_state = rstate0
         if p0 is not None:
-            self.set_state(p0, lnp0)
-        if store:
-            self.chain = torch.empty((nsteps, self.W, self.ndim), dtype=torch.float64, device=self.dev)
-            self.lnprob_chain = torch.empty((nsteps, self.W), dtype=torch.float64, device=self.dev)
-        for i in range(nsteps):
+            self.set_state(p0, lnprob0)
+        thin = max(1, int(thin))
+        if not store:
+            return None, thin
+        n = -(-int(iterations) // thin)  # steps i with i % thin == 0 (emcee 2.x stores those)
+        buf = (torch.empty((n, self.W, self.ndim), dtype=torch.float64, device=self.dev),
+               torch.empty((n, self.W), dtype=torch.float64, device=self.dev))
+        self._chunks.append(buf)
+        self._cat = None
+        return buf, thin
+
+    def _store(self, buf, i, thin):
+        if buf is not None and i % thin == 0:
+            buf[0][i // thin].copy_(self.pos)
+            buf[1][i // thin].copy_(self.lnp)
+
+    def sample(self, p0=None, lnprob0=None, rstate0=None, blobs0=None, iterations=1, thin=1,
+               storechain=True, store=None, skip_initial_state_check=False, **kwargs):
+        """emcee 2.x EnsembleSampler.sample: a generator over `iterations`
+        steps yielding (pos [W, ndim], lnprob [W], state) as host arrays after
+        each step (mcmc_utils.py:121-126, 151-164).  `p0` None continues from
+        the current state; `rstate0` sets the RNG counter (random_state);
+        storechain (emcee 2.x) / store (emcee 3) append every thin-th step to
+        the chain.  Each yield copies the ensemble to the host: the bulk,
+        sync-free path is run_mcmc()."""
+        buf, thin = self._begin(p0, lnprob0, rstate0, iterations,
+                                thin, storechain if store is None else store)
+        for i in range(int(iterations)):
             self.step()
-            if store:
-                self.chain[i].copy_(self.pos)
-                self.lnprob_chain[i].copy_(self.lnp)
-        return self.pos.cpu().numpy(), self.lnp.cpu().numpy()
+            self._store(buf, i, thin)
+            yield _host(self.pos), _host(self.lnp), self.random_state
+
+    def run_mcmc(self, pos0, N, rstate0=None, lnprob0=None, storechain=True, store=None, thin=1, **kwargs):
+        """emcee 2.x run_mcmc: N steps from pos0 (None: the current state);
+        returns (pos, lnprob, state) of the last step as host arrays.  The
+        steps are launched back to back and the stored chain stays on the
+        device (chain_dev) until it is read."""
+        buf, thin = self._begin(pos0, lnprob0, rstate0, N, thin, storechain if store is None else store)
+        for i in range(int(N)):
+            self.step()
+            self._store(buf, i, thin)
+        return _host(self.pos), _host(self.lnp), self.random_state
+
+    def _concat(self):
+        import torch
+        if self._cat is None:
+            if not self._chunks:
+                self._cat = (torch.empty((0, self.W, self.ndim), dtype=torch.float64, device=self.dev),
+                             torch.empty((0, self.W), dtype=torch.float64, device=self.dev))
+            elif len(self._chunks) == 1:
+                self._cat = self._chunks[0]
+            else:
+                self._cat = (torch.cat([c for c, _ in self._chunks]), torch.cat([l for _, l in self._chunks]))
+                self._chunks = [self._cat]
+        return self._cat
+
+    @property
+    def chain_dev(self):
+        """the stored chain on the device, step-major [nsteps, W, ndim]"""
+        return self._concat()[0]
+
+    @property
+    def lnprob_dev(self):
+        """the stored ln_prob on the device, [nsteps, W]"""
+        return self._concat()[1]
+
+    def last_run(self):
+        """(chain [n, W, ndim], lnprob [n, W]) device views of the most recent
+        stored sample()/run_mcmc() call (bulk chain_prod.txt writes)"""
+        return self._chunks[-1] if self._chunks else self._concat()
+
+    @property
+    def chain(self):
+        """emcee's chain: host array (nwalkers, nsteps, ndim)"""
+        return _host(self.chain_dev.permute(1, 0, 2).contiguous())
+
+    @property
+    def lnprobability(self):
+        """emcee's lnprobability: host array (nwalkers, nsteps)"""
+        return _host(self.lnprob_dev.t().contiguous())
+
+    @property
+    def flatchain(self):
+        return self.chain.reshape((-1, self.ndim))
+
+    @property
+    def flatlnprobability(self):
+        return self.lnprobability.reshape(-1)
+
+    @property
+    def iterations(self):
+        """emcee 2.x's step counter (cleared by reset())"""
+        return self.iteration
+
+    @property
+    def naccepted(self):
+        return self.naccept.cpu().numpy()
 
     @property
     def acceptance_fraction(self):
@@ -345,7 +443,8 @@ class EnsembleSampler:
         acceptance counters; the RNG stream carries on (rng_step is kept)."""
         self.iteration = 0
         self.naccept.zero_()
-        self.chain = self.lnprob_chain = None
+        self._chunks = []
+        self._cat = None
 
     @property
     def random_state(self):

@@ -43,3 +43,31 @@ def phase_grid(n=300, lo=-0.3, hi=0.3):
     x = np.linspace(lo, hi, n)
     w = np.mean(np.diff(x)) * np.ones_like(x) / 2.0
     return x, w
+
+
+# ---- the reference's sampler call patterns (emcee 2.x surface)
+def pattern_run_burnin(sampler, startPos, nSteps, storechain=False):
+    """mcmc_utils.run_burnin's use of the sampler (mcmc_utils.py:114-132):
+    iterate sample() to the end, keep the last (pos, prob, state)"""
+    try:
+        for pos, prob, state in sampler.sample(startPos, iterations=nSteps, storechain=storechain):
+            pass
+    except TypeError:  # emcee 3 spelling
+        for pos, prob, state in sampler.sample(startPos, iterations=nSteps, store=storechain):
+            pass
+    return pos, prob, state
+
+
+def pattern_run_mcmc_save(sampler, startPos, nSteps, rState, file, col_names=''):
+    """mcmc_utils.run_mcmc_save's use of the sampler (mcmc_utils.py:135-164):
+    sample() with rstate0 and store=True, one appended row per walker per step"""
+    with open(file, "w") as fh:
+        fh.write(col_names)
+        if col_names:
+            fh.write("\n")
+    for pos, prob, state in sampler.sample(startPos, iterations=nSteps, rstate0=rState, store=True,
+                                           skip_initial_state_check=True):
+        for k in range(pos.shape[0]):
+            with open(file, "a") as fh:
+                fh.write("{0:4d} {1:s} {2:f}\n".format(k, " ".join(map(str, pos[k])), prob[k]))
+    return sampler

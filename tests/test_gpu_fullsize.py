@@ -125,7 +125,7 @@ def test_config4_eight_shards_bit_identical(oracle):
             S.shard_timer = eight
         S.set_state(init)
         S.run_mcmc(None, 3)
-        chains.append((S.chain.cpu().numpy(), S.lnprob_chain.cpu().numpy(), S.naccept.cpu().numpy()))
+        chains.append((S.chain_dev.cpu().numpy(), S.lnprob_dev.cpu().numpy(), S.naccept.cpu().numpy()))
     for a, b in zip(*chains):
         np.testing.assert_array_equal(a, b)
     q, lnp = got["q"].cpu().numpy(), got["lnp"].cpu().numpy()
@@ -156,7 +156,7 @@ def _rank(rank, port, init, out):
         assert S.world == 2 and S.fuse_shard
         S.set_state(init)
         S.run_mcmc(None, 4)
-        out[rank] = (S.chain.cpu().numpy(), S.lnprob_chain.cpu().numpy())
+        out[rank] = (S.chain_dev.cpu().numpy(), S.lnprob_dev.cpu().numpy())
         S.close()
     finally:
         dist.destroy_process_group()
@@ -174,7 +174,7 @@ def test_two_real_ranks_hip_shards_match_single_rank():
     S = sampler.EnsembleSampler(256, t.ndim, ev, seed=17)
     S.set_state(init)
     S.run_mcmc(None, 4)
-    ref = (S.chain.cpu().numpy(), S.lnprob_chain.cpu().numpy())
+    ref = (S.chain_dev.cpu().numpy(), S.lnprob_dev.cpu().numpy())
     out = mp.Manager().dict()
     mp.start_processes(_rank, args=(_free_port(), init, out), nprocs=2, join=True, start_method="spawn")
     for r in (0, 1):

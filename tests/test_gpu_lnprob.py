@@ -215,14 +215,53 @@ def test_device_mcmc_runs():
     init = sampler.initialise_walkers(p0, sampler.comp_scatter(m.dynasty_par_names, 0.1), 128,
                                       lambda p: ev(torch.as_tensor(p, device="cuda")).cpu().numpy())
     S = sampler.EnsembleSampler(128, t.ndim, ev, seed=3)
-    pos, lnp = S.run_mcmc(init, 20)
+    pos, lnp, _ = S.run_mcmc(init, 20)
     assert np.all(np.isfinite(lnp))
-    assert S.chain.shape == (20, 128, t.ndim)
+    assert S.chain_dev.shape == (20, 128, t.ndim)
     acc = S.acceptance_fraction.mean()
     assert 0.05 < acc < 0.9
     # the stored ln_prob is the ln_prob of the stored positions
-    again = ev(S.chain[-1].contiguous()).cpu().numpy()
-    np.testing.assert_allclose(again, S.lnprob_chain[-1].cpu().numpy(), rtol=1e-12)
+    again = ev(S.chain_dev[-1].contiguous()).cpu().numpy()
+    np.testing.assert_allclose(again, S.lnprob_dev[-1].cpu().numpy(), rtol=1e-12)
+
+
+def test_reference_call_pattern_on_device(tmp_path):
+    """The reference's burn-in -> reset -> production sequence through the
+    emcee 2.x surface (mcmc_utils.py:114-164, mcmcfit.py:292-341) on the HIP
+    sampler (config 2, 64 walkers): sampler.chain is (nwalkers, nsteps,
+    npars), flatchain(sampler.chain, npars, thin=10) keeps steps 0, 10, 20,
+    and the bulk mcmc_utils path writes the same chain_prod.txt byte for byte."""
+    import torch
+    from lfit_python_amd import batch, mcmc_utils, sampler, synthetic
+    from tests.helpers import pattern_run_burnin, pattern_run_mcmc_save
+    m = synthetic.config_single(300, flux_fn=_flux_fn)
+    t = batch.compile_tree(m)
+    ev = batch.LnProbEvaluator(t)
+    p0 = np.array(m.dynasty_par_vals)
+    init = sampler.initialise_walkers(p0, sampler.comp_scatter(m.dynasty_par_names, 0.1), 64,
+                                      lambda p: ev(torch.as_tensor(p, device="cuda")).cpu().numpy())
+    names = "walker_no " + " ".join(m.dynasty_par_names) + " ln_prob"
+    npars, nprod = t.ndim, 25
+    S1 = sampler.EnsembleSampler(64, npars, ev, seed=17)
+    pos, prob, state = pattern_run_burnin(S1, init, 6)
+    S1.reset()
+    f1 = str(tmp_path / "pattern.txt")
+    S1 = pattern_run_mcmc_save(S1, pos, nprod, state, f1, col_names=names)
+    chain = S1.chain
+    assert chain.shape == (64, nprod, npars) and S1.lnprobability.shape == (64, nprod)
+    flat = mcmc_utils.flatchain(S1.chain, npars, thin=10)
+    dev = S1.chain_dev.cpu().numpy()
+    np.testing.assert_array_equal(flat, dev[::10].transpose(1, 0, 2).reshape(-1, npars))
+    S2 = sampler.EnsembleSampler(64, npars, ev, seed=17)
+    pos2, prob2, state2 = mcmc_utils.run_burnin(S2, init, 6)
+    S2.reset()
+    f2 = str(tmp_path / "bulk.txt")
+    mcmc_utils.run_mcmc_save(S2, pos2, nprod, state2, f2, col_names=names, chunk=10)
+    assert open(f1).read() == open(f2).read()
+    np.testing.assert_array_equal(S2.chain, chain)
+    # the stored ln_prob is the ln_prob of the stored positions
+    again = ev(torch.as_tensor(chain[:, -1].copy(), device="cuda")).cpu().numpy()
+    np.testing.assert_allclose(again, S1.lnprobability[:, -1], rtol=1e-12)
 
 
 def test_fused_half_step_matches_separate_kernels():
@@ -269,9 +308,9 @@ def test_fused_half_step_matches_separate_kernels():
             S.run_mcmc(init, 4)
             S.reset()
             S.run_mcmc(None, 3)
-            ch, lc = S.chain.cpu().numpy(), S.lnprob_chain.cpu().numpy()
+            ch, lc = S.chain_dev.cpu().numpy(), S.lnprob_dev.cpu().numpy()
             S.run_mcmc(ch[1], 2)  # set_state: new positions drop the speculative candidates
-            res.append((ch, lc, S.chain.cpu().numpy(), S.naccept.cpu().numpy()))
+            res.append((ch, lc, S.chain_dev.cpu().numpy(), S.naccept.cpu().numpy()))
         for other in res[1:]:
             for a, b in zip(res[0], other):
                 np.testing.assert_array_equal(a, b)
@@ -294,8 +333,8 @@ def test_graph_replay_matches_eager():
         S.use_graph = graph
         S.run_mcmc(init, 6)
         S.reset()
-        pos, lnp = S.run_mcmc(None, 4)
-        out.append((S.chain.cpu().numpy(), S.lnprob_chain.cpu().numpy(), S.naccept.cpu().numpy()))
+        pos, lnp, _ = S.run_mcmc(None, 4)
+        out.append((S.chain_dev.cpu().numpy(), S.lnprob_dev.cpu().numpy(), S.naccept.cpu().numpy()))
         if graph:
             assert S._graph is not None
     for a, b in zip(out[0], out[1]):
@@ -396,7 +435,7 @@ def test_gp_tree_spec_chain():
         S = sampler.EnsembleSampler(W, t.ndim, ev, seed=9)
         S.spec = spec
         S.run_mcmc(init, 3)
-        out.append((S.chain.cpu().numpy(), S.lnprob_chain.cpu().numpy(), S.naccept.cpu().numpy()))
+        out.append((S.chain_dev.cpu().numpy(), S.lnprob_dev.cpu().numpy(), S.naccept.cpu().numpy()))
     for a, b in zip(*out):
         np.testing.assert_array_equal(a, b)
 

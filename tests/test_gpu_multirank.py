@@ -37,7 +37,7 @@ def _chain(spec, world=1, rank=0):
     S = sampler.EnsembleSampler(W, t.ndim, ev, seed=23)
     S.spec = spec
     S.run_mcmc(_init(W), 4)
-    out = (S.chain.cpu().numpy(), S.lnprob_chain.cpu().numpy(), S.naccept.cpu().numpy())
+    out = (S.chain_dev.cpu().numpy(), S.lnprob_dev.cpu().numpy(), S.naccept.cpu().numpy())
     S.close()
     return out
 

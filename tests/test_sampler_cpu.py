@@ -12,6 +12,8 @@ import torch.multiprocessing as mp
 
 from lfit_python_amd.sampler import EnsembleSampler, comp_scatter, initialise_walkers
 from tests import stretch_double as sd
+from tests.helpers import pattern_run_burnin as _pattern_run_burnin
+from tests.helpers import pattern_run_mcmc_save as _pattern_run_mcmc_save
 
 NDIM, W, STEPS = 5, 16, 30
 
@@ -45,7 +47,7 @@ def _run_single():
     S = EnsembleSampler(W, NDIM, ev, seed=99, ops=sd.TorchCpuOps())
     S.set_state(_p0())
     S.run_mcmc(None, STEPS)
-    return S.chain.numpy(), S.lnprob_chain.numpy(), ev.calls
+    return S.chain_dev.numpy(), S.lnprob_dev.numpy(), ev.calls
 
 
 def test_stretch_move_matches_numpy_reference():
@@ -86,7 +88,7 @@ def _worker(rank, port, out):
         assert S.world == 2 and S.shard == W // 4
         S.set_state(_p0())
         S.run_mcmc(None, STEPS)
-        out[rank] = (S.chain.numpy().copy(), S.lnprob_chain.numpy().copy(), list(ev.calls))
+        out[rank] = (S.chain_dev.numpy().copy(), S.lnprob_dev.numpy().copy(), list(ev.calls))
     finally:
         dist.destroy_process_group()
 
@@ -141,7 +143,7 @@ def test_reset_keeps_the_random_stream():
     reference passes the burn-in RNG state on, mcmc_utils.py:135-183)."""
     ev = GaussLnProb()
     S = EnsembleSampler(W, NDIM, ev, seed=99, ops=sd.TorchCpuOps())
-    S.run_mcmc(_p0(), 4, store=False)
+    S.run_mcmc(_p0(), 4, storechain=False)
     S.reset()
     assert S.iteration == 0 and S.random_state == 4 and int(S.naccept.sum()) == 0
     S.run_mcmc(None, 3)
@@ -154,7 +156,7 @@ def test_reset_keeps_the_random_stream():
             q, zf = sd.propose(pos, half, 2.0, 99, it)
             sd.accept(pos, lp, half, q, zf, GaussLnProb()(torch.as_tensor(q)).numpy(), 99, it, nacc)
         if it >= 4:
-            np.testing.assert_array_equal(S.chain[it - 4].numpy(), pos)
+            np.testing.assert_array_equal(S.chain_dev[it - 4].numpy(), pos)
     # replaying step 0 after the reset would have drawn the burn-in's z
     assert not np.array_equal(sd.propose(pos, 0, 2.0, 99, 0)[1], sd.propose(pos, 0, 2.0, 99, 4)[1])
 
@@ -192,3 +194,104 @@ def test_initialise_walkers_reference_signature():
         return -np.inf if p[0] > 1.05 else 0.0
     p0 = mcmc_utils.initialise_walkers(np.array([1.0, 2.0]), 0.1, 32, ln_prior, "m", seed=2)
     assert p0.shape == (32, 2) and np.all(p0[:, 0] <= 1.05) and set(calls) == {"m"}
+
+
+# ---- emcee 2.x surface: the reference's own call patterns over the sampler
+def test_reference_call_pattern_and_flatchain(tmp_path):
+    """The reference's burn-in -> reset -> production -> flatchain sequence
+    (mcmcfit.py:292-341) through sample(): sampler.chain is
+    (nwalkers, nsteps, npars), flatchain(sampler.chain, npars, thin=10)
+    keeps every 10th step, and the bulk mcmc_utils path writes the same file
+    and chain byte for byte."""
+    from lfit_python_amd import mcmc_utils
+    names = "walker_no " + " ".join("p%d" % i for i in range(NDIM)) + " ln_prob"
+    nprod = 25
+    S1 = EnsembleSampler(W, NDIM, GaussLnProb(), seed=99, ops=sd.TorchCpuOps())
+    pos, prob, state = _pattern_run_burnin(S1, _p0(), 4)
+    assert state == 4 and pos.shape == (W, NDIM) and prob.shape == (W,)
+    S1.reset()
+    f1 = str(tmp_path / "pattern.txt")
+    S1 = _pattern_run_mcmc_save(S1, pos, nprod, state, f1, col_names=names)
+    assert S1.chain.shape == (W, nprod, NDIM) and S1.lnprobability.shape == (W, nprod)
+    assert S1.iterations == nprod and S1.flatchain.shape == (W * nprod, NDIM)
+    flat = mcmc_utils.flatchain(S1.chain, NDIM, thin=10)
+    assert flat.shape == (W * 3, NDIM)
+    steps = S1.chain_dev.numpy()[::10]                    # steps 0, 10, 20 of production
+    np.testing.assert_array_equal(flat, steps.transpose(1, 0, 2).reshape(-1, NDIM))
+    np.testing.assert_array_equal(mcmc_utils.flatchain(S1.chain_dev.permute(1, 0, 2), NDIM, thin=10), flat)
+    # the stored production steps are the stretch move's (numpy double),
+    # continuing the burn-in's random stream
+    p, lp = _p0(), None
+    lp = GaussLnProb()(torch.as_tensor(p)).numpy()
+    nacc = np.zeros(W, np.int64)
+    for it in range(4 + nprod):
+        for half in (0, 1):
+            q, zf = sd.propose(p, half, 2.0, 99, it)
+            sd.accept(p, lp, half, q, zf, GaussLnProb()(torch.as_tensor(q)).numpy(), 99, it, nacc)
+        if it >= 4:
+            np.testing.assert_array_equal(S1.chain[:, it - 4], p)
+            # (production starts from set_state's batched ln_prob: rounding apart)
+            np.testing.assert_allclose(S1.lnprobability[:, it - 4], lp, rtol=1e-14)
+    # the bulk path: same file, same chain
+    S2 = EnsembleSampler(W, NDIM, GaussLnProb(), seed=99, ops=sd.TorchCpuOps())
+    pos2, prob2, state2 = mcmc_utils.run_burnin(S2, _p0(), 4)
+    np.testing.assert_array_equal(pos2, pos)
+    S2.reset()
+    f2 = str(tmp_path / "bulk.txt")
+    mcmc_utils.run_mcmc_save(S2, pos2, nprod, state2, f2, col_names=names, chunk=7)
+    assert open(f1).read() == open(f2).read()
+    np.testing.assert_array_equal(S2.chain, S1.chain)
+    np.testing.assert_array_equal(S2.lnprobability, S1.lnprobability)
+    c = mcmc_utils.readchain(f1)
+    np.testing.assert_array_equal(c[:, :, :NDIM], S1.chain)
+    # readflatchain: a headerless whitespace table
+    f3 = str(tmp_path / "flat.txt")
+    np.savetxt(f3, flat)
+    np.testing.assert_array_equal(mcmc_utils.readflatchain(f3), flat)
+
+
+def test_sample_thin_and_accumulation():
+    """emcee 2.x storage rules: sample() with thin keeps steps i % thin == 0,
+    successive runs append to the chain, reset() empties it"""
+    S = EnsembleSampler(W, NDIM, GaussLnProb(), seed=4, ops=sd.TorchCpuOps())
+    rows = []
+    for pos, prob, state in S.sample(_p0(), iterations=7, thin=3):
+        rows.append(pos)
+    assert S.chain.shape == (W, 3, NDIM)
+    for j, i in enumerate((0, 3, 6)):
+        np.testing.assert_array_equal(S.chain[:, j], rows[i])
+    S.run_mcmc(None, 2)
+    assert S.chain.shape == (W, 5, NDIM) and state == 7 and S.random_state == 9
+    S.run_mcmc(None, 2, storechain=False)
+    assert S.chain.shape == (W, 5, NDIM)
+    S.reset()
+    assert S.chain.shape == (W, 0, NDIM) and S.iterations == 0
+
+
+def _save_worker(rank, port, path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    try:
+        from lfit_python_amd import mcmc_utils
+        S = EnsembleSampler(W, NDIM, GaussLnProb(), seed=99, ops=sd.TorchCpuOps())
+        pos, prob, state = mcmc_utils.run_burnin(S, _p0(), 3)
+        S.reset()
+        mcmc_utils.run_mcmc_save(S, pos, 5, state, path, col_names="walker_no a b c d e ln_prob", chunk=2)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_run_mcmc_save_writes_once(tmp_path):
+    """Every rank runs the production steps, rank 0 alone writes the file:
+    1 header line + nSteps * W rows."""
+    path = str(tmp_path / "chain_prod.txt")
+    mp.spawn(_save_worker, args=(_free_port(), path), nprocs=2, join=True)
+    lines = open(path).read().splitlines()
+    assert len(lines) == 1 + 5 * W
+    S = EnsembleSampler(W, NDIM, GaussLnProb(), seed=99, ops=sd.TorchCpuOps())
+    from lfit_python_amd import mcmc_utils
+    pos, prob, state = mcmc_utils.run_burnin(S, _p0(), 3)
+    S.reset()
+    one = str(tmp_path / "one.txt")
+    mcmc_utils.run_mcmc_save(S, pos, 5, state, one, col_names="walker_no a b c d e ln_prob")
+    assert open(one).read() == open(path).read()

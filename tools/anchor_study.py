@@ -57,12 +57,12 @@ def study(tag, walkers, burn, prod, seed):
                                       lambda p: ev(torch.as_tensor(p, device="cuda")).cpu().numpy(), seed=seed)
     S = sampler.EnsembleSampler(walkers, t.ndim, ev, seed=seed)
     t0 = time.time()
-    pos, lnp = S.run_mcmc(init, burn, store=False)
+    pos, lnp, _ = S.run_mcmc(init, burn, storechain=False)
     S.reset()
-    S.run_mcmc(None, prod, store=True, lnp0=None)
+    S.run_mcmc(None, prod, storechain=True)
     el = time.time() - t0
-    ch = S.chain.cpu().numpy().reshape(-1, t.ndim)
-    lc = S.lnprob_chain.cpu().numpy().reshape(-1)
+    ch = S.chain_dev.cpu().numpy().reshape(-1, t.ndim)
+    lc = S.lnprob_dev.cpu().numpy().reshape(-1)
     best = ch[np.argmax(lc)]
     out = {"tree": tag, "ndim": t.ndim, "eclipses": t.leaf_labels, "npts": n.tolist(), "walkers": walkers,
            "burn": burn, "prod": prod, "seconds": el, "acceptance": float(np.mean(S.acceptance_fraction)),
