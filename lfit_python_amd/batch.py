@@ -256,7 +256,12 @@ class LnProbEvaluator:
                                               self._ws.numel(), _native.stream_ptr(self.device), events)
             _native.check(rc, "lfg_stretch_step_half")
             return
-        ens = (W, pos.data_ptr(), lnp.data_ptr(), q.data_ptr(), zfac.data_ptr(), seed, float(a))
+        # the key includes torch's in-place version counters of pos and lnp: a
+        # write to S.pos / S.lnp between steps (same pointers) bumps them and
+        # drops the candidates (the kernels' own writes go through raw
+        # pointers and leave the counters alone)
+        ens = (W, pos.data_ptr(), lnp.data_ptr(), q.data_ptr(), zfac.data_ptr(), seed, float(a),
+               pos._version, lnp._version)
         spec_in = gen == self.generation and self._spec_key == ens + (half, step)
         self._spec_key = None
         rc = self.L.lfg_stretch_step_half_spec(vp(pos), vp(lnp), W, half, a, seed, step, vp(q), vp(zfac),
@@ -289,7 +294,8 @@ class LnProbEvaluator:
             return
         gen = self.generation
         self._ensure(W // 2)  # the acceptances of the whole half live here
-        ens = ("shard", W, pos.data_ptr(), q.data_ptr(), zfac.data_ptr(), seed, float(a), lo, n)
+        ens = ("shard", W, pos.data_ptr(), q.data_ptr(), zfac.data_ptr(), seed, float(a), lo, n,
+               pos._version)  # as in step_half: an in-place write to pos drops the candidates
         spec_in = gen == self.generation and self._spec_key == ens + (half, step, "accepted")
         self._spec_key = None
         rc = self.L.lfg_stretch_step_shard_spec(vp(pos), W, half, a, seed, step, lo, n, vp(q), vp(zfac),
@@ -310,7 +316,8 @@ class LnProbEvaluator:
                                                   vp(naccept), ctypes.byref(self.ctree), n, vp(self._ws),
                                                   self._ws.numel(), _native.stream_ptr(self.device))
         _native.check(rc, "lfg_stretch_accept_regen_spec")
-        if key is not None and key[-3:] == (half, step, "pending") and key[2] == pos.data_ptr() and key[8] == n:
+        if (key is not None and key[-3:] == (half, step, "pending") and key[2] == pos.data_ptr() and key[8] == n
+                and key[9] == pos._version):
             self._spec_key = key[:-3] + (1 - half, step + half, "accepted")
 
     def ln_prior(self, walkers, out=None):

@@ -334,8 +334,12 @@ __device__ inline void prior_lane(const SetupArgs& A, int w)
         if (A.prior_type && A.prior_c) {
             // Prior.ln_prob from the tree's constants (include/lfg.h): the
             // terms c0 - z^2/2 (gauss) or c0, summed in order, and one log of
-            // the chunk's product of log_uniform / mod_jeff arguments
+            // the chunk's product of log_uniform / mod_jeff arguments.  The
+            // product is kept as mantissa x 2^pex (frexp per factor: the
+            // mantissas lie in [1/2, 1), so 16 of them never leave the normal
+            // range and no partial product loses digits)
             double prod = 1.0;
+            int pex = 0;
             bool ok = true;
 #pragma unroll
             for (int k = 0; k < PCH; ++k) {
@@ -346,23 +350,17 @@ __device__ inline void prior_lane(const SetupArgs& A, int w)
                     const double z = (v[k] - p1) * A.prior_c[2 * d + 1];
                     const double term = (ty <= 1) ? fma(-0.5 * z, z, c0) : c0;
                     lp += term;
-                    prod *= (ty == 3) ? v[k] : (ty == 4 ? v[k] + p1 : 1.0);
+                    int fe;
+                    const double fm = frexp((ty == 3) ? v[k] : (ty == 4 ? v[k] + p1 : 1.0), &fe);
+                    prod *= fm;
+                    pex += fe;
                     // scipy's pdf underflows to 0 (log -> -inf) below e^-745.13
                     ok = ok && ((ty <= 1) ? (term > PDF_LN_MIN && (ty == 0 || v[k] > 0.0))
                                           : (ty == 4 ? (v[k] > 0.0 && v[k] < p2)
                                                      : (ty <= 3 && v[k] > p1 && v[k] < p2)));
                 }
             }
-            if (ok && !(prod >= 1e-290 && prod <= 1e290)) {  // product out of range: one log each
-                prod = 0.0;
-                for (int k = 0; k < PCH && d0 + k < A.ndim; ++k) {
-                    const int ty = A.prior_type[d0 + k];
-                    if (ty >= 3) prod += log(ty == 3 ? v[k] : v[k] + A.prior_p1[d0 + k]);
-                }
-                lp -= prod;
-                prod = 1.0;
-            }
-            lp = ok ? lp - log(prod) : -INFINITY;
+            lp = ok ? lp - fma(double(pex), LN2, log(prod)) : -INFINITY;
         } else if (A.prior_type) {
 #pragma unroll
             for (int k = 0; k < PCH; ++k) {
@@ -386,17 +384,6 @@ __device__ __forceinline__ void setup_any(const SetupArgs& A, int t)
 {
     const int npairs = A.W * A.E;
     if (t >= 2 * npairs + A.W) return;
-#if defined(LFG_EXP_SETUP_EMPTY)  // experiment build: the launch alone (every pair fails)
-    if (t < npairs) { A.status[t] = ST_BAD_ARGS; A.bstatus[t] = ST_BAD_ARGS; }
-    if (t >= npairs && t < npairs + A.W) A.prior[t - npairs] = -INFINITY;
-    return;
-#endif
-#if defined(LFG_EXP_SETUP_NOPRIOR)  // experiment build: no prior lanes
-    if (t >= npairs && t < npairs + A.W) { A.prior[t - npairs] = 0.0; return; }
-#endif
-#if defined(LFG_EXP_SETUP_NOSTREAM)  // experiment build: no stream work
-    if (t >= npairs + A.W) { A.bstatus[t - npairs - A.W] = ST_BAD_STREAM; return; }
-#endif
     if (t >= npairs + A.W) {  // stream lanes (own waves: npairs + W is a multiple of 64 in the bench)
         bspot_lane(A, t - npairs - A.W);
         return;
@@ -496,9 +483,6 @@ __device__ __forceinline__ void setup_any(const SetupArgs& A, int t)
     LFG_CY(3, t, tl);
 }
 
-#ifdef LFG_ELEM_OOL
-__device__ __noinline__ void setup_any_ool(const SetupArgs& A, int t) { setup_any(A, t); }
-#endif
 __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
 {
     setup_any(A, blockIdx.x * SETUP_BLOCK + threadIdx.x);
@@ -615,29 +599,10 @@ __device__ __forceinline__ void element_lane(int v, int pair, int npairs, const 
         return;
     }
     static_assert((NUNIQ % ELEM_BLOCK) + NDISC_R + 1 <= ELEM_BLOCK, "ring-weight lanes fit in the last chunk");
-#if defined(LFG_EXP_ORDER2)  // experiment: spot, disc, WD, donor
-    const int u = (v < U_BS) ? U_MAIN + v
-                : (v < U_BS + U_DISC) ? U_WD + (v - U_BS)
-                : (v < U_BS + U_DISC + U_WD) ? v - U_BS - U_DISC : v - U_BS;
-#elif defined(LFG_EXP_ORDER3)  // experiment: disc, spot, WD, donor
-    const int u = (v < U_DISC) ? U_WD + v
-                : (v < U_DISC + U_BS) ? U_MAIN + (v - U_DISC)
-                : (v < U_DISC + U_BS + U_WD) ? v - U_DISC - U_BS : v - U_BS;
-#elif !defined(LFG_EXP_OLDORDER)
     // launch order WD, disc, spot, donor: the last chunk, dispatched last,
     // holds the cheap donor items (one 1-D root) instead of spot tangencies
     constexpr int V_BS = U_WD + U_DISC;
     const int u = (v < V_BS) ? v : (v < V_BS + U_BS ? U_MAIN + (v - V_BS) : v - U_BS);
-#else
-    const int u = v;
-#endif
-#if defined(LFG_EXP_NODONOR)  // experiment builds: time one region alone
-    if (u >= U_WD + U_DISC && u < U_MAIN) return;
-#elif defined(LFG_EXP_ONLYDONOR)
-    if (u < U_WD + U_DISC || u >= U_MAIN) return;
-#elif defined(LFG_EXP_ONLYWD)
-    if (u >= U_WD) return;
-#endif
     if (st0 != ST_OK) return;
     if (bst != ST_OK) {
         if (u == 0 && !X.jk) status[pair] = bst;
@@ -759,11 +724,7 @@ __global__ __launch_bounds__(ELEM_BLOCK) __attribute__((amdgpu_waves_per_eu(ELEM
     if (int(blockIdx.x) < X.nspecblk) {  // speculative setup lanes of the next half
         const int t = int(blockIdx.x) * int(blockDim.x) + int(threadIdx.x);
         const int c = t < X.nspec ? 0 : 1;
-#ifdef LFG_ELEM_OOL
-        if (t < 2 * X.nspec) setup_any_ool(X.S[c], t - c * X.nspec);
-#else
         if (t < 2 * X.nspec) setup_any(X.S[c], t - c * X.nspec);
-#endif
         return;
     }
     const unsigned bid = blockIdx.x - unsigned(X.nspecblk);
@@ -1142,9 +1103,6 @@ __device__ __forceinline__ long long to_fx(double x) { return static_cast<long l
 
 __device__ __forceinline__ void fx_add(unsigned long long* acc, int p, long long q)
 {
-#ifdef LFG_EXP_ATOM_TID  // timing experiment only (wrong sums): every lane its own address
-    p = threadIdx.x;
-#endif
     atomicAdd(acc + p, static_cast<unsigned long long>(q));
 }
 

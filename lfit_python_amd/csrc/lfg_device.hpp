@@ -16,6 +16,7 @@ namespace lfg {
 constexpr double PI = 3.14159265358979323846;
 constexpr double TWO_PI = 6.28318530717958647693;
 constexpr double DEG = PI / 180.0;
+constexpr double LN2 = 0.69314718055994530942;
 
 // MODEL_SPEC.md section 7
 constexpr double RAY_TOL = 1e-13;
@@ -95,14 +96,10 @@ __device__ __forceinline__ double rcp_fast(double x)
 // 1/x for a Newton step's length only (the step's direction and size need a
 // few digits: the root is fixed by F = 0, and a relative error e in the
 // step leaves e |dth| after it, ~1e-7 x 3e-8 at the last step): the raw
-// v_rcp_f64.  LFG_STEP_RCP_EXACT restores rcp_fast (A/B).
+// v_rcp_f64.
 __device__ __forceinline__ double rcp_step(double x)
 {
-#ifdef LFG_STEP_RCP_EXACT
-    return rcp_fast(x);
-#else
     return __builtin_amdgcn_rcp(x);
-#endif
 }
 
 __device__ __forceinline__ double rpot(const Roche& R, double x, double y, double z)
@@ -365,13 +362,6 @@ __device__ inline bool element_interval(const Roche& R, double Px, double Py, do
 }
 
 // ---------------------------------------------------------------------------
-#ifdef LFG_ELEM_OOL
-__device__ __noinline__ bool element_interval_ool(const Roche& R, double Px, double Py, double Pz, double s, double c,
-                                                  double Reff, double& a, double& b)
-{
-    return element_interval(R, Px, Py, Pz, s, c, Reff, a, b);
-}
-#endif
 // Fast path for element_interval (same converged answer, ~10x less work).
 // The contact phases are the tangencies of the line of sight with the lobe
 // surface: F1 = Phi(X) - Phi_L1 = 0 and F2 = grad Phi(X).e = 0 at
@@ -443,12 +433,8 @@ __device__ __forceinline__ void rotate(double& cs, double& sn, double d)
 // converges one step earlier (tools/newton_emul statistics in DESIGN.md).
 // Stop once |dth| <= TH_LAST (th error ~TH_LAST^2 after the step) and
 // |dt| <= T_LAST (t errors reach th squared): ~1e-14 rad (MODEL_SPEC 7).
-#ifndef LFG_TH_LAST  // experiment builds may override (tools/build_exp.sh)
-#define LFG_TH_LAST 3e-8
-#define LFG_T_LAST 1e-5
-#endif
-constexpr double TH_LAST = LFG_TH_LAST;
-constexpr double T_LAST = LFG_T_LAST;
+constexpr double TH_LAST = 3e-8;
+constexpr double T_LAST = 1e-5;
 
 struct Tan {
     double th, cs, sn, t;
@@ -597,15 +583,7 @@ __device__ inline bool element_interval_fast(const Roche& R, double Px, double P
         }
     }
     if (fallback) *fallback = true;
-#ifdef LFG_EXP_NOFALLBACK  // timing experiment only: no nested-solver fallback
-    a = 1.0; b = -1.0; return false;
-#else
-#ifdef LFG_ELEM_OOL  // experiment: the fallback out of line (its registers off the fast path)
-    return element_interval_ool(R, Px, Py, Pz, s, c, Reff, a, b);
-#else
     return element_interval(R, Px, Py, Pz, s, c, Reff, a, b);
-#endif
-#endif
 }
 
 // findphi / findi with the same 2-D tangency Newton, nested solver fallback

@@ -11,6 +11,8 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP) GPU")
     config.addinivalue_line("markers", "slow: longer CPU test")
+    config.addinivalue_line("markers", "perf: asserts wall-clock ratios (run alone on a quiet GPU; "
+                                       "-m 'gpu and not perf' leaves them out)")
 
 
 def pytest_collection_modifyitems(config, items):

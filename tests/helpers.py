@@ -71,3 +71,28 @@ def pattern_run_mcmc_save(sampler, startPos, nSteps, rState, file, col_names='')
             with open(file, "a") as fh:
                 fh.write("{0:4d} {1:s} {2:f}\n".format(k, " ".join(map(str, pos[k])), prob[k]))
     return sampler
+
+
+# ---- golden example trees (tests/golden/lnprob_<tag>.npz hold their input text)
+GOLD = __import__("os").path.join(__import__("os").path.dirname(__file__), "golden")
+
+
+def golden_tree(tag, tmpdir):
+    """(fixture, model) of a golden variant of the example input.  The input
+    text is written under `tmpdir` (tests never write into tests/golden) with
+    its light-curve paths pointed at tests/golden/ref_test_data."""
+    import os
+    from lfit_python_amd import cvmodel
+    d = np.load(os.path.join(GOLD, "lnprob_%s.npz" % tag))
+    data = os.path.join(GOLD, "ref_test_data")
+    lines = []
+    for line in str(d["input"]).splitlines():
+        tok = line.split("=", 1)
+        key = tok[0].strip()
+        if key.startswith("file_") and len(tok) == 2 and not os.path.isabs(tok[1].strip()):
+            line = "%s = %s" % (key, os.path.join(data, tok[1].strip()))
+        lines.append(line)
+    path = os.path.join(str(tmpdir), "mcmc_input_%s.dat" % tag)
+    with open(path, "w") as fh:
+        fh.write("\n".join(lines) + "\n")
+    return d, cvmodel.construct_model(path)

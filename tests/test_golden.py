@@ -171,18 +171,14 @@ def test_oracle_gp_lnprob_matches_reference(oracle):
     _same(lle.sum(1)[fin], d["ln_like"][fin], rtol=1e-10)
 
 
-def _tree_from_golden(tag):
-    d = np.load(os.path.join(GOLD, "lnprob_%s.npz" % tag))
-    path = os.path.join(GOLD, "ref_test_data", "mcmc_input_%s.dat" % tag)
-    if not os.path.exists(path):
-        with open(path, "w") as fh:
-            fh.write(str(d["input"]))
-    return d, cvmodel.construct_model(path)
+def _tree_from_golden(tag, tmpdir):
+    from tests.helpers import golden_tree
+    return golden_tree(tag, tmpdir)
 
 
 @pytest.mark.parametrize("tag", ["tree", "simple"])
-def test_compiled_gather_reproduces_cv_parlists(tag):
-    d, m = _tree_from_golden(tag)
+def test_compiled_gather_reproduces_cv_parlists(tag, tmp_path):
+    d, m = _tree_from_golden(tag, tmp_path)
     assert m.dynasty_par_names == list(d["names"])
     t = batch.compile_tree(m)
     assert t.ndim == len(d["names"])
@@ -200,8 +196,8 @@ def test_compiled_gather_reproduces_cv_parlists(tag):
         assert t.prior_p1[k] == par.prior.p1 and t.prior_p2[k] == par.prior.p2
 
 
-def test_fixed_parameters_become_constants():
-    d, m = _tree_from_golden("tree")
+def test_fixed_parameters_become_constants(tmp_path):
+    d, m = _tree_from_golden("tree", tmp_path)
     m['ulimb_g'].isVar = False
     m['tilt_3'].isVar = False
     t = batch.compile_tree(m)
@@ -211,12 +207,12 @@ def test_fixed_parameters_become_constants():
 
 
 @pytest.mark.parametrize("tag", ["tree", "simple"])
-def test_oracle_lnprob_matches_reference_tree(oracle, tag):
+def test_oracle_lnprob_matches_reference_tree(oracle, tag, tmp_path):
     """The oracle's batched ln_prob (the composition the HIP kernels
     implement) against the reference's own Node.ln_prob on the same walkers
     (reference flux = oracle flux, so this pins priors, Roche priors,
     routing and chi^2 composition)."""
-    d, m = _tree_from_golden(tag)
+    d, m = _tree_from_golden(tag, tmp_path)
     t = batch.compile_tree(m)
     lnp, lle, _ = oracle.lnprob_batch(d["walkers"], t)
     _same(lnp, d["ln_prob"], rtol=1e-10)

@@ -16,21 +16,18 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
 
-def _chi2_tree():
+def _chi2_tree(tmpdir):
     """The example input with useGP = 0 (tests/golden/lnprob_tree.npz holds it)."""
-    from lfit_python_amd import batch, cvmodel
-    d = np.load(os.path.join(GOLD, "lnprob_tree.npz"))
-    path = os.path.join(GOLD, "ref_test_data", "mcmc_input_tree.dat")
-    if not os.path.exists(path):
-        open(path, "w").write(str(d["input"]))
-    m = cvmodel.construct_model(path)
+    from lfit_python_amd import batch
+    from tests.helpers import golden_tree
+    _, m = golden_tree("tree", tmpdir)
     return m, batch.compile_tree(m)
 
 
-def test_real_data_chi2_at_the_lfit_fit(oracle):
+def test_real_data_chi2_at_the_lfit_fit(oracle, tmp_path):
     import torch
     from lfit_python_amd import batch
-    m, t = _chi2_tree()
+    m, t = _chi2_tree(tmp_path)
     ev = batch.LnProbEvaluator(t)
     p0 = np.array(m.dynasty_par_vals)[None, :]
     lle = torch.empty((1, t.E), dtype=torch.float64, device="cuda")
@@ -42,5 +39,13 @@ def test_real_data_chi2_at_the_lfit_fit(oracle):
     for lab in "12345":
         assert per[lab] < 5.0, per
     assert 5.0 < per["0"] < 30.0, per       # the outlier fit of eclipse 0 (MODEL_SPEC 9.2)
+    # regression pin of the model on the real data (MODEL_SPEC 9.1, the
+    # oracle's values, 5 decimals): a 1 % change of any component's flux
+    # moves the chi^2/N of the eclipses it shows in by 9e-5 to 0.12 relative
+    # (rsFlux_g / sFlux_0 / dFlux_1 / wdFlux_r), so a convention change of a
+    # component cannot pass this
+    pinned = {"0": 13.56261, "1": 1.44603, "2": 3.53235, "3": 2.77220, "4": 2.08496, "5": 2.05772}
+    for lab, v in pinned.items():
+        assert abs(per[lab] - v) <= 1e-5 * v, (lab, per[lab], v)
     _, lle_o, _ = oracle.lnprob_batch(p0, t)
     np.testing.assert_allclose(chi2, -2.0 * lle_o[0], rtol=1e-9)

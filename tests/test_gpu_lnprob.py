@@ -20,20 +20,16 @@ def _same(a, b, rtol):
     np.testing.assert_allclose(a[f], b[f], rtol=rtol, atol=1e-9)
 
 
-def _golden_tree(tag):
-    from lfit_python_amd import cvmodel
-    d = np.load(os.path.join(GOLD, "lnprob_%s.npz" % tag))
-    path = os.path.join(GOLD, "ref_test_data", "mcmc_input_%s.dat" % tag)
-    if not os.path.exists(path):
-        open(path, "w").write(str(d["input"]))
-    return d, cvmodel.construct_model(path)
+def _golden_tree(tag, tmpdir):
+    from tests.helpers import golden_tree
+    return golden_tree(tag, tmpdir)
 
 
 @pytest.mark.parametrize("tag", ["tree", "simple"])
-def test_lnprob_matches_reference_tree(tag):
+def test_lnprob_matches_reference_tree(tag, tmp_path):
     import torch
     from lfit_python_amd import batch
-    d, m = _golden_tree(tag)
+    d, m = _golden_tree(tag, tmp_path)
     t = batch.compile_tree(m)
     ev = batch.LnProbEvaluator(t)
     W = len(d["walkers"])
@@ -142,6 +138,7 @@ def test_non_finite_walkers_give_minus_inf(oracle, cfg):
     _same(got, ref, LNP_RTOL)
 
 
+@pytest.mark.perf
 def test_long_chain_keeps_its_pace():
     """A config-2 chain (1024 walkers) must not slow down as it leaves the
     starting ball: proposals outside the prior box once ran the nested
@@ -370,6 +367,42 @@ def test_spec_chain_with_interleaved_calls():
         np.testing.assert_array_equal(la, lb)
 
 
+def test_spec_chain_survives_inplace_writes():
+    """Writing S.pos / S.lnp in place between steps (same pointers) must drop
+    the speculative candidates formed from the old positions: the chain
+    equals the plain (spec off) chain with the same writes, bit for bit,
+    on the single-process and the sharded path."""
+    import torch
+    from lfit_python_amd import batch, sampler, synthetic
+    m = synthetic.config_single(300, flux_fn=_flux_fn)
+    t = batch.compile_tree(m)
+    ev = batch.LnProbEvaluator(t)
+    p0 = np.array(m.dynasty_par_vals)
+    init = sampler.initialise_walkers(p0, sampler.comp_scatter(m.dynasty_par_names, 0.1), 64,
+                                      lambda p: ev(torch.as_tensor(p, device="cuda")).cpu().numpy())
+    for shard in (False, True):
+        out = []
+        for spec in (False, True):
+            S = sampler.EnsembleSampler(64, t.ndim, ev, seed=13)
+            S.spec = spec
+            S.force_shard = shard
+            S.set_state(init)
+            rows = []
+            for i in range(6):
+                S.step()
+                if i == 1:
+                    S.pos[0] = S.pos[1]          # in place: same data_ptr
+                    S.lnp[0] = S.lnp[1]
+                if i == 3:
+                    S.pos[5:9] *= 1.0 + 1e-9
+                    S.lnp[5:9] = ev(S.pos[5:9].contiguous())
+                rows.append((S.pos.cpu().numpy().copy(), S.lnp.cpu().numpy().copy()))
+            out.append(rows)
+        for (pa, la), (pb, lb) in zip(*out):
+            np.testing.assert_array_equal(pa, pb)
+            np.testing.assert_array_equal(la, lb)
+
+
 # ---------------------------------------------------------------- GP trees
 def test_wdphases_matches_oracle(oracle):
     from lfit_python_amd import roche
@@ -459,7 +492,7 @@ def test_gp_leaf_scalar_path():
 
 
 @pytest.mark.parametrize("tag", ["tree", "simple", "gp"])
-def test_lnprior_matches_reference(tag):
+def test_lnprior_matches_reference(tag, tmp_path):
     """lfg_lnprior (mcmcfit.ln_prior, used for the walker ball) against the
     reference tree's own ln_prior on the golden walkers."""
     import torch
@@ -468,7 +501,35 @@ def test_lnprior_matches_reference(tag):
         d = np.load(os.path.join(GOLD, "lnprob_gp.npz"))
         m = cvmodel.construct_model(os.path.join(GOLD, "ref_test_data", "mcmc_input.dat"))
     else:
-        d, m = _golden_tree(tag)
+        d, m = _golden_tree(tag, tmp_path)
     ev = batch.LnProbEvaluator(batch.compile_tree(m))
     got = ev.ln_prior(torch.as_tensor(d["walkers"], device="cuda")).cpu().numpy()
     _same(got, d["ln_prior"], 1e-10)
+
+
+def test_lnprior_tiny_log_uniform_products():
+    """The prior lanes form one log per chunk of 16 log_uniform / mod_jeff
+    arguments: a chunk of tiny values (partial products far below the
+    normal range) must still give the sum of the per-parameter terms
+    (the running product keeps its exponent apart)."""
+    import dataclasses
+    import torch
+    from lfit_python_amd import batch, synthetic
+    from lfit_python_amd.tree import Prior
+    m = synthetic.config_single(300, flux_fn=_flux_fn)
+    t = batch.compile_tree(m)
+    nd = t.ndim
+    rng = np.random.default_rng(8)
+    types = np.array([3 if k % 3 else 4 for k in range(nd)], np.int32)    # log_uniform, mod_jeff
+    p1 = np.where(types == 3, 1e-30, 1e-200)
+    p2 = np.where(types == 3, 1e-5, 1.0)
+    pri = [Prior("log_uniform" if ty == 3 else "mod_jeff", a, b) for ty, a, b in zip(types, p1, p2)]
+    t2 = dataclasses.replace(t, prior_type=types, prior_p1=p1.astype(np.float64), prior_p2=p2.astype(np.float64),
+                             prior_norm=np.array([p.normalise for p in pri]), roche_priors=False)
+    ev = batch.LnProbEvaluator(t2)
+    W = 64
+    walkers = np.exp(rng.uniform(np.log(1e-29), np.log(1e-6), (W, nd)))
+    walkers[:, types == 4] = np.exp(rng.uniform(np.log(1e-199), np.log(0.5), (W, int((types == 4).sum()))))
+    got = ev.ln_prior(torch.as_tensor(walkers, device="cuda")).cpu().numpy()
+    ref = np.array([sum(p.ln_prob(v) for p, v in zip(pri, row)) for row in walkers])
+    np.testing.assert_allclose(got, ref, rtol=1e-13, atol=1e-11)
