@@ -124,11 +124,20 @@ def parse(argv=None):
     ap.add_argument("--exchange-path", action="store_true",
                     help="one GPU: a one-rank RCCL group and the multi-rank code path with its real "
                          "exchange (shard kernels, ncclAllGather on the compute stream, k_accept_regen)")
+    ap.add_argument("--emulate-rank", default=None, metavar="K/N",
+                    help="timing rehearsal of rank K of an N-GPU run on this one GPU (config 4: W = 16384 held, "
+                         "W/2/N walkers evaluated per half, a one-rank RCCL exchange of the shard, the acceptance "
+                         "over the whole half); also times the fused one-GPU step and reports the implied 1->N ratio")
     ap.add_argument("--seed", type=int, default=20261015)
     ap.add_argument("--time-every", type=int, default=4,
                     help="record the dominant kernel's event pair on every k-th ln_prob call of the timed region")
     args = ap.parse_args(argv)
     cfg = CONFIGS[args.config]
+    args.emu = None
+    if args.emulate_rank:
+        k, n = (int(v) for v in args.emulate_rank.split("/"))
+        args.emu = (k, n)
+        args.exchange_path = True
     args.npts = args.npts or cfg["npts"]
     args.nsub = args.nsub or cfg["nsub"]
     return args
@@ -172,6 +181,8 @@ def walker_count(args, world):
         return args.walkers
     if "walkers_total" in cfg:
         tot = cfg["walkers_total"]
+        if args.emu:  # one rank of N: the whole ensemble is held, 1/N of each half evaluated
+            return tot
         if tot % (2 * world):
             raise SystemExit("config 4: 16384 walkers do not shard over %d ranks" % world)
         return tot // world
@@ -269,6 +280,8 @@ def run(args):
     S = sampler.EnsembleSampler(W, tree.ndim, ev, seed=args.seed)
     S.force_shard = args.shard_path
     S.force_exchange = args.exchange_path
+    if args.emu:
+        S.emulate_rank(*args.emu)
     S.set_state(init)
 
     # HIP events around kernels of lfg_lnprob calls (include/lfg.h LFG_NEV)
@@ -369,6 +382,29 @@ def run(args):
     # the dominant kernel's device time over the timed region
     shard = events[0][1] if events else W // 2   # walkers per launch
     dom_ms, ncalls = kernel_ms([KERNELS[dom]])
+    emu = None
+    if args.emu:
+        # the same ensemble on one GPU through the fused single-process path
+        S1 = sampler.EnsembleSampler(W, tree.ndim, ev, seed=args.seed)
+        S1.set_state(init)
+        for _ in range(args.warmup):
+            S1.step()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            S1.step()
+        torch.cuda.synchronize()
+        el1 = time.perf_counter() - t1
+        S1.close()
+        k, n = args.emu
+        emu = {"rank": k, "nranks": n, "walkers_held": W, "walkers_evaluated_per_half": shard,
+               "ms_per_step_rank": elapsed / args.steps * 1e3, "ms_per_step_one_gpu_fused": el1 / args.steps * 1e3,
+               "projected_speedup_1_to_n": el1 / elapsed,
+               "note": "one rank's launches (shard kernels, a one-rank ncclAllGather of its shard, the acceptance "
+                       "over the whole half) timed on one GPU; the other shards' ln_prob entries are stale, so the "
+                       "chain is not a sample.  Projected: the N ranks run these concurrently; the exchange of a "
+                       "real N-rank all_gather over xGMI is latency-bound (W/2 doubles) and not included beyond "
+                       "the one-rank call"}
     avg_dom = float(dom_ms[0])
     E = tree.E
     npts = int(np.max(np.diff(tree.offsets)))
@@ -469,6 +505,7 @@ def run(args):
                                                                   "(DESIGN.md 3): an intermediate, not 8(d) work"}},
             },
             "acceptance_fraction": acc,
+            **({"emulation": emu} if emu else {}),
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), file=json_out, flush=True)

@@ -146,6 +146,7 @@ class EnsembleSampler:
         self.force_exchange = False  # one rank: still exchange through the collective (rehearsal)
         self.shard_timer = None
         self._q_sh = self._zf_sh = self._lnp_sh = None
+        self._emu = None   # (rank, nranks) of emulate_rank()
         self._rccl = None  # direct RCCL all-gather (built at the first nccl exchange)
         # HIP-graph replay of whole iterations (single rank, HIP ops): the first
         # step() after enabling runs eagerly, the next captures, later ones replay
@@ -295,6 +296,23 @@ class EnsembleSampler:
         self.iteration += 1
         self.rng_step += 1
 
+    def emulate_rank(self, k, nranks):
+        """Timing rehearsal of one rank of an nranks-GPU run on this one
+        process: each half-step evaluates only walkers k*n .. (k+1)*n - 1 of
+        the half (n = W / 2 / nranks) through the multi-rank kernels, the
+        exchange moves that shard alone (a one-rank group's all_gather with
+        force_exchange), and the acceptance runs over the whole half as on
+        every rank.  The other shards' entries of the gathered ln_prob are
+        left as the last values written there, so the chain is NOT a valid
+        sample; the launches are exactly rank k's (bench.py --emulate-rank)."""
+        ns = self.W // 2
+        if ns % nranks or not (0 <= k < nranks):
+            raise ValueError("W/2 = %d does not shard over %d ranks" % (ns, nranks))
+        self.force_shard = True
+        self.shard = ns // nranks
+        self._emu = (int(k), int(nranks))
+        self._q_sh = self._zf_sh = self._lnp_sh = None
+
     def _shard_half(self, half):
         import torch
         if self._lnp_sh is None:
@@ -302,15 +320,17 @@ class EnsembleSampler:
             self._q_sh = torch.empty((self.shard, self.ndim), **f64)
             self._zf_sh = torch.empty(self.shard, **f64)
             self._lnp_sh = torch.empty(self.shard, **f64)
+        lo = (self._emu[0] if self._emu else self.rank) * self.shard
         f = self.shard_timer or self.ev.step_shard
         spec = self.spec and hasattr(self.ev, "accept_regen") and (
             self.shard_timer is None or getattr(self.shard_timer, "takes_spec", False))
-        f(self.pos, half, self.a, self.seed, self.rng_step, self.rank * self.shard, self._q_sh, self._zf_sh,
+        f(self.pos, half, self.a, self.seed, self.rng_step, lo, self._q_sh, self._zf_sh,
           self._lnp_sh, **(dict(spec=True) if spec else {}))
+        dst = self.lnp_new[lo:lo + self.shard] if self._emu else self.lnp_new
         if self.world > 1 or self.force_exchange:
-            self._gather(self.lnp_new, self._lnp_sh)
+            self._gather(dst, self._lnp_sh)
         else:
-            self.lnp_new.copy_(self._lnp_sh)
+            dst.copy_(self._lnp_sh)
         if spec:  # records the acceptances for the next half's speculative setup
             self.ev.accept_regen(self.pos, self.lnp, half, self.a, self.seed, self.rng_step, self.lnp_new,
                                  self.naccept, self.shard)

@@ -133,6 +133,58 @@ def test_config4_eight_shards_bit_identical(oracle):
     _check_against_oracle(oracle, t, q, lnp, 1, nsubset=64)
 
 
+def test_config4_eight_rank_workspaces_spec_path(oracle):
+    """The path a real N = 8 run of config 4 takes, rank by rank: 8
+    evaluators (one workspace each, as 8 processes have), each holding the
+    whole 16 384-walker ensemble, running lfg_stretch_step_shard_spec on its
+    1 024 walkers of the half (lo = k x 1024), the shard vectors concatenated
+    as ncclAllGather would, then lfg_stretch_accept_regen_spec over the whole
+    half on every rank.  From the second half-step on, every rank's shard
+    takes its setup from the candidates its previous k_elements formed.  The
+    chain is bit-identical on all 8 ranks and to the single-process fused
+    chain; 64 proposals of the last half match the oracle."""
+    import torch
+    from lfit_python_amd import batch, sampler
+    m, t, ev0, init = _ensemble("c4")
+    W, R, iters = 16384, 8, 3
+    n = W // 2 // R
+    S = sampler.EnsembleSampler(W, t.ndim, ev0, seed=29)
+    S.set_state(init)
+    lnp_init = S.lnp.clone()
+    S.run_mcmc(None, iters)
+    ref = (S.chain_dev.cpu().numpy(), S.lnprob_dev.cpu().numpy(), S.naccept.cpu().numpy())
+    del S
+    f64 = dict(dtype=torch.float64, device="cuda")
+    evs = [batch.LnProbEvaluator(t, max_walkers=W // 2) for _ in range(R)]
+    pos = [torch.as_tensor(init, **f64).contiguous() for _ in range(R)]
+    lnp = [lnp_init.clone() for _ in range(R)]
+    nacc = [torch.zeros(W, dtype=torch.int32, device="cuda") for _ in range(R)]
+    q = [torch.empty((n, t.ndim), **f64) for _ in range(R)]
+    zf = [torch.empty(n, **f64) for _ in range(R)]
+    lsh = [torch.empty(n, **f64) for _ in range(R)]
+    chain, lchain, spec_used = [], [], 0
+    for it in range(iters):
+        for half in (0, 1):
+            for k in range(R):
+                key = evs[k]._spec_key
+                spec_used += int(key is not None and key[-3:] == (half, it, "accepted"))
+                evs[k].step_shard(pos[k], half, 2.0, 29, it, k * n, q[k], zf[k], lsh[k], spec=True)
+            lnp_new = torch.cat(lsh)                 # what the all_gather hands every rank
+            for k in range(R):
+                evs[k].accept_regen(pos[k], lnp[k], half, 2.0, 29, it, lnp_new, nacc[k], n)
+        for k in range(1, R):
+            assert torch.equal(pos[k], pos[0]) and torch.equal(lnp[k], lnp[0])
+        chain.append(pos[0].cpu().numpy())
+        lchain.append(lnp[0].cpu().numpy())
+    assert spec_used == R * (2 * iters - 1)          # every half but the first ran on candidates
+    np.testing.assert_array_equal(np.stack(chain), ref[0])
+    np.testing.assert_array_equal(np.stack(lchain), ref[1])
+    np.testing.assert_array_equal(nacc[0].cpu().numpy(), ref[2])
+    qa = torch.cat(q).cpu().numpy()
+    assert torch.isfinite(lnp_new).sum() > W // 4
+    _check_against_oracle(oracle, t, qa, lnp_new.cpu().numpy(), 1, nsubset=64)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
