@@ -401,8 +401,8 @@ def run(args):
                "ms_per_step_rank": elapsed / args.steps * 1e3, "ms_per_step_one_gpu_fused": el1 / args.steps * 1e3,
                "projected_speedup_1_to_n": el1 / elapsed,
                "note": "one rank's launches (shard kernels, a one-rank ncclAllGather of its shard, the acceptance "
-                       "over the whole half) timed on one GPU; the other shards' ln_prob entries are stale, so the "
-                       "chain is not a sample.  Projected: the N ranks run these concurrently; the exchange of a "
+                       "over the whole half) timed on one GPU; the other shards' ln_prob entries are -inf (their "
+                       "walkers stay in the starting ball), so the chain is not a sample.  Projected: the N ranks run these concurrently; the exchange of a "
                        "real N-rank all_gather over xGMI is latency-bound (W/2 doubles) and not included beyond "
                        "the one-rank call"}
     avg_dom = float(dom_ms[0])

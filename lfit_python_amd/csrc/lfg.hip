@@ -34,7 +34,8 @@ constexpr int ELEM_BLOCK = LFG_ELEM_BLOCK;
 #define LFG_ELEM_IPL 1  // items per k_elements lane
 #endif
 #ifndef ELEM_MINW
-#define ELEM_MINW 5  // minimum waves per SIMD of k_elements (94 VGPRs: the speculative setup lanes spill to fit)
+#define ELEM_MINW 4  // minimum waves per SIMD of k_elements: <= 128 VGPRs, no spill (at 5 waves / 96 VGPRs the
+                     // speculative setup lanes spilled ~100 B/lane; 4 waves measured 3 % faster)
 #endif
 // per-pair weight block written by k_elements: disc ring weights, the disc
 // total 2 pi [P(rdisc) - P(rin)], spot element weights
@@ -208,6 +209,16 @@ __device__ inline Prop make_prop(const SetupArgs& A, int w)
     return P;
 }
 
+// CV parameter count of eclipse e.  P is pinned to a register first: written
+// as `npars ? npars[e] : P` the compiler selected between the two ADDRESSES
+// and, to give the kernel argument P one, copied it into scratch
+__device__ __forceinline__ int npars_of(const SetupArgs& A, int e)
+{
+    int P = A.P;
+    asm volatile("" : "+s"(P));
+    return A.npars ? A.npars[e] : P;
+}
+
 __device__ __forceinline__ double gather_par(const SetupArgs& A, const Prop& P, int g)
 {
     if (g < 0) return A.consts[-1 - g];
@@ -245,7 +256,7 @@ __device__ inline void bspot_lane(const SetupArgs& A, int t)
     const int* gat = A.gather ? A.gather : kIdentityGather;
     const int w = t / A.E, e = t - w * A.E;
     const Prop P = make_prop(A, w);
-    const int np = A.npars ? A.npars[e] : A.P;
+    const int np = npars_of(A, e);
     const double q = gather_par(A, P, gat[e * 18 + 4]);
     const double rdisc = gather_par(A, P, gat[e * 18 + 6]);
     const double az = gather_par(A, P, gat[e * 18 + 10]);
@@ -398,9 +409,10 @@ __device__ __forceinline__ void setup_any(const SetupArgs& A, int t)
     const int* gat = A.gather ? A.gather : kIdentityGather;
     const int w = t / A.E, e = t - (t / A.E) * A.E;
     const Prop P = make_prop(A, w);
-    const int np = A.npars ? A.npars[e] : A.P;
+    const int np = npars_of(A, e);
     double p[18];
     bool finite = (np == 14 || np == 18);
+#pragma unroll  // p[] stays in registers (a rolled loop kept it in scratch)
     for (int k = 0; k < 18; ++k) {
         p[k] = (k < np) ? gather_par(A, P, gat[e * 18 + k]) : 0.0;
         finite = finite && isfinite(p[k]);
@@ -411,26 +423,52 @@ __device__ __forceinline__ void setup_any(const SetupArgs& A, int t)
     unsigned long long tf = tl;
     LFG_CY(0, t, tf);
 #endif
+    // what does not depend on the inclination is formed and stored before
+    // findi, so that only q's Roche record and dphi stay live through the
+    // solve (this lane also runs, twice, inside k_elements' register budget:
+    // lfg_stretch_step_half_spec); the few values needed after it are read
+    // back from the record
+    {
+        const double tilt = p[16] * DEG, psi = (p[10] - 90.0 + p[17]) * DEG;
+        double st_, ct_, sp_, cp_, saz, caz;
+        sincos(tilt, &st_, &ct_);
+        sincos(psi, &sp_, &cp_);
+        sincos(p[10] * DEG, &saz, &caz);
+        G[G_CAZ] = caz; G[G_SAZ] = saz;
+        G[G_NB0] = st_ * cp_; G[G_NB1] = st_ * sp_; G[G_NB2] = ct_;
+        G[G_BDEN] = fabs(st_);  // |sin tilt| until the inclination is known
+        G[G_ULIMB] = p[7]; G[G_DEXP] = p[12];
+        G[G_FIS] = p[11]; G[G_PHI0] = p[13];
+        G[G_WDF] = p[0]; G[G_DF] = p[1]; G[G_SF] = p[2]; G[G_RSF] = p[3];
+    }
     int st = ST_OK;
     double rprior = 0.0;
     Roche R;
     if (!finite) st = ST_BAD_ARGS;
     else st = roche_init(R, p[4]);
     LFG_CY(1, t, tf);
+    bool bad_geo = false;
     if (st == ST_OK) {
         // SimpleEclipse.ln_prior Roche checks not involving the stream (CVModel.py:215-316)
         if (p[6] * R.xl1 > DISC_MAX_A) rprior = -INFINITY;
         const double rwd = p[8], scale = p[9];
         if (scale > rwd * 3.0 || scale < rwd / 3.0) rprior = -INFINITY;
+        // geometry (MODEL_SPEC 6), reported after findi's status
+        const double rwd_a = p[8] * R.xl1, rdisc_a = p[6] * R.xl1;
+        bad_geo = !(rwd_a > 0.0) || !(rdisc_a > rwd_a) || !(rdisc_a < R.xl1) || !(p[9] > 0.0) || !(p[14] > 0.0) ||
+                  !(p[15] > 0.0);
+        G[G_Q] = R.q; G[G_CA] = R.cA; G[G_CB] = R.cB; G[G_MU] = R.mu;
+        G[G_XL1] = R.xl1; G[G_PL1] = R.pl1; G[G_RS] = R.Rs; G[G_RS2] = R.Rs2;
+        G[G_RWD] = rwd_a; G[G_RDISC] = rdisc_a; G[G_REFF] = eggleton(R.q);
+        G[G_L] = p[9] * R.xl1;
     } else {
         rprior = -INFINITY;
     }
+    const double dphi = p[5];
     double inc = 0.0;
-    if (st == ST_OK) st = findi_fast(R, p[5], inc);
+    if (st == ST_OK) st = findi_fast(R, dphi, inc);
     LFG_CY(2, t, tf);
-    const double rwd_a = p[8] * R.xl1, rdisc_a = p[6] * R.xl1;
-    if (st == ST_OK && (!(rwd_a > 0.0) || !(rdisc_a > rwd_a) || !(rdisc_a < R.xl1))) st = ST_BAD_GEOMETRY;
-    if (st == ST_OK && (!(p[9] > 0.0) || !(p[14] > 0.0) || !(p[15] > 0.0))) st = ST_BAD_GEOMETRY;
+    if (st == ST_OK && bad_geo) st = ST_BAD_GEOMETRY;
 
     A.status[t] = st;
     G[G_RPRIOR] = A.roche_priors ? rprior : 0.0;
@@ -438,47 +476,35 @@ __device__ __forceinline__ void setup_any(const SetupArgs& A, int t)
 
     double s, c;
     sincos(inc * DEG, &s, &c);
-    const double tilt = p[16] * DEG, psi = (p[10] - 90.0 + p[17]) * DEG;
-    double st_, ct_, sp_, cp_;
-    sincos(tilt, &st_, &ct_);
-    sincos(psi, &sp_, &cp_);
-    const double nmax = fabs(st_) * s + ct_ * c;
-    double saz, caz;
-    sincos(p[10] * DEG, &saz, &caz);
-
-    G[G_Q] = R.q; G[G_CA] = R.cA; G[G_CB] = R.cB; G[G_MU] = R.mu;
-    G[G_XL1] = R.xl1; G[G_PL1] = R.pl1; G[G_RS] = R.Rs; G[G_RS2] = R.Rs2;
+    const double fis = G[G_FIS];
+    const double nmax = G[G_BDEN] * s + G[G_NB2] * c;
     G[G_S] = s; G[G_C] = c; G[G_INC] = inc;
-    G[G_RWD] = rwd_a; G[G_RDISC] = rdisc_a; G[G_REFF] = eggleton(R.q);
-    G[G_ULIMB] = p[7]; G[G_DEXP] = p[12];
-    G[G_L] = p[9] * R.xl1; G[G_CAZ] = caz; G[G_SAZ] = saz;
-    G[G_NB0] = st_ * cp_; G[G_NB1] = st_ * sp_; G[G_NB2] = ct_;
-    G[G_BDEN] = p[11] + (1.0 - p[11]) * fmax(nmax, 0.0);
-    G[G_FIS] = p[11]; G[G_PHI0] = p[13];
-    G[G_WDF] = p[0]; G[G_DF] = p[1]; G[G_SF] = p[2]; G[G_RSF] = p[3];
-    const double sce = s * cos(PI * p[5]);
+    G[G_BDEN] = fis + (1.0 - fis) * fmax(nmax, 0.0);
+    const double sce = s * cos(PI * dphi);
     G[G_RCAL] = sqrt(1.0 - sce * sce);
     if (A.gp) {
         // SimpleGPEclipse.create_GP / calcChangepoints (CVModel.py:529-648):
         // amplitudes exp(ln_amp), metric exp(ln_tau); the changepoint
-        // distance from the cache unless q, dphi or rwd moved > 120 %
+        // distance from the cache unless q, dphi or rwd moved > 120 %.  A
+        // walker that trips the rule needs wdphases (ten nested eclipse
+        // solves): it is marked pending (G_GP_OK = 2) and k_gp_dcp solves the
+        // ten limb points in parallel lanes before k_lnlike<2> (kept out of
+        // this lane, whose registers the speculative copies inside
+        // k_elements share)
         const int* gg = A.gp_gather + e * 3;
         const double ain = exp(gather_par(A, P, gg[0])), aout = exp(gather_par(A, P, gg[1]));
         const double tau = exp(gather_par(A, P, gg[2]));
         const double* B = A.gp_base + e * 4;
-        const double q = p[4], dphi = p[5], rwd = p[8];
-        double dcp = B[3];
-        bool ok = isfinite(dcp);
-        if (fabs(B[1] - dphi) / dphi > 1.2 || fabs(B[0] - q) / q > 1.2 || fabs(B[2] - rwd) / rwd > 1.2) {
-            double ph3, ph4;
-            ok = wdphases(R, inc, rwd, 10, ph3, ph4) == ST_OK;  // inc = roche.findi(q, dphi)
-            dcp = (dphi + (ph4 - ph3)) / 2.0;
-        }
+        const double q = R.q, rwd = p[8];
+        const bool pend = fabs(B[1] - dphi) / dphi > 1.2 || fabs(B[0] - q) / q > 1.2 || fabs(B[2] - rwd) / rwd > 1.2;
+        const bool ok = tau > 0.0 && isfinite(ain) && isfinite(aout);
         G[G_GP_AIN] = ain;
         G[G_GP_AOUT] = aout;
         G[G_GP_LAM] = sqrt(3.0 / tau);
-        G[G_GP_DCP] = dcp;
-        G[G_GP_OK] = (ok && tau > 0.0 && isfinite(ain) && isfinite(aout)) ? 1.0 : 0.0;
+        G[G_GP_DCP] = B[3];
+        G[G_GP_DPHI] = dphi;
+        G[G_GP_RWD] = rwd;
+        G[G_GP_OK] = !ok ? 0.0 : (pend ? 2.0 : (isfinite(B[3]) ? 1.0 : 0.0));
     }
     LFG_CY(3, t, tl);
 }
@@ -722,9 +748,13 @@ __global__ __launch_bounds__(ELEM_BLOCK) __attribute__((amdgpu_waves_per_eu(ELEM
                                                          ElemSpec X)
 {
     if (int(blockIdx.x) < X.nspecblk) {  // speculative setup lanes of the next half
-        const int t = int(blockIdx.x) * int(blockDim.x) + int(threadIdx.x);
-        const int c = t < X.nspec ? 0 : 1;
-        if (t < 2 * X.nspec) setup_any(X.S[c], t - c * X.nspec);
+        // candidate c's lanes fill blocks [c * nb, (c + 1) * nb): c is uniform
+        // in a block, so X.S[c] is selected in scalar registers (a lane-varying
+        // c made the compiler keep both SetupArgs in a private array)
+        const int nb = (X.nspec + int(blockDim.x) - 1) / int(blockDim.x);
+        const int c = int(blockIdx.x) < nb ? 0 : 1;
+        const int t = (int(blockIdx.x) - c * nb) * int(blockDim.x) + int(threadIdx.x);
+        if (t < X.nspec) setup_any(X.S[__builtin_amdgcn_readfirstlane(c)], t);
         return;
     }
     const unsigned bid = blockIdx.x - unsigned(X.nspecblk);
@@ -1928,6 +1958,49 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
     }
 }
 
+// -------------------------------------------------------------- k_gp_dcp
+// GP trees: the changepoint distance of pairs whose walker tripped the
+// cache rule (k_setup marked them G_GP_OK = 2): dist_cp = (dphi + phi4 -
+// phi3) / 2 with phi3 / phi4 = wdphases(q, i, rwd, 10) (CVModel.py:561-570,
+// MODEL_SPEC 10.2-10.3).  16 lanes per pair, lane k < 10 solves limb point k
+// (the nested eclipse solver), min / max by shuffles; other pairs return at
+// once.  Runs after k_elements (the pair's record is in the standard slot)
+// and before k_lnlike<2>, which reads G_GP_DCP.
+constexpr int DCP_LANES = 16, DCP_NTHETA = 10;
+__global__ __launch_bounds__(64) void k_gp_dcp(double* __restrict__ geo, const int* __restrict__ status, int npairs)
+{
+    const int pair = int(blockIdx.x) * (64 / DCP_LANES) + int(threadIdx.x) / DCP_LANES;
+    const int k = int(threadIdx.x) % DCP_LANES;
+    if (pair >= npairs) return;
+    double* G = geo + size_t(pair) * LFG_NGEO;
+    if (G[G_GP_OK] != 2.0) return;  // uniform over the pair's 16 lanes
+    bool ok = status[pair] == ST_OK && G[G_GP_RWD] > 0.0;
+    double b = NAN;
+    if (ok && k < DCP_NTHETA) {
+        const Roche R{G[G_Q], G[G_CA], G[G_CB], G[G_MU], G[G_XL1], G[G_PL1], G[G_RS], G[G_RS2]};
+        const double s = G[G_S], c = G[G_C], r1 = G[G_GP_RWD];
+        double dphi_c;
+        if (findphi_fast(R, G[G_INC], dphi_c) == ST_OK) {  // as wdphases: the egress phase of the WD centre
+            double sth, cth, sp, cp, a;
+            sincos(PI * dphi_c, &sth, &cth);
+            sincos(TWO_PI * k / DCP_NTHETA, &sp, &cp);
+            if (!element_interval(R, r1 * (cp * sth - sp * c * cth), r1 * (cp * cth + sp * c * sth), r1 * (sp * s), s,
+                                  c, eggleton(R.q), a, b))
+                b = NAN;
+        }
+    }
+    double lo = isnan(b) ? INFINITY : b, hi = isnan(b) ? -INFINITY : b;
+    for (int off = DCP_LANES / 2; off > 0; off >>= 1) {
+        lo = fmin(lo, __shfl_xor(lo, off, DCP_LANES));
+        hi = fmax(hi, __shfl_xor(hi, off, DCP_LANES));
+    }
+    if (k == 0) {
+        ok = ok && lo <= hi;  // no eclipsed limb point: wdphases fails
+        G[G_GP_DCP] = ok ? (G[G_GP_DPHI] + (hi - lo)) / 2.0 : NAN;
+        G[G_GP_OK] = ok ? 1.0 : 0.0;
+    }
+}
+
 // -------------------------------------------------------------- k_gp_like
 // GP trees (MODEL_SPEC 10.4): the Kalman filter over each pair's residuals
 // (k_lnlike<2> wrote them), one LANE per pair.  The recursion is serial in
@@ -2498,7 +2571,7 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
                 N.jkout = ws.jk + size_t(hn) * W;
             }
             X.nspec = 2 * npairs + W;
-            X.nspecblk = ((2 * X.nspec + ELEM_BLOCK - 1) / ELEM_BLOCK + 7) / 8 * 8;  // keeps the pair -> XCD map
+            X.nspecblk = (2 * ((X.nspec + ELEM_BLOCK - 1) / ELEM_BLOCK) + 7) / 8 * 8;  // keeps the pair -> XCD map
         }
     }
     int rc = run_front(S, ws, st, ev, !kFused, &X, !(sp && sp->in));
@@ -2516,6 +2589,9 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
         L.res = ws.res;
         L.gpx = ws.gpx;
         L.gpb = ws.gpb;
+        hipLaunchKernelGGL(k_gp_dcp, dim3((npairs + 64 / DCP_LANES - 1) / (64 / DCP_LANES)), dim3(64), 0, st, ws.geo,
+                           ws.status, npairs);
+        if ((rc = launch_ok())) return rc;
         hipLaunchKernelGGL((k_lnlike<2, kFused>), dim3(npairs), dim3(LIKE_THREADS), 0, st, L);
         if ((rc = launch_ok())) return rc;
         hipLaunchKernelGGL(k_gp_like, dim3((npairs + GP_LANES - 1) / GP_LANES), dim3(GP_BLOCK), 0, st, L);

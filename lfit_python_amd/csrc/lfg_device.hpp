@@ -64,6 +64,7 @@ enum Geo {
     G_FIS, G_PHI0, G_WDF, G_DF, G_SF, G_RSF, G_RPRIOR, G_RCAL,
     G_RPRIOR_BS,  // bright-spot part of the eclipse Roche prior (stream lanes)
     G_GP_AIN, G_GP_AOUT, G_GP_LAM, G_GP_DCP, G_GP_OK,  // GP likelihood (MODEL_SPEC 10)
+    G_GP_DPHI, G_GP_RWD,  // a changepoint distance pending (G_GP_OK = 2): the walker's dphi, rwd for k_gp_dcp
     G_COUNT
 };
 static_assert(G_COUNT <= 48, "LFG_NGEO");

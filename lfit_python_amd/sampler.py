@@ -302,9 +302,10 @@ class EnsembleSampler:
         the half (n = W / 2 / nranks) through the multi-rank kernels, the
         exchange moves that shard alone (a one-rank group's all_gather with
         force_exchange), and the acceptance runs over the whole half as on
-        every rank.  The other shards' entries of the gathered ln_prob are
-        left as the last values written there, so the chain is NOT a valid
-        sample; the launches are exactly rank k's (bench.py --emulate-rank)."""
+        every rank.  The other shards' entries of the gathered ln_prob stay
+        -inf, so their walkers never move (they stay in the valid starting
+        ball and keep rank k's partners realistic); the chain is NOT a valid
+        sample, but the launches are exactly rank k's (bench.py --emulate-rank)."""
         ns = self.W // 2
         if ns % nranks or not (0 <= k < nranks):
             raise ValueError("W/2 = %d does not shard over %d ranks" % (ns, nranks))
@@ -312,6 +313,7 @@ class EnsembleSampler:
         self.shard = ns // nranks
         self._emu = (int(k), int(nranks))
         self._q_sh = self._zf_sh = self._lnp_sh = None
+        self.lnp_new.fill_(float("-inf"))
 
     def _shard_half(self, half):
         import torch

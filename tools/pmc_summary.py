@@ -12,7 +12,7 @@ import sys
 
 d = sys.argv[1]
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
-for f in sorted(glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv"), recursive=True)):
+for f in sorted(glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)):
     per = collections.defaultdict(float)
     grid = {}
     for r in csv.DictReader(open(f)):
