@@ -1374,109 +1374,216 @@ __device__ __forceinline__ double direct_donor(const double* DONp, double e0, do
 }
 
 
-// ---- the fused element phase of k_lnlike (FUSED = true) ----
-// k_elements' item body (MODEL_SPEC 5, 4.3) with its outputs in the block's
-// LDS instead of HBM: WD/disc intervals in sweep order into `stage`, spot
-// intervals and weights into sab / sbw, donor tiles into sdq, disc ring
-// weights and the disc total into swt.  ABg (nullable): the pair's global
-// interval table, kept only when a window of the pair is unsorted and the
-// direct (point-major) WD/disc path may need every interval.
-__device__ __noinline__ void element_item(int u, const double* __restrict__ G, double2* stage, double2* sab,
-                                             double* sbw, double* sdq, double* swt, double2* ABg)
+
+// ---- S > 1: the spot and donor from per-pair breakpoint tables ----
+// With sub-bins the spot's eclipse and the donor's visibility are needed at
+// N S sub-phases.  Instead of one sweep (every spot element and donor tile
+// located in the pass's windows, a block scan) per tile and sub-bin, the
+// pair's breakpoints are bucketed once into TCELLS uniform cells (counting
+// sort in LDS) with int64 fixed-point prefix sums per cell, and every
+// sub-bin is a lookup: the prefix of its cell plus the few entries of the
+// cell (MODEL_SPEC 3, 5.3-5.4 restated; the sums are exact integers, so
+// entry order inside a cell does not matter).
+//  * donor (point mode at the sub-bin centre th): V(th) = sum of the tile
+//    vectors visible at th; tile arc (cen - hw, cen + hw) mod 1: +q at its
+//    start (counted for th > start), -q at its end (counted for th >= end);
+//    arcs wrapping past +-1/2 and always-visible tiles go into V0, and
+//    breakpoints outside the cells' range [t0, t1] are folded into V0 or dropped;
+//  * spot (window [lo, hi]): E = C(lo) + [sum over elements with a
+//    breakpoint inside (lo, hi) of the partial overlaps] / (hi - lo), with
+//    C(x) = the weight of the elements covering x (a_k <= x < b_k): +W_k at
+//    a_k, -W_k at b_k, both counted for x >= pos.  Zero-width windows: the
+//    elements with a_k < ph < b_k.
+constexpr int TCELLS = 256;
+constexpr int TD_MAX = 2 * NDONOR, TS_MAX = 2 * NBS;
+struct SubTables {
+    long long dpre[TCELLS][3];   // donor: V at each cell's start (V0 + cells below), fixed point
+    long long spre[TCELLS];      // spot: covering weight at each cell's start
+    int dend[TCELLS], send[TCELLS];  // entry counts -> exclusive offsets -> (after the scatter) cell ends
+    double spos[TS_MAX];
+    int scode[TS_MAX];           // element k: 2 k + (1: end b_k)
+    long long dv0[3];
+    double dt0, dginv, st0, sginv;
+};
+struct SubEntries {              // donor entries (in sacc rows 2..5: free when S > 1)
+    double dpos[TD_MAX];
+    int dcode[TD_MAX];           // tile t (0..399 as the donor lanes number them): 2 t + (1: end)
+};
+static_assert(sizeof(SubEntries) <= 4 * (LIKE_TILE + 1) * sizeof(unsigned long long), "donor entries fit sacc[2..5]");
+
+__device__ __forceinline__ int tcell(double x, double t0, double ginv)
 {
-    const Roche R{G[G_Q], G[G_CA], G[G_CB], G[G_MU], G[G_XL1], G[G_PL1], G[G_RS], G[G_RS2]};
-    const double s = G[G_S], c = G[G_C];
-    if (u >= U_WD + U_DISC && u < U_MAIN) {  // donor tile (MODEL_SPEC 5.4), phi' in (0, pi/2)
-        const int uu = u - (U_WD + U_DISC);
-        const int it = uu / (NDONOR_P / 4), ip = uu - it * (NDONOR_P / 4);
-        const double stc = kDonSt[it], ctc = kDonCt[it];
-        const double dx = -ctc, dy = stc * kDonCp[ip], dz = stc * kDonSp[ip];
-        double lo = 0.0, hi = R.Rs, r = G[G_REFF];
-        if (!(r > lo && r < hi)) r = 0.5 * hi;
-        double gx, gy, gz;
-        for (int itr = 0; itr < ROOT_MAXIT; ++itr) {
-            const double X0 = fma(r, dx, 1.0), X1 = r * dy, X2 = r * dz;
-            const double f = rpot_grad(R, X0, X1, X2, gx, gy, gz) - R.pl1;
-            const double df = gx * dx + gy * dy + gz * dz;
-            if (f > 0.0) hi = r; else lo = r;
-            if (df > 0.0 && fabs(f / df) <= ROOT_LAST) { r -= f / df; break; }
-            double rn = (df > 0.0) ? r - f / df : 0.5 * (lo + hi);
-            if (!(rn > lo && rn < hi)) rn = 0.5 * (lo + hi);
-            r = rn;
-        }
-        rgrad(R, fma(r, dx, 1.0), r * dy, r * dz, gx, gy, gz);
-        const double ig = rsqrt(gx * gx + gy * gy + gz * gz);
-        const double nx = gx * ig, ny = gy * ig, nz = gz * ig;
-        const double dA = r * r * kDonOmega[it] / (nx * dx + ny * dy + nz * dz);
-        const double vx = dA * nx, vy = dA * ny, vz = dA * nz;
-        const double srho = s * sqrt(vx * vx + vy * vy);
-        const double kap = (srho > 0.0) ? -c * vz / srho : (c * vz > 0.0 ? -2.0 : 2.0);
-        double* D = sdq + uu * DON_STRIDE;
-        D[0] = vx;
-        D[1] = vy;
-        D[2] = vz;
-        D[3] = -atan2(vy, vx) * (1.0 / TWO_PI);
-        D[4] = acos(fmin(fmax(kap, -1.0), 1.0)) * (1.0 / TWO_PI);
-        return;
-    }
-    double Px, Py, Pz;
-    if (u < U_WD) {  // white dwarf tile (MODEL_SPEC 5.1), cos(psi) > 0 half
-        const int ir = wd_ring_of(u);
-        const double rc = kWdRc[ir], mu0 = kWdMu0[ir];
-        const double cp = kWdCos[u], sp = kWdSin[u];
-        const double rw = G[G_RWD];
-        Px = rw * (-rc * sp * c + mu0 * s);
-        Py = rw * (rc * cp);
-        Pz = rw * (rc * sp * s + mu0 * c);
-    } else if (u < U_WD + U_DISC) {  // disc (MODEL_SPEC 5.2), alpha in (0, pi)
-        const int uu = u - U_WD;
-        const int ir = uu / (NDISC_AZ / 2), j = uu - ir * (NDISC_AZ / 2);
-        const double rin = G[G_RWD];
-        const double rc = rin + (ir + 0.5) * ((G[G_RDISC] - rin) / NDISC_R);
-        if (j == 0) {
-            swt[WT_DISC + ir] = disc_ring_weight(ir, G);
-            if (ir == 0) swt[WT_TD] = TWO_PI * (disc_boundary(NDISC_R, G) - disc_boundary(0, G));
-        }
-        Px = rc * kDiscCos[j];
-        Py = rc * kDiscSin[j];
-        Pz = 0.0;
-    } else {  // bright-spot strip (MODEL_SPEC 5.3): no mirror partner
-        const int j = u - U_MAIN;
-        const double uk = (j + 0.5) * (G[G_UMAX] / NBS);
-        sbw[j] = bs_weight(j, G);
-        const double off = G[G_L] * (uk - G[G_UPK]);
-        Px = fma(off, G[G_CAZ], G[G_BSX]);
-        Py = fma(off, G[G_SAZ], G[G_BSY]);
-        Pz = 0.0;
-    }
-    double a, b;
-    element_interval_fast(R, Px, Py, Pz, s, c, G[G_RCAL], G[G_REFF], a, b);
-    if (u >= U_MAIN) {
-        sab[u - U_MAIN] = make_double2(a, b);
-        if (ABg) ABg[NU_WDD + (u - U_MAIN)] = make_double2(a, b);
-        return;
-    }
-    stage[uslot(u)] = make_double2(a, b);
-    if (ABg) ABg[uslot(u)] = make_double2(a, b);
+    const double u = (x - t0) * ginv;
+    return u <= 0.0 ? 0 : (u >= double(TCELLS - 1) ? TCELLS - 1 : int(u));
 }
 
-// does every exposure window of the pair's points come in sorted order
-// (the sweep's precondition; MODEL_SPEC 6 restated)?  1 when not: the
-// direct WD/disc path will need the global interval table
-__device__ __forceinline__ int windows_unsorted(const LikeArgs& L, int o0, int n, double phi0, int tid)
+// donor tile t's fixed-point vector (mirror image t & 3 of unique tile t >> 2),
+// exactly as its lane forms it
+__device__ __forceinline__ void donor_q(const double* sdq, int t, double ivs, long long& qx, long long& qy, long long& qz)
 {
-    int bad = 0;
-    for (int p = tid; p < n; p += LIKE_THREADS) {
-        const double hw = L.w ? L.w[o0 + p] : 0.0;
-        const double ph = wrap_phase(L.x[o0 + p] - phi0);
-        bad |= (hw >= 0.0) ? 0 : 1;
-        if (p > 0) {
-            const double hwb = L.w ? L.w[o0 + p - 1] : 0.0;
-            const double phb = wrap_phase(L.x[o0 + p - 1] - phi0);
-            bad |= (ph - hw < phb - hwb || ph + hw < phb + hwb) ? 1 : 0;
+    const int mr = t & 3;
+    const double* dq = sdq + (t >> 2) * DON_STRIDE;
+    qx = to_fx(dq[0] * ivs);
+    qy = to_fx(((mr & 1) ? -dq[1] : dq[1]) * ivs);
+    qz = to_fx(((mr & 2) ? -dq[2] : dq[2]) * ivs);
+}
+
+// wave-wide min / max (shuffles; once per pair)
+__device__ __forceinline__ double wave_min(double v)
+{
+    for (int off = 32; off > 0; off >>= 1) v = fmin(v, __shfl_xor(v, off, 64));
+    return v;
+}
+__device__ __forceinline__ double wave_max(double v)
+{
+    for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
+    return v;
+}
+
+// exclusive prefix over TCELLS cells of NA int64 arrays held one cell per
+// thread (threads >= TCELLS pass zeros); totals of each wave through part[]
+template <int NA>
+__device__ __forceinline__ void cell_scan(long long (&v)[NA], long long (*part)[LIKE_THREADS / 64], int tid)
+{
+    const int lane = tid & 63, wv = tid >> 6;
+    long long incl[NA];
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+        incl[i] = wave_scan_incl(v[i], lane);
+        if (lane == 63) part[i][wv] = incl[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+        long long off = 0;
+        for (int k = 0; k < wv; ++k) off += part[i][k];
+        v[i] = incl[i] - v[i] + off;
+    }
+}
+
+// spot eclipse fraction of window [lo, hi] (h = (hi - lo) / 2; h = 0: point ph = lo)
+__device__ __forceinline__ double sub_spot(const SubTables& T, const double2* sab, const double* sbw, double itb,
+                                           double lo, double hi, double amin, double bmax)
+{
+    const bool pt = !(hi > lo);
+    if (pt ? !(lo > amin && lo < bmax) : !(hi > amin && lo < bmax)) return 0.0;
+    const int g0 = tcell(lo, T.st0, T.sginv), g1 = pt ? g0 : tcell(hi, T.st0, T.sginv);
+    long long C = T.spre[g0];
+    double corr = 0.0;
+    for (int g = g0; g <= g1; ++g) {
+        for (int i = g ? T.send[g - 1] : 0; i < T.send[g]; ++i) {
+            const double pos = T.spos[i];
+            const int code = T.scode[i], k = code >> 1;
+            const bool end = code & 1;
+            if (g == g0 && pos <= lo) {
+                const long long W = to_fx(sbw[k] * itb);
+                // point mode: eclipsed when a_k < ph < b_k (MODEL_SPEC 5; the oracle's rule)
+                C += end ? -W : ((pt && pos == lo) ? 0 : W);
+            } else if (!pt && pos < hi) {
+                const double2 ab = sab[k];
+                const double wn = sbw[k] * itb;
+                if (!end) corr = fma(wn, fmin(ab.y, hi) - ab.x, corr);
+                else if (ab.x <= lo) corr = fma(-wn, hi - ab.y, corr);
+            }
         }
     }
-    return bad;
+    const double e = double(C) * FX_INV;
+    return pt ? e : fma(corr, 1.0 / (hi - lo), e);
+}
+
+// donor sum vector V (fixed point) at phase th
+__device__ __forceinline__ void sub_donor(const SubTables& T, const SubEntries& D, const double* sdq, double ivs,
+                                          double th, long long& vx, long long& vy, long long& vz)
+{
+    const int g = tcell(th, T.dt0, T.dginv);
+    vx = T.dpre[g][0];
+    vy = T.dpre[g][1];
+    vz = T.dpre[g][2];
+    for (int i = g ? T.dend[g - 1] : 0; i < T.dend[g]; ++i) {
+        const double pos = D.dpos[i];
+        const int code = D.dcode[i];
+        const bool end = code & 1;
+        if (end ? pos <= th : pos < th) {
+            long long qx, qy, qz;
+            donor_q(sdq, code >> 1, ivs, qx, qy, qz);
+            if (end) { vx -= qx; vy -= qy; vz -= qz; }
+            else { vx += qx; vy += qy; vz += qz; }
+        }
+    }
+}
+
+
+// this lane's breakpoints of the S > 1 tables (<= 2): donor tile t (lanes
+// nt - NDONOR ..) or spot element (lanes < NBS); formed twice (count, then
+// scatter) instead of held across the barriers between.  v0: how many times
+// the tile's vector goes into V0 (+-1, 0)
+__device__ __forceinline__ void lane_breakpoints(int tid, const double* sdq, const double2* sab, double t0d, double t1d,
+                                                 double& p0, double& p1, bool& in0, bool& in1, int& v0)
+{
+    // slot 0: the start (code 2 x), slot 1: the end (code 2 x + 1); fixed
+    // slots (a compacted pair indexed by a count went to scratch)
+    in0 = in1 = false;
+    p0 = p1 = 0.0;
+    v0 = 0;
+    if (tid >= LIKE_THREADS - NDONOR) {
+        const int t = tid - (LIKE_THREADS - NDONOR), mr = t & 3;
+        const double* dq5 = sdq + (t >> 2) * DON_STRIDE;
+        const double cen = (mr & 1) ? -dq5[3] : dq5[3];
+        const double hw = (mr & 2) ? 0.5 - dq5[4] : dq5[4];
+        if (!(hw > 0.0)) return;
+        double sp = NAN, ep = NAN;  // start (counted for th > sp), end (counted for th >= ep)
+        if (hw >= 0.5) {
+            v0 = 1;
+        } else {
+            const double lo = cen - hw, hi = cen + hw;
+            if (lo < -0.5) { v0 = 1; ep = hi; sp = lo + 1.0; }
+            else if (hi > 0.5) { v0 = 1; ep = hi - 1.0; sp = lo; }
+            else { sp = lo; ep = hi; }
+        }
+        if (sp == sp) {  // a start below the range counts for every phase; at or above t1 for none
+            if (sp < t0d) v0 += 1;
+            else if (sp < t1d) { p0 = sp; in0 = true; }
+        }
+        if (ep == ep) {
+            if (ep <= t0d) v0 -= 1;
+            else if (ep <= t1d) { p1 = ep; in1 = true; }
+        }
+    } else if (tid < NBS) {
+        const double2 ab = sab[tid];
+        if (ab.x < ab.y) {
+            p0 = ab.x;
+            p1 = ab.y;
+            in0 = in1 = true;
+        }
+    }
+}
+
+
+// S > 1: the spot and donor terms of one point, summed over its S sub-bins
+// (spot eclipse over each sub-bin window, donor at each sub-bin centre, from
+// the tables).
+__device__ __forceinline__ double2 sub_point(const SubTables& T, const SubEntries& D, const double2* sab, const double* sbw,
+                                          const double* sdq, const double* snorm, const double* shull, const double* SG,
+                                          double ph0, double wk, int S)
+{
+    const double sg = SG[G_S], cg = SG[G_C], bden = SG[G_BDEN], fis = SG[G_FIS];
+    const double h = wk / S;
+    double sbs = 0.0, srs = 0.0;
+    for (int j = 0; j < S; ++j) {
+        const double ph = wrap_phase(ph0 - wk + (2 * j + 1) * h);
+        const double ebj = sub_spot(T, sab, sbw, snorm[0], ph - h, ph + h, shull[2], shull[3]);
+        long long vx, vy, vz;
+        sub_donor(T, D, sdq, snorm[1], ph, vx, vy, vz);
+        const double2 scp2 = sincospi_ool(2.0 * ph);
+        const double e0 = sg * scp2.y, e1 = -sg * scp2.x;
+        const double Dv = (e0 * double(vx) + e1 * double(vy) + cg * double(vz)) * (FX_INV * snorm[3]);
+        double beam = 0.0;
+        if (bden > 0.0)
+            beam = (fis + (1.0 - fis) * fmax(SG[G_NB0] * e0 + SG[G_NB1] * e1 + SG[G_NB2] * cg, 0.0)) / bden;
+        sbs += beam * (1.0 - ebj);
+        srs += Dv / snorm[2];
+    }
+    return make_double2(sbs, srs);
 }
 
 #ifdef LFG_PROFILE_LIKE  // diagnostic build only: phase stamps (first tile) into spare geo slots 41..46
@@ -1542,9 +1649,9 @@ __device__ inline void finish_walker(const LikeArgs& L, int pair, int tid, bool 
 // MODE 0: flux (and components) only; 1: fused chi^2 -> ln_like; 2: GP
 // ln_like of the residuals (a Kalman filter over each tile's sorted points,
 // run by wave 0 while the other waves wait at the tile barrier)
-// FUSED: the pair's element intervals are solved in this block (the
-// element phase) straight into LDS, instead of read from k_elements' table
-template <int MODE, bool FUSED>
+// SUB: nsub > 1 (the table path for the spot and donor, MODE as above); the
+// host launches SUB = (nsub > 1), so each instantiation holds only its path
+template <int MODE, bool SUB>
 __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
 {
     constexpr bool CHI = MODE != 0, GP = MODE == 2;
@@ -1565,24 +1672,30 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
     __shared__ double sacc1[3];                   // fused acceptance: ln u, zfac, old ln_prob
     __shared__ double snorm[4];                   // 1 / spot total, 1 / donor |v| sum, donor norm, |v| sum
     __shared__ double sgeo[LFG_NGEO];             // the pair's geometry record, read at use in the tile loop
-    // TA: WD/disc windows.  TB: the spot windows of the current sub-bin when
-    // S > 1; at S = 1 (spot windows = TA's) its space holds second copies of
-    // the WD and disc difference arrays, taken by the odd lanes of the sweep:
-    // half the same-address LDS atomics where contacts cluster (four WD
-    // copies measured no faster: more arrays to zero and scan)
+    // TA: WD/disc windows.  S = 1: the spot sweep reuses TA's windows, and
+    // SU.s1.X holds second copies of the WD and disc difference arrays, taken
+    // by the odd lanes of the sweep (half the same-address LDS atomics where
+    // contacts cluster; four WD copies measured no faster), sph / scp the
+    // donor's phases and their cells.  S > 1: SU.tb, the pair's breakpoint
+    // tables (spot and donor), with the donor entries in sacc rows 2..5.
     __shared__ TileBufs TA;
-    __shared__ union TBU_ {
-        TileBufs B;
-        unsigned long long X[2][LIKE_TILE + 1];
-    } TBU;
-    TileBufs& TB = TBU.B;
-    __shared__ double sph[LIKE_TILE];  // sub-bin centre phases (donor)
-    __shared__ int scp[LIKE_NC + 1];
+    __shared__ union SubU_ {
+        struct {
+            unsigned long long X[2][LIKE_TILE + 1];
+            double sph[LIKE_TILE];  // point phases (donor)
+            int scp[LIKE_NC + 1];
+        } s1;
+        SubTables tb;
+    } SU;
+    double* const sph = SU.s1.sph;
+    int* const scp = SU.s1.scp;
+    __shared__ double shull[4];  // WD/disc and spot element hulls: min a, max b (eclipsed elements)
+    __shared__ double shw[4][LIKE_THREADS / 64];  // their wave partials
+    __shared__ double sqr[2][LIKE_THREADS / 64];  // S > 1: wave partials of the sub-bin phase range
     __shared__ unsigned long long sacc[6][LIKE_TILE + 1];
     __shared__ long long spart[6][LIKE_THREADS / 64];
     __shared__ double red[3][LIKE_THREADS / 64];
     __shared__ int sflag[2];
-    __shared__ double swt[FUSED ? WT_N : 1];      // fused: disc ring weights and total (spot weights in sbw)
 
     constexpr int nt = LIKE_THREADS, nw = LIKE_THREADS / 64;
     const int pair = blockIdx.x;
@@ -1644,80 +1757,34 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
     double dq[DON_STRIDE] = {0.0, 0.0, 0.0, 0.0, 0.0};
     double gv = 0.0;     // one geometry word per lane for sgeo
     double wring = 0.0;  // ring weights for the direct path
-    if constexpr (FUSED) {
-        // the element phase: status (setup failures first, then the stream:
-        // MODEL_SPEC 6), geometry into LDS, every symmetry-unique element of
-        // the pair solved by the block's lanes into LDS
-        st = L.status[pair];
-        const int bst = L.bstatus[pair];
-        if (st == ST_OK && bst != ST_OK) st = bst;
-        if (tid < G_COUNT) sgeo[tid] = G[tid];
-        if (tid < n) {
-            px = L.x[o0 + tid];
-            pw = L.w ? L.w[o0 + tid] : 0.0;
-        }
-        if (tid == 0) {
-            sflag[0] = 0;
-            if (st != L.status[pair]) const_cast<int*>(L.status)[pair] = st;
-        }
-        if (st == ST_OK && prej) st = ST_PRIOR_SKIP;
-        __syncthreads();
-        if (st == ST_OK) {
-            if (windows_unsorted(L, o0, n, sgeo[G_PHI0], tid)) atomicOr(&sflag[0], 1);
-            __syncthreads();
-            double2* stage = reinterpret_cast<double2*>(&sacc[0][0]);  // free until the first pass
-            double2* ABg = sflag[0] ? const_cast<double2*>(AB) : nullptr;
-            for (int u = tid; u < NUNIQ; u += nt) element_item(u, sgeo, stage, sab, sbw, sdq, swt, ABg);
-            __syncthreads();
-            for (int i = 0; i < NI; ++i) {
-                const int g = tid + i * nt;
-                abk[i] = (g < NWD + NDISC) ? sweep_ab(stage, g) : make_double2(1.0, -1.0);
-            }
-            if (tid < NBS) {
-                abB = sab[tid];
-                wB = sbw[tid];
-            } else if (tid >= nt - NDONOR) {
-                const int t = tid - (nt - NDONOR);
-                for (int i = 0; i < DON_STRIDE; ++i) dq[i] = sdq[(t >> 2) * DON_STRIDE + i];
-            }
-        }
-        s = sgeo[G_S];
-        c = sgeo[G_C];
-        ul = sgeo[G_ULIMB];
-        td = swt[WT_TD];
-        if (tid >= NBS && tid < NBS + NWD_RINGS) wring = wd_ring_weight(tid - NBS, ul);
-        else if (tid >= NBS + NWD_RINGS && tid < NBS + NWD_RINGS + NDISC_R)
-            wring = swt[WT_DISC + tid - NBS - NWD_RINGS];
-    } else {
-        // every global load of the prologue is issued before anything waits on
-        // one (the status included): a single memory round trip
-        st = L.status[pair];
-        if (st == ST_OK && prej) st = ST_PRIOR_SKIP;
-        s = G[G_S];
-        c = G[G_C];
-        ul = G[G_ULIMB];
-        td = Wt[WT_TD];
-        if (tid < n) {
-            px = L.x[o0 + tid];
-            pw = L.w ? L.w[o0 + tid] : 0.0;
-        }
-        for (int i = 0; i < NI; ++i) {
-            const int g = tid + i * nt;
-            abk[i] = (g < NWD + NDISC) ? sweep_ab(AB, g) : make_double2(1.0, -1.0);
-        }
-        if (tid < NBS) {
-            abB = AB[NU_WDD + tid];
-            wB = Wt[WT_BS + tid];
-        } else if (tid >= nt - NDONOR) {
-            const int t = tid - (nt - NDONOR);
-            for (int i = 0; i < DON_STRIDE; ++i) dq[i] = DONp[(t >> 2) * DON_STRIDE + i];
-        }
-        if (tid >= NBS + NWD_RINGS + NDISC_R && tid < NBS + NWD_RINGS + NDISC_R + G_COUNT)
-            gv = G[tid - (NBS + NWD_RINGS + NDISC_R)];
-        if (tid >= NBS && tid < NBS + NWD_RINGS) wring = wd_ring_weight(tid - NBS, ul);
-        else if (tid >= NBS + NWD_RINGS && tid < NBS + NWD_RINGS + NDISC_R)
-            wring = Wt[WT_DISC + tid - NBS - NWD_RINGS];
+    // every global load of the prologue is issued before anything waits on
+    // one (the status included): a single memory round trip
+    st = L.status[pair];
+    if (st == ST_OK && prej) st = ST_PRIOR_SKIP;
+    s = G[G_S];
+    c = G[G_C];
+    ul = G[G_ULIMB];
+    td = Wt[WT_TD];
+    if (tid < n) {
+        px = L.x[o0 + tid];
+        pw = L.w ? L.w[o0 + tid] : 0.0;
     }
+    for (int i = 0; i < NI; ++i) {
+        const int g = tid + i * nt;
+        abk[i] = (g < NWD + NDISC) ? sweep_ab(AB, g) : make_double2(1.0, -1.0);
+    }
+    if (tid < NBS) {
+        abB = AB[NU_WDD + tid];
+        wB = Wt[WT_BS + tid];
+    } else if (tid >= nt - NDONOR) {
+        const int t = tid - (nt - NDONOR);
+        for (int i = 0; i < DON_STRIDE; ++i) dq[i] = DONp[(t >> 2) * DON_STRIDE + i];
+    }
+    if (tid >= NBS + NWD_RINGS + NDISC_R && tid < NBS + NWD_RINGS + NDISC_R + G_COUNT)
+        gv = G[tid - (NBS + NWD_RINGS + NDISC_R)];
+    if (tid >= NBS && tid < NBS + NWD_RINGS) wring = wd_ring_weight(tid - NBS, ul);
+    else if (tid >= NBS + NWD_RINGS && tid < NBS + NWD_RINGS + NDISC_R)
+        wring = Wt[WT_DISC + tid - NBS - NWD_RINGS];
     // the acceptance draw by the block's last lane, after its prologue loads
     // are in flight (in wave 0 the Philox rounds and the log delayed every
     // load of that wave's prologue)
@@ -1743,7 +1810,7 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
     }
     double tb = 0.0, dn = 0.0, vs = 0.0;
     if (tid < NBS) {
-        if (!FUSED) sbw[tid] = wB;
+        sbw[tid] = wB;
         tb = wB;
     } else if (tid >= nt - NDONOR) {
         // donor normalisation at quadrature (theta = pi/2): e = (0, -s, c)
@@ -1753,12 +1820,21 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
         vs = fabs(dq[0]) + fabs(dq[1]) + fabs(dq[2]);
     }
     if (tid >= NBS && tid < NBS + NWD_RINGS + NDISC_R) swr[tid - NBS] = wring;
-    if (!FUSED) {
+    {
         if (tid >= NBS + NWD_RINGS + NDISC_R && tid < NBS + NWD_RINGS + NDISC_R + G_COUNT)
             sgeo[tid - (NBS + NWD_RINGS + NDISC_R)] = gv;
         if (tid < NBS) sab[tid] = abB;
         else if (tid >= nt - NDONOR && ((tid - (nt - NDONOR)) & 3) == 0)
             for (int i = 0; i < DON_STRIDE; ++i) sdq[((tid - (nt - NDONOR)) >> 2) * DON_STRIDE + i] = dq[i];
+    }
+    {   // hulls of the eclipsed WD/disc and spot intervals (tiles outside skip them)
+        double wa = INFINITY, wb = -INFINITY, sa = INFINITY, sb = -INFINITY;
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+            if (abk[i].x < abk[i].y) { wa = fmin(wa, abk[i].x); wb = fmax(wb, abk[i].y); }
+        if (tid < NBS && abB.x < abB.y) { sa = abB.x; sb = abB.y; }
+        wa = wave_min(wa); wb = wave_max(wb); sa = wave_min(sa); sb = wave_max(sb);
+        if (lane == 0) { shw[0][wv] = wa; shw[1][wv] = wb; shw[2][wv] = sa; shw[3][wv] = sb; }
     }
     tb = wave_sum(tb);
     dn = wave_sum(dn);
@@ -1782,6 +1858,11 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
             snorm[2] = p1;
             snorm[3] = p2;
         }
+        if (lane < 4) {
+            double h = (lane & 1) ? -INFINITY : INFINITY;
+            for (int k = 0; k < nw; ++k) h = (lane & 1) ? fmax(h, shw[lane][k]) : fmin(h, shw[lane][k]);
+            shull[lane] = h;
+        }
     }
     const double twd = TWO_PI * ((1.0 - ul) * 0.5 + ul / 3.0);  // 2 pi [F(1) - F(0)]
     if (tid >= NBS && tid < NBS + NWD_RINGS + NDISC_R)  // visible to the sweep after the pass barrier
@@ -1791,6 +1872,116 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
     // loads of G would hold ~13 doubles in VGPRs through every pass)
     const double* SG = sgeo;
     const int S = L.nsub;
+    constexpr bool TAB = SUB;  // sub-bins: the spot and donor from breakpoint tables
+    SubEntries& DE = *reinterpret_cast<SubEntries*>(&sacc[2][0]);
+    if (TAB) {
+        SubTables& T = SU.tb;
+        // (a) the range of every sub-bin centre of the pair (the donor cells
+        // span it), and the tables zeroed
+        double qlo = INFINITY, qhi = -INFINITY;
+        for (int p = tid; p < n; p += nt) {
+            const double xp = L.x[o0 + p], wp = L.w ? L.w[o0 + p] : 0.0;
+            const double a0 = xp - SG[G_PHI0], hp = wp / S;
+            for (int j = 0; j < S; ++j) {
+                const double ph = wrap_phase(a0 - wp + (2 * j + 1) * hp);
+                qlo = fmin(qlo, ph);
+                qhi = fmax(qhi, ph);
+            }
+        }
+        for (int g = tid; g < TCELLS; g += nt) {
+            T.dpre[g][0] = T.dpre[g][1] = T.dpre[g][2] = 0;
+            T.spre[g] = 0;
+            T.dend[g] = T.send[g] = 0;
+        }
+        if (tid < 3) T.dv0[tid] = 0;
+        qlo = wave_min(qlo);
+        qhi = wave_max(qhi);
+        if (lane == 0) { sqr[0][wv] = qlo; sqr[1][wv] = qhi; }
+        __syncthreads();
+        double t0d = INFINITY, t1d = -INFINITY;
+        for (int k = 0; k < nw; ++k) { t0d = fmin(t0d, sqr[0][k]); t1d = fmax(t1d, sqr[1][k]); }
+        const double dginv = (t1d > t0d) ? TCELLS / (t1d - t0d) : 0.0;
+        const double st0 = shull[2], sginv = (shull[3] > shull[2]) ? TCELLS / (shull[3] - shull[2]) : 0.0;
+        if (tid == 0) { T.dt0 = t0d; T.dginv = dginv; T.st0 = st0; T.sginv = sginv; }
+        // (b) this lane's breakpoints (<= 2): counts and fixed-point sums per cell
+        {
+            const double itb = snorm[0], ivs = snorm[1];
+            double p0, p1;
+            bool in0, in1;
+            int v0;
+            lane_breakpoints(tid, sdq, sab, t0d, t1d, p0, p1, in0, in1, v0);
+            if (tid >= nt - NDONOR) {
+                long long q[3];
+                donor_q(sdq, tid - (nt - NDONOR), ivs, q[0], q[1], q[2]);
+                if (v0)
+                    for (int k = 0; k < 3; ++k)
+                        atomicAdd(reinterpret_cast<unsigned long long*>(&T.dv0[k]),
+                                  static_cast<unsigned long long>(v0 * q[k]));
+#pragma unroll
+                for (int b = 0; b < 2; ++b) {
+                    if (!(b ? in1 : in0)) continue;
+                    const int g = tcell(b ? p1 : p0, t0d, dginv);
+                    atomicAdd(&T.dend[g], 1);
+                    for (int k = 0; k < 3; ++k)
+                        atomicAdd(reinterpret_cast<unsigned long long*>(&T.dpre[g][k]),
+                                  static_cast<unsigned long long>(b ? -q[k] : q[k]));
+                }
+            } else if (in0) {
+                const long long W = to_fx(sbw[tid] * itb);
+#pragma unroll
+                for (int b = 0; b < 2; ++b) {
+                    const int g = tcell(b ? p1 : p0, st0, sginv);
+                    atomicAdd(&T.send[g], 1);
+                    atomicAdd(reinterpret_cast<unsigned long long*>(&T.spre[g]),
+                              static_cast<unsigned long long>(b ? -W : W));
+                }
+            }
+        }
+        __syncthreads();
+        // (c) exclusive prefixes over the cells: entry offsets, V0 + sums below, covering weights
+        long long v[6] = {0, 0, 0, 0, 0, 0};
+        if (tid < TCELLS) {
+            v[0] = T.dend[tid];
+            v[1] = T.send[tid];
+            v[2] = T.dpre[tid][0];
+            v[3] = T.dpre[tid][1];
+            v[4] = T.dpre[tid][2];
+            v[5] = T.spre[tid];
+        }
+        cell_scan<6>(v, spart, tid);
+        if (tid < TCELLS) {
+            T.dend[tid] = int(v[0]);
+            T.send[tid] = int(v[1]);
+            T.dpre[tid][0] = v[2] + T.dv0[0];
+            T.dpre[tid][1] = v[3] + T.dv0[1];
+            T.dpre[tid][2] = v[4] + T.dv0[2];
+            T.spre[tid] = v[5];
+        }
+        __syncthreads();
+        // (d) the entries into cell order; afterwards dend / send hold each cell's end
+        {
+            double p0, p1;
+            bool in0, in1;
+            int v0;
+            lane_breakpoints(tid, sdq, sab, t0d, t1d, p0, p1, in0, in1, v0);
+            const int base = (tid >= nt - NDONOR) ? 2 * (tid - (nt - NDONOR)) : 2 * tid;
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                if (!(b ? in1 : in0)) continue;
+                const double pos = b ? p1 : p0;
+                if (tid >= nt - NDONOR) {
+                    const int slot = atomicAdd(&T.dend[tcell(pos, t0d, dginv)], 1);
+                    DE.dpos[slot] = pos;
+                    DE.dcode[slot] = base + b;
+                } else {
+                    const int slot = atomicAdd(&T.send[tcell(pos, st0, sginv)], 1);
+                    T.spos[slot] = pos;
+                    T.scode[slot] = base + b;
+                }
+            }
+        }
+        __syncthreads();
+    }
     for (int t0 = 0; t0 < n; t0 += LIKE_TILE) {
         double chi = 0.0;  // this tile's chi^2 (summed per wave into red[1] at the tile's end)
         const int m = min(LIKE_TILE, n - t0);
@@ -1810,119 +2001,119 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
         const double wk = own ? pw : 0.0;
         const double ph0 = own ? px - SG[G_PHI0] : 0.0;
         const double phc = wrap_phase(ph0);
-        const double h = wk / S;
         double fw = 0.0, fd = 0.0, sbs = 0.0, srs = 0.0;
-        // pass j = 0 also carries the WD and disc; passes j > 0 the spot and donor only
-        for (int j = 0; j < S; ++j) {
-            const double ph = wrap_phase(ph0 - wk + (2 * j + 1) * h);
-            if (tid == 0) { sflag[0] = 0; sflag[1] = 0; }
-            // S = 1: the sub-bin window is the point's own window (ph = phc,
-            // h = wk), so the spot sweep reuses TA's windows and cells
-            const bool one = S == 1;
-            int flA = (j == 0) ? put_window(TA, tid, own, phc, wk) : 0;
-            int flB = one ? 0 : put_window(TB, tid, own, ph, h);
-            if (own) sph[tid] = ph;
-            for (int i = (j == 0) ? 0 : 2; i < 6; ++i) sacc[i][tid] = 0ull;
-            if (one) {
-                TBU.X[0][tid] = 0ull;
-                TBU.X[1][tid] = 0ull;
-            }
-            if (tid == 0)
-                for (int i = (j == 0) ? 0 : 2; i < 6; ++i) sacc[i][nt] = 0ull;
-            __syncthreads();
-            if (j == 0) {
-                flA |= check_sorted(TA, tid, own);
-                if (flA) atomicOr(&sflag[0], flA);
-                build_cells(TA.lo, m, TA.cell, tid);
-            }
-            flB |= (one ? flA : check_sorted(TB, tid, own)) | ((own && tid && sph[tid] < sph[tid - 1]) ? 4 : 0);
+        // the pass over the points' own windows: the WD and disc (and, S = 1,
+        // the spot on the same windows and the donor at the point phases)
+        if (tid == 0) { sflag[0] = 0; sflag[1] = 0; }
+        int flA = put_window(TA, tid, own, phc, wk);
+        if (!TAB && own) sph[tid] = phc;
+        for (int i = 0; i < (TAB ? 2 : 6); ++i) sacc[i][tid] = 0ull;
+        if (!TAB) {
+            SU.s1.X[0][tid] = 0ull;
+            SU.s1.X[1][tid] = 0ull;
+        }
+        if (tid == 0)
+            for (int i = 0; i < (TAB ? 2 : 6); ++i) sacc[i][nt] = 0ull;
+        // does this point's window reach the WD/disc hull?  (any does: the tile sweeps)
+        if (own && wk >= 0.0 && !(phc + wk < shull[0] || phc - wk > shull[1])) flA |= 8;
+        __syncthreads();
+        flA |= check_sorted(TA, tid, own);
+        if (flA) atomicOr(&sflag[0], flA);
+        build_cells(TA.lo, m, TA.cell, tid);
+        if (!TAB) {
+            const int flB = (flA & 7) | ((own && tid && sph[tid] < sph[tid - 1]) ? 4 : 0);
             if (flB) atomicOr(&sflag[1], flB);
-            if (!one) build_cells(TB.lo, m, TB.cell, tid);
             build_cells(sph, m, scp, tid);
-            __syncthreads();
-            // any unsorted / mixed window (or invalid width) of the tile: the
-            // whole pass goes point-major (every element against each point)
-            const bool dir = (j == 0 && sflag[0] != 0) || sflag[1] != 0;
-            LIKE_STAMP(1);
-            double eb = 0.0, R3 = 0.0, R4 = 0.0, R5 = 0.0;
-            if (dir) {
-                if (own) {
-                    if (j == 0) {
-                        const double ulg = SG[G_ULIMB];
-                        const double2 f2 = direct_wd_disc(AB, swr, phc, wk, TWO_PI * ((1.0 - ulg) * 0.5 + ulg / 3.0),
-                                                          FUSED ? swt[WT_TD] : Wt[WT_TD]);
-                        fw = f2.x;
-                        fd = f2.y;
-                    }
-                    eb = direct_spot(sab, sbw, ph, h, snorm[0]);
-                }
-                __syncthreads();  // every wave has read sflag before the next pass resets it
-            } else {
-                if (j == 0) {
-                    const PhaseIndex X = phase_index(TA.lo, TA.cell, m);
-                    double qx[2 * NI];
-                    int J[2 * NI], Jb[2 * NI];
+        }
+        __syncthreads();
+        // any unsorted / mixed window (or invalid width) of the tile: the
+        // pass goes point-major (every element against each point)
+        const bool dir = (sflag[0] & 7) != 0 || (!TAB && sflag[1] != 0);
+        const bool wdd = (sflag[0] & 8) != 0;  // the WD/disc elements touch the tile
+        LIKE_STAMP(1);
+        double eb = 0.0, R3 = 0.0, R4 = 0.0, R5 = 0.0;
+        if (dir) {
+            if (own) {
+                const double ulg = SG[G_ULIMB];
+                const double2 f2 = direct_wd_disc(AB, swr, phc, wk, TWO_PI * ((1.0 - ulg) * 0.5 + ulg / 3.0), Wt[WT_TD]);
+                fw = f2.x;
+                fd = f2.y;
+                if (!TAB) eb = direct_spot(sab, sbw, phc, wk, snorm[0]);
+            }
+            __syncthreads();  // every wave has read sflag before the next tile resets it
+        } else {
+            if (wdd) {
+                if constexpr (TAB) {
+                    // re-read per tile (L2): held over the tiles they would not
+                    // leave the sub-bin queries their registers
 #pragma unroll
                     for (int i = 0; i < NI; ++i) {
-                        qx[2 * i] = abk[i].x;
-                        qx[2 * i + 1] = abk[i].y;
+                        const int g = tid + i * nt;
+                        abk[i] = (g < NWD + NDISC) ? sweep_ab(AB, g) : make_double2(1.0, -1.0);
                     }
-                    count_lt_multi<2 * NI>(X, qx, J);
-                    count_le_back_multi<2 * NI>(TA.hi, qx, J, Jb);
+                }
+                const PhaseIndex X = phase_index(TA.lo, TA.cell, m);
+                double qx[2 * NI];
+                int J[2 * NI], Jb[2 * NI];
 #pragma unroll
-                    for (int i = 0; i < NI; ++i)
-                        if (abk[i].x < abk[i].y) {
-                            const int g = tid + i * nt;
-                            const int u = uitem(g < NU_WDD ? g : g - NU_WDD);
-                            apply_runs(Runs{Jb[2 * i], J[2 * i], Jb[2 * i + 1], J[2 * i + 1]}, abk[i].x, abk[i].y,
-                                       swn[uring(u)], X, TA.hi, TA.iw,
-                                       ((one && (lane & 1)) ? TBU.X : sacc)[(u < U_WD) ? 0 : 1]);
-                        }
+                for (int i = 0; i < NI; ++i) {
+                    qx[2 * i] = abk[i].x;
+                    qx[2 * i + 1] = abk[i].y;
                 }
-                LIKE_STAMP(2);
-                {
-                    const PhaseIndex XP = phase_index(sph, scp, m);
-                    if (one)
-                        sweep_spot_donor(tid, phase_index(TA.lo, TA.cell, m), TA, XP, sab, sbw, snorm[0], sdq,
-                                         snorm[1], sacc + 2);
-                    else
-                        sweep_spot_donor(tid, phase_index(TB.lo, TB.cell, m), TB, XP, sab, sbw, snorm[0], sdq,
-                                         snorm[1], sacc + 2);
-                }
-                __syncthreads();
-                LIKE_STAMP(3);
-                long long r[6] = {0, 0, 0, 0, 0, 0};
-                if (j == 0) block_scan<6>(sacc, spart, tid, r, one ? TBU.X : nullptr);
-                else block_scan<4>(sacc + 2, spart + 2, tid, r + 2);  // sub-bin passes: spot and donor only
-                LIKE_STAMP(4);
-                if (j == 0) {
-                    fw = double(r[0]) * FX_INV;
-                    fd = double(r[1]) * FX_INV;
-                }
-                eb = double(r[2]) * FX_INV;
-                R3 = double(r[3]);
-                R4 = double(r[4]);
-                R5 = double(r[5]);
+                count_lt_multi<2 * NI>(X, qx, J);
+                count_le_back_multi<2 * NI>(TA.hi, qx, J, Jb);
+#pragma unroll
+                for (int i = 0; i < NI; ++i)
+                    if (abk[i].x < abk[i].y) {
+                        const int g = tid + i * nt;
+                        const int u = uitem(g < NU_WDD ? g : g - NU_WDD);
+                        apply_runs(Runs{Jb[2 * i], J[2 * i], Jb[2 * i + 1], J[2 * i + 1]}, abk[i].x, abk[i].y,
+                                   swn[uring(u)], X, TA.hi, TA.iw,
+                                   ((!TAB && (lane & 1)) ? SU.s1.X : sacc)[(u < U_WD) ? 0 : 1]);
+                    }
             }
-            const double2 scp2 = sincospi_ool(2.0 * ph);  // |2 ph| <= 1: cheap exact reduction
-            const double sn = scp2.x, cs = scp2.y;
-            const double sg = SG[G_S], cg = SG[G_C];
-            const double e0 = sg * cs, e1 = -sg * sn;
+            LIKE_STAMP(2);
+            if (!TAB)
+                sweep_spot_donor(tid, phase_index(TA.lo, TA.cell, m), TA, phase_index(sph, scp, m), sab, sbw,
+                                 snorm[0], sdq, snorm[1], sacc + 2);
+            __syncthreads();
+            LIKE_STAMP(3);
+            long long r[6] = {0, 0, 0, 0, 0, 0};
+            if (!TAB) block_scan<6>(sacc, spart, tid, r, SU.s1.X);
+            else if (wdd) block_scan<2>(sacc, spart, tid, r);
+            LIKE_STAMP(4);
+            fw = double(r[0]) * FX_INV;
+            fd = double(r[1]) * FX_INV;
+            eb = double(r[2]) * FX_INV;
+            R3 = double(r[3]);
+            R4 = double(r[4]);
+            R5 = double(r[5]);
+        }
+        const double sg = SG[G_S], cg = SG[G_C];
+        const double bden = SG[G_BDEN], fis = SG[G_FIS];
+        if (!TAB) {
+            const double2 scp2 = sincospi_ool(2.0 * phc);  // |2 ph| <= 1: cheap exact reduction
+            const double e0 = sg * scp2.y, e1 = -sg * scp2.x;
             double D = 0.0;
             if (!dir) D = (e0 * R3 + e1 * R4 + cg * R5) * (FX_INV * snorm[3]);
             else if (own) D = direct_donor(sdq, e0, e1, cg);
             double beam = 0.0;
-            const double bden = SG[G_BDEN], fis = SG[G_FIS];
             if (bden > 0.0)
                 beam = (fis + (1.0 - fis) * fmax(SG[G_NB0] * e0 + SG[G_NB1] * e1 + SG[G_NB2] * cg, 0.0)) / bden;
-            sbs += beam * (1.0 - eb);
-            srs += D / snorm[2];
-            // no barrier before the next pass rewrites the tile buffers: every
-            // read of TA/TB/sph/scp/sacc/sflag of this pass precedes the
-            // block scan's barriers (after them only registers, part[] and
-            // the pass-invariant LDS are read, none of which the next
-            // pass's prologue writes)
+            sbs = beam * (1.0 - eb);
+            srs = D / snorm[2];
+        } else if (own) {
+            const double2 r2 = sub_point(SU.tb, DE, sab, sbw, sdq, snorm, shull, SG, ph0, wk, S);
+            sbs = r2.x;
+            srs = r2.y;
         }
+        // no barrier before the next tile rewrites the tile buffers: every
+        // read of TA / sph / scp / sacc / sflag of this tile precedes the
+        // block scan's barriers or the direct path's barrier (after them only
+        // registers, part[], the tables and the pass-invariant LDS are read,
+        // none of which the next tile's prologue writes); a table tile that
+        // skipped the scan waits here instead
+        if (TAB && !dir && !wdd) __syncthreads();
         if (own) {
             const double fwv = SG[G_WDF] * (1.0 - fw), fdv = SG[G_DF] * (1.0 - fd);
             const double fb = SG[G_SF] * sbs / S, fr = SG[G_RSF] * srs / S;
@@ -2401,19 +2592,8 @@ inline int launch_ok() { return hipGetLastError() == hipSuccess ? LFG_OK : LFG_E
 // k_setup (setup, prior and stream lanes) then k_elements, on the caller's
 // stream.  ev (nullable, LFG_NEV events): 0 before k_setup, 1 after k_setup,
 // 2 after k_elements
-// k_elements then k_lnlike<MODE, false>.  A build with LFG_FUSED solves the
-// elements inside k_lnlike instead (k_lnlike<MODE, true>): measured at
-// config 2 it is slower, 64.5 us vs 33.7 + 28.3 us (its element phase runs
-// at 4 waves/SIMD with a 1.76-round item imbalance per block, where
-// k_elements' independent one-wave blocks keep 5 waves/SIMD busy;
-// profiles/r02/bench_c2_fused_by_grid.txt), so it stays an option
-#ifdef LFG_FUSED
-constexpr bool kFused = true;
-#else
-constexpr bool kFused = false;
-#endif
-
-int run_front(const SetupArgs& S, const Ws& ws, hipStream_t st, void* const* ev, bool elements = !kFused,
+// k_setup (unless the speculative candidates stand in for it) then k_elements
+int run_front(const SetupArgs& S, const Ws& ws, hipStream_t st, void* const* ev, bool elements = true,
               const ElemSpec* X = nullptr, bool setup = true)
 {
     auto mark = [&](int i) {
@@ -2471,7 +2651,8 @@ int lfg_flux(const double* pars, int W, int P, const double* x, const double* w,
                    nsub, flux, comps, nullptr, W, nullptr, nullptr, nullptr, false, nullptr,
                    nullptr, nullptr, nullptr, 0, 0, 0ull, 0ull, nullptr};
         L.bstatus = ws.bstatus;
-        hipLaunchKernelGGL((k_lnlike<0, kFused>), dim3(W), dim3(LIKE_THREADS), 0, st, L);
+        if (nsub > 1) hipLaunchKernelGGL((k_lnlike<0, true>), dim3(W), dim3(LIKE_THREADS), 0, st, L);
+        else hipLaunchKernelGGL((k_lnlike<0, false>), dim3(W), dim3(LIKE_THREADS), 0, st, L);
         if ((rc = launch_ok())) return rc;
     }
     if (status && hipMemcpyAsync(status, ws.status, sizeof(int) * W, hipMemcpyDeviceToDevice, st) != hipSuccess)
@@ -2574,7 +2755,7 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
             X.nspecblk = (2 * ((X.nspec + ELEM_BLOCK - 1) / ELEM_BLOCK) + 7) / 8 * 8;  // keeps the pair -> XCD map
         }
     }
-    int rc = run_front(S, ws, st, ev, !kFused, &X, !(sp && sp->in));
+    int rc = run_front(S, ws, st, ev, true, &X, !(sp && sp->in));
     if (rc) return rc;
     double* lle = lnlike_e ? lnlike_e : ws.lle;
     LikeArgs L{ws.geo, ws.status, ws.ab, ws.donor, ws.wts, T->E, T->off, T->max_n, T->x, T->y, T->ye,
@@ -2592,11 +2773,13 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
         hipLaunchKernelGGL(k_gp_dcp, dim3((npairs + 64 / DCP_LANES - 1) / (64 / DCP_LANES)), dim3(64), 0, st, ws.geo,
                            ws.status, npairs);
         if ((rc = launch_ok())) return rc;
-        hipLaunchKernelGGL((k_lnlike<2, kFused>), dim3(npairs), dim3(LIKE_THREADS), 0, st, L);
+        if (T->nsub > 1) hipLaunchKernelGGL((k_lnlike<2, true>), dim3(npairs), dim3(LIKE_THREADS), 0, st, L);
+        else hipLaunchKernelGGL((k_lnlike<2, false>), dim3(npairs), dim3(LIKE_THREADS), 0, st, L);
         if ((rc = launch_ok())) return rc;
         hipLaunchKernelGGL(k_gp_like, dim3((npairs + GP_LANES - 1) / GP_LANES), dim3(GP_BLOCK), 0, st, L);
     } else {
-        hipLaunchKernelGGL((k_lnlike<1, kFused>), dim3(npairs), dim3(LIKE_THREADS), 0, st, L);
+        if (T->nsub > 1) hipLaunchKernelGGL((k_lnlike<1, true>), dim3(npairs), dim3(LIKE_THREADS), 0, st, L);
+        else hipLaunchKernelGGL((k_lnlike<1, false>), dim3(npairs), dim3(LIKE_THREADS), 0, st, L);
     }
     if ((rc = launch_ok())) return rc;
     if (T->E > 1) {
@@ -2662,7 +2845,7 @@ int lfg_stretch_step_half_spec(double* pos, double* lnp, int W, int half, double
     const Propose prop{pos, a, q, zfac, half, seed, step, 0, W / 2};
     const SpecCtl sp{spec_in != 0, spec_out != 0};
     // the fused-element build has no k_elements to host the candidates: plain half-step
-    return lnprob_impl(q, W / 2, T, lnp_new, nullptr, wsp, ws_bytes, stream, ev, &acc, &prop, kFused ? nullptr : &sp);
+    return lnprob_impl(q, W / 2, T, lnp_new, nullptr, wsp, ws_bytes, stream, ev, &acc, &prop, &sp);
 }
 
 int lfg_stretch_step_shard(const double* pos, int W, int half, double a, unsigned long long seed,
@@ -2686,7 +2869,7 @@ int lfg_stretch_step_shard_spec(const double* pos, int W, int half, double a, un
         return LFG_E_ARGS;
     const Propose prop{pos, a, q, zfac, half, seed, step, lo, W / 2};
     const SpecCtl sp{spec_in != 0, spec_out != 0};
-    return lnprob_impl(q, n, T, lnp_new, nullptr, wsp, ws_bytes, stream, ev, nullptr, &prop, kFused ? nullptr : &sp);
+    return lnprob_impl(q, n, T, lnp_new, nullptr, wsp, ws_bytes, stream, ev, nullptr, &prop, &sp);
 }
 
 int lfg_stretch_lnprob_accept(double* pos, double* lnp, int W, int half, const double* q, const double* zfac,
@@ -2881,7 +3064,7 @@ int lfg_debug_setup_cycles(unsigned long long* host)
 }
 #endif
 
-const char* lfg_version(void) { return kFused ? "lfg 0.2.0 gfx950 fp64 fused-elements" : "lfg 0.2.0 gfx950 fp64"; }
+const char* lfg_version(void) { return "lfg 0.3.0 gfx950 fp64"; }
 
 #ifdef LFG_COUNT_ITERS
 // diagnostic builds only: read and clear the iteration counters of k_elements
