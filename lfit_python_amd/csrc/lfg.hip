@@ -17,6 +17,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "lfg.h"
 #include "lfg_device.hpp"
 #include "lfg_tables.hpp"
@@ -1245,6 +1247,16 @@ __device__ __forceinline__ double wrap_phase(double ph) { return ph - floor(ph +
 
 // sincospi out of line: inlined into the tile loop, its polynomial constants
 // are hoisted into ~20 loop-invariant VGPRs
+// sin, cos of pi x and of pi y in one call (the sub-bin queries: the line of
+// sight at the first sub-bin and its turn per sub-bin)
+__device__ __noinline__ double4 sincospi2_ool(double x, double y)
+{
+    double sx, cx, sy, cy;
+    sincospi(x, &sx, &cx);
+    sincospi(y, &sy, &cy);
+    return make_double4(sx, cx, sy, cy);
+}
+
 __device__ __noinline__ double2 sincospi_ool(double x)
 {
     double sn, cs;
@@ -1428,17 +1440,36 @@ __device__ __forceinline__ void donor_q(const double* sdq, int t, double ivs, lo
     qz = to_fx(((mr & 2) ? -dq[2] : dq[2]) * ivs);
 }
 
-// wave-wide min / max (shuffles; once per pair)
-__device__ __forceinline__ double wave_min(double v)
+// wave-wide min / max, every lane: DPP row shifts as wave_sum does, with each
+// lane's own value standing in where the source lane is absent (the
+// min / max identity), then lane 63's result
+template <bool MAX>
+__device__ __forceinline__ double wave_ext(double v)
 {
-    for (int off = 32; off > 0; off >>= 1) v = fmin(v, __shfl_xor(v, off, 64));
-    return v;
+    auto step = [&](auto ctrl_tag, auto rm_tag) {
+        constexpr int CTRL = decltype(ctrl_tag)::value, RM = decltype(rm_tag)::value;
+        const long long b = __double_as_longlong(v);
+        const int lo = __builtin_amdgcn_update_dpp(static_cast<int>(b), static_cast<int>(b), CTRL, RM, 0xf, false);
+        const int hi = __builtin_amdgcn_update_dpp(static_cast<int>(b >> 32), static_cast<int>(b >> 32), CTRL, RM, 0xf,
+                                                   false);
+        const double o = __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
+        v = MAX ? fmax(v, o) : fmin(v, o);
+    };
+    using I = std::integral_constant<int, 0>;
+    (void)sizeof(I);
+    step(std::integral_constant<int, 0x111>{}, std::integral_constant<int, 0xf>{});
+    step(std::integral_constant<int, 0x112>{}, std::integral_constant<int, 0xf>{});
+    step(std::integral_constant<int, 0x114>{}, std::integral_constant<int, 0xf>{});
+    step(std::integral_constant<int, 0x118>{}, std::integral_constant<int, 0xf>{});
+    step(std::integral_constant<int, 0x142>{}, std::integral_constant<int, 0xa>{});
+    step(std::integral_constant<int, 0x143>{}, std::integral_constant<int, 0xc>{});
+    const long long t = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane(static_cast<int>(t), 63);
+    const int hi = __builtin_amdgcn_readlane(static_cast<int>(t >> 32), 63);
+    return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
 }
-__device__ __forceinline__ double wave_max(double v)
-{
-    for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
-    return v;
-}
+__device__ __forceinline__ double wave_min(double v) { return wave_ext<false>(v); }
+__device__ __forceinline__ double wave_max(double v) { return wave_ext<true>(v); }
 
 // exclusive prefix over TCELLS cells of NA int64 arrays held one cell per
 // thread (threads >= TCELLS pass zeros); totals of each wave through part[]
@@ -1559,29 +1590,70 @@ __device__ __forceinline__ void lane_breakpoints(int tid, const double* sdq, con
 }
 
 
+// donor entries with (start: th0 <= pos < th1, end: th0 < pos <= th1): what
+// V gains from th0 to th1 > th0 (cells g(th0) .. g(th1))
+__device__ __forceinline__ void sub_donor_step(const SubTables& T, const SubEntries& D, const double* sdq, double ivs,
+                                               double th0, double th1, long long& vx, long long& vy, long long& vz)
+{
+    const int g0 = tcell(th0, T.dt0, T.dginv), g1 = tcell(th1, T.dt0, T.dginv);
+    for (int i = g0 ? T.dend[g0 - 1] : 0; i < T.dend[g1]; ++i) {
+        const double pos = D.dpos[i];
+        const int code = D.dcode[i];
+        const bool end = code & 1;
+        if (end ? (pos > th0 && pos <= th1) : (pos >= th0 && pos < th1)) {
+            long long qx, qy, qz;
+            donor_q(sdq, code >> 1, ivs, qx, qy, qz);
+            if (end) { vx -= qx; vy -= qy; vz -= qz; }
+            else { vx += qx; vy += qy; vz += qz; }
+        }
+    }
+}
+
 // S > 1: the spot and donor terms of one point, summed over its S sub-bins
 // (spot eclipse over each sub-bin window, donor at each sub-bin centre, from
-// the tables).
+// the tables).  The donor vector is looked up at the first sub-bin and
+// carried forward over the breakpoints between sub-bins (usually none), and
+// the line of sight is rotated from sub-bin to sub-bin (one sincospi per
+// point); a sub-bin past +-1/2 starts over.
 __device__ __forceinline__ double2 sub_point(const SubTables& T, const SubEntries& D, const double2* sab, const double* sbw,
-                                          const double* sdq, const double* snorm, const double* shull, const double* SG,
-                                          double ph0, double wk, int S)
+                                             const double* sdq, const double* snorm, const double* shull, const double* SG,
+                                             double ph0, double wk, int S)
 {
-    const double sg = SG[G_S], cg = SG[G_C], bden = SG[G_BDEN], fis = SG[G_FIS];
+    // the pair's constants are read from LDS at each use (volatile: held in
+    // registers over the loop they pushed k_lnlike past its budget)
+    const volatile double* VG = SG;
+    const volatile double* VN = snorm;
     const double h = wk / S;
-    double sbs = 0.0, srs = 0.0;
+    double sbs = 0.0, srs = 0.0, ph = 0.0, sn = 0.0, cs = 1.0, rs = 0.0, rc = 1.0;
+    long long vx = 0, vy = 0, vz = 0;
     for (int j = 0; j < S; ++j) {
-        const double ph = wrap_phase(ph0 - wk + (2 * j + 1) * h);
-        const double ebj = sub_spot(T, sab, sbw, snorm[0], ph - h, ph + h, shull[2], shull[3]);
-        long long vx, vy, vz;
-        sub_donor(T, D, sdq, snorm[1], ph, vx, vy, vz);
-        const double2 scp2 = sincospi_ool(2.0 * ph);
-        const double e0 = sg * scp2.y, e1 = -sg * scp2.x;
-        const double Dv = (e0 * double(vx) + e1 * double(vy) + cg * double(vz)) * (FX_INV * snorm[3]);
+        const double phn = wrap_phase(ph0 - wk + (2 * j + 1) * h);
+        if (j == 0 || !(phn >= ph)) {  // a fresh lookup
+            sub_donor(T, D, sdq, VN[1], phn, vx, vy, vz);
+            const double4 e4 = sincospi2_ool(2.0 * phn, 4.0 * h);  // the turn per sub-bin: 2 pi (2 h)
+            sn = e4.x;
+            cs = e4.y;
+            rs = e4.z;
+            rc = e4.w;
+        } else {
+            if (phn > ph) sub_donor_step(T, D, sdq, VN[1], ph, phn, vx, vy, vz);
+            const double c2 = fma(cs, rc, -sn * rs);
+            sn = fma(sn, rc, cs * rs);
+            cs = c2;
+        }
+        ph = phn;
+        const double ebj = sub_spot(T, sab, sbw, VN[0], ph - h, ph + h, shull[2], shull[3]);
+        const double sg = VG[G_S], cg = VG[G_C];
+        const double e0 = sg * cs, e1 = -sg * sn;
+        const double Dv = (e0 * double(vx) + e1 * double(vy) + cg * double(vz)) * (FX_INV * VN[3]);
         double beam = 0.0;
-        if (bden > 0.0)
-            beam = (fis + (1.0 - fis) * fmax(SG[G_NB0] * e0 + SG[G_NB1] * e1 + SG[G_NB2] * cg, 0.0)) / bden;
+        const double bden = VG[G_BDEN];
+        if (bden > 0.0) {
+            const double fis = VG[G_FIS];
+            beam = (fis + (1.0 - fis) * fmax(VG[G_NB0] * e0 + VG[G_NB1] * e1 + VG[G_NB2] * cg, 0.0)) / bden;
+        }
         sbs += beam * (1.0 - ebj);
-        srs += Dv / snorm[2];
+        srs += Dv / VN[2];
     }
     return make_double2(sbs, srs);
 }
@@ -1827,7 +1899,10 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
         else if (tid >= nt - NDONOR && ((tid - (nt - NDONOR)) & 3) == 0)
             for (int i = 0; i < DON_STRIDE; ++i) sdq[((tid - (nt - NDONOR)) >> 2) * DON_STRIDE + i] = dq[i];
     }
-    {   // hulls of the eclipsed WD/disc and spot intervals (tiles outside skip them)
+    // hulls of the eclipsed WD/disc and spot intervals (tiles outside skip
+    // them): only when there is more than one tile or sub-bin tables
+    const bool hull = SUB || n > LIKE_TILE;
+    if (hull) {
         double wa = INFINITY, wb = -INFINITY, sa = INFINITY, sb = -INFINITY;
 #pragma unroll
         for (int i = 0; i < NI; ++i)
@@ -1858,7 +1933,7 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
             snorm[2] = p1;
             snorm[3] = p2;
         }
-        if (lane < 4) {
+        if (hull && lane < 4) {
             double h = (lane & 1) ? -INFINITY : INFINITY;
             for (int k = 0; k < nw; ++k) h = (lane & 1) ? fmax(h, shw[lane][k]) : fmin(h, shw[lane][k]);
             shull[lane] = h;
@@ -2015,7 +2090,7 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
         if (tid == 0)
             for (int i = 0; i < (TAB ? 2 : 6); ++i) sacc[i][nt] = 0ull;
         // does this point's window reach the WD/disc hull?  (any does: the tile sweeps)
-        if (own && wk >= 0.0 && !(phc + wk < shull[0] || phc - wk > shull[1])) flA |= 8;
+        if (own && (!hull || (wk >= 0.0 && !(phc + wk < shull[0] || phc - wk > shull[1])))) flA |= 8;
         __syncthreads();
         flA |= check_sorted(TA, tid, own);
         if (flA) atomicOr(&sflag[0], flA);
