@@ -1,0 +1,64 @@
+"""The GPU path's algorithm on CPU cores (cpu_baseline/lfg_cpu.cpp): a fair
+CPU baseline for bench.py, beside the oracle.  Not a product path: nothing
+in lfit_python_amd loads it.
+
+    build(out=None, march="native") -> path of liblfg_cpu.so
+    CpuPort(path).lnprob_batch(walkers, tree, nthreads=0) -> (lnp, threads)
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+LIB_PATH = os.path.join(HERE, "liblfg_cpu.so")
+_dp = ctypes.POINTER(ctypes.c_double)
+_ip = ctypes.POINTER(ctypes.c_int)
+
+
+def build(out=None, march="x86-64-v3"):
+    out = out or LIB_PATH
+    cmd = ["g++", "-O3", "-march=%s" % march, "-fopenmp", "-std=c++17", "-fPIC", "-shared",
+           "-I", os.path.join(HERE, "shim"), "-I", os.path.join(ROOT, "lfit_python_amd", "csrc"),
+           "-I", os.path.join(ROOT, "include"), "-o", out, os.path.join(HERE, "lfg_cpu.cpp")]
+    subprocess.run(cmd, check=True)
+    return out
+
+
+class CpuPort:
+    def __init__(self, path=None):
+        self.lib = ctypes.CDLL(path or LIB_PATH)
+        f = self.lib.lfc_lnprob_batch
+        f.restype = ctypes.c_int
+        f.argtypes = [_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _ip, _ip, _dp, _ip, _dp, _dp, _dp, _dp,
+                      ctypes.c_int, _ip, _dp, _dp, _dp, ctypes.c_int, _dp, ctypes.c_int]
+
+    def lnprob_batch(self, walkers, tree, nthreads=0):
+        """ln_prob of walkers [W, ndim] of a compiled chi^2 tree
+        (lfit_python_amd.batch.CompiledTree)."""
+        if getattr(tree, "gp", False):
+            raise ValueError("the CPU port runs chi^2 trees only")
+        keep = []
+
+        def F(a):
+            a = np.ascontiguousarray(a, dtype=np.float64)
+            keep.append(a)
+            return a.ctypes.data_as(_dp)
+
+        def I(a):
+            a = np.ascontiguousarray(a, dtype=np.int32)
+            keep.append(a)
+            return a.ctypes.data_as(_ip)
+        w = np.ascontiguousarray(walkers, dtype=np.float64)
+        W, ndim = w.shape
+        lnp = np.empty(W)
+        used = self.lib.lfc_lnprob_batch(
+            F(w), W, ndim, tree.E, I(tree.gather.reshape(-1)), I(tree.npars),
+            F(tree.consts if len(tree.consts) else np.zeros(1)), I(tree.offsets), F(tree.x), F(tree.y), F(tree.ye),
+            F(tree.w), int(tree.nsub), I(tree.prior_type), F(tree.prior_p1), F(tree.prior_p2), F(tree.prior_norm),
+            int(tree.roche_priors), lnp.ctypes.data_as(_dp), int(nthreads))
+        if getattr(tree, "fixed_invalid", False):
+            lnp[:] = -np.inf
+        return lnp, used

@@ -1,0 +1,426 @@
+// lfg_cpu.cpp -- the MI355X path's algorithm run on the host: a CPU baseline
+// for bench.py (kind "port-fast"), not a product path and not the oracle.
+//
+// The oracle (oracle/lfg_oracle.c) restates MODEL_SPEC with the nested
+// eclipse solver and the direct element x point sum: the slow, independent
+// form.  This file runs what the GPU runs, on CPU cores: the device functions
+// of lfit_python_amd/csrc/lfg_device.hpp compiled for the host (stream table,
+// L1 and findi solves, the envelope-Newton tangency solver with its nested
+// fallback, mirror symmetry), then the interval sweep of k_lnlike over the
+// sorted exposure windows (each element's covered run into a difference
+// array, partial windows directly, O((N S + N_el) log N) per walker), one
+// walker per OpenMP thread at a time.  Chi^2 trees only (the GP likelihood
+// is left to the oracle).  Sums are in FP64 in a fixed order; results match
+// the oracle and the GPU to ~1e-12 (tests/test_cpu_baseline.py).
+#include <omp.h>
+#include <stdint.h>
+#include <stdlib.h>
+
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "lfg_device.hpp"
+#include "lfg_tables.hpp"
+
+using namespace lfg;
+
+namespace {
+
+constexpr int U_WD = NWD / 2, U_DISC = NDISC / 2, U_DON = NDONOR / 4;
+
+// the pair's geometry (k_setup's record)
+struct Pair {
+    Roche R;
+    double s, c, rwd_a, rdisc_a, reff, rcal, ulimb, dexp, L, upk, umax, lnpk, exp1, exp2;
+    double bsx, bsy, caz, saz, nb0, nb1, nb2, bden, fis, phi0, wdf, df, sf, rsf;
+};
+
+int wd_ring_of(int u)
+{
+    int ir = int(std::sqrt(u * 0.5));
+    if (2 * (ir + 1) * (ir + 1) <= u) ++ir;
+    if (2 * ir * ir > u) --ir;
+    return ir;
+}
+
+double disc_boundary(int i, const Pair& G)
+{
+    const double r = G.rwd_a + i * ((G.rdisc_a - G.rwd_a) / NDISC_R);
+    const double ex = 2.0 - G.dexp;
+    return (std::fabs(ex) < 1e-10) ? std::log(r) : std::pow(r, ex) / ex;
+}
+
+// k_setup's setup lane and stream lane for one (walker, eclipse): status and
+// the eclipse's Roche prior (CVModel.py:193-324), MODEL_SPEC 6 order
+int setup_pair(const double* pin, int np, Pair& G, double& rprior)
+{
+    double p[18];
+    bool finite = (np == 14 || np == 18);
+    for (int k = 0; k < 18; ++k) {
+        p[k] = k < np ? pin[k] : 0.0;
+        finite = finite && std::isfinite(p[k]);
+    }
+    if (np == 14) { p[14] = 2.0; p[15] = 1.0; p[16] = 90.0; p[17] = 0.0; }
+    rprior = 0.0;
+    if (!finite) { rprior = -INFINITY; return ST_BAD_ARGS; }
+    QPatch qp;
+    int st = roche_init(G.R, p[4], &qp);
+    if (st != ST_OK) { rprior = -INFINITY; return st; }
+    const Roche& R = G.R;
+    if (p[6] * R.xl1 > DISC_MAX_A) rprior = -INFINITY;
+    if (p[9] > p[8] * 3.0 || p[9] < p[8] / 3.0) rprior = -INFINITY;
+    double inc = 0.0;
+    st = findi_fast(R, p[5], inc);
+    G.rwd_a = p[8] * R.xl1;
+    G.rdisc_a = p[6] * R.xl1;
+    if (st == ST_OK && (!(G.rwd_a > 0.0) || !(G.rdisc_a > G.rwd_a) || !(G.rdisc_a < R.xl1))) st = ST_BAD_GEOMETRY;
+    if (st == ST_OK && (!(p[9] > 0.0) || !(p[14] > 0.0) || !(p[15] > 0.0))) st = ST_BAD_GEOMETRY;
+    // stream lane: impact point, azimuth prior, strip profile
+    double bs[4] = {0.0, 0.0, 0.0, 0.0};
+    int bst = (std::isfinite(p[6]) && std::isfinite(p[10])) ? bspot<false>(R, G.rdisc_a, bs, &qp) : ST_BAD_ARGS;
+    if (bst != ST_OK) {
+        rprior = -INFINITY;
+    } else {
+        double alpha = std::atan2(bs[1], bs[0]) / DEG;
+        if (alpha < 0.0) alpha = 90.0 - alpha;
+        const double tangent = alpha + 90.0;
+        if (p[10] < std::fmax(0.0, tangent - AZ_SLOPE) || p[10] > std::fmin(178.0, tangent + AZ_SLOPE)) rprior = -INFINITY;
+    }
+    if (st != ST_OK) return st;
+    if (bst != ST_OK) return bst;
+    const double a1 = p[14], a2 = p[15];
+    G.upk = std::pow(a1 / a2, 1.0 / a2);
+    G.lnpk = a1 * std::log(G.upk) - std::pow(G.upk, a2);
+    G.umax = bs_umax(a1, a2, G.lnpk);
+    if (!(std::isfinite(G.upk) && std::isfinite(G.lnpk) && std::isfinite(G.umax))) return ST_BAD_GEOMETRY;
+    G.exp1 = a1;
+    G.exp2 = a2;
+    G.bsx = bs[0];
+    G.bsy = bs[1];
+    G.s = std::sin(inc * DEG);
+    G.c = std::cos(inc * DEG);
+    const double tilt = p[16] * DEG, psi = (p[10] - 90.0 + p[17]) * DEG;
+    const double st_ = std::sin(tilt), ct_ = std::cos(tilt);
+    G.nb0 = st_ * std::cos(psi);
+    G.nb1 = st_ * std::sin(psi);
+    G.nb2 = ct_;
+    G.caz = std::cos(p[10] * DEG);
+    G.saz = std::sin(p[10] * DEG);
+    G.bden = p[11] + (1.0 - p[11]) * std::fmax(std::fabs(st_) * G.s + ct_ * G.c, 0.0);
+    G.fis = p[11];
+    G.phi0 = p[13];
+    G.ulimb = p[7];
+    G.dexp = p[12];
+    G.L = p[9] * R.xl1;
+    G.reff = eggleton(R.q);
+    const double sce = G.s * std::cos(PI * p[5]);
+    G.rcal = std::sqrt(1.0 - sce * sce);
+    G.wdf = p[0]; G.df = p[1]; G.sf = p[2]; G.rsf = p[3];
+    return ST_OK;
+}
+
+// the 1400 WD/disc intervals (each unique item and its mirror) with their
+// weights normalised by the component totals, the 100 spot intervals and
+// weights (normalised), and the 400 donor tile vectors with visibility arcs
+struct Tables {
+    double a[NWD + NDISC], b[NWD + NDISC], w[NWD + NDISC];
+    int wd[NWD + NDISC];  // 1: WD element, 0: disc
+    double sa[NBS], sb[NBS], sw[NBS];
+    double dv[NDONOR][3], dcen[NDONOR], dhw[NDONOR];
+    double dnorm;  // donor flux at quadrature
+};
+
+void elements(const Pair& G, Tables& T)
+{
+    const Roche& R = G.R;
+    const double s = G.s, c = G.c;
+    const double twd = TWO_PI * ((1.0 - G.ulimb) * 0.5 + G.ulimb / 3.0);
+    const double td = TWO_PI * (disc_boundary(NDISC_R, G) - disc_boundary(0, G));
+    int k = 0;
+    for (int u = 0; u < U_WD + U_DISC; ++u) {
+        double Px, Py, Pz, wgt;
+        bool isw = u < U_WD;
+        if (isw) {
+            const int ir = wd_ring_of(u);
+            const double rc = kWdRc[ir], mu0 = kWdMu0[ir], cp = kWdCos[u], sp = kWdSin[u];
+            Px = G.rwd_a * (-rc * sp * c + mu0 * s);
+            Py = G.rwd_a * (rc * cp);
+            Pz = G.rwd_a * (rc * sp * s + mu0 * c);
+            wgt = std::fma(kWdA[ir], 1.0 - G.ulimb, kWdB[ir] * G.ulimb) / twd;
+        } else {
+            const int uu = u - U_WD, ir = uu / (NDISC_AZ / 2), j = uu - ir * (NDISC_AZ / 2);
+            const double rc = G.rwd_a + (ir + 0.5) * ((G.rdisc_a - G.rwd_a) / NDISC_R);
+            Px = rc * kDiscCos[j];
+            Py = rc * kDiscSin[j];
+            Pz = 0.0;
+            wgt = (TWO_PI / NDISC_AZ) * (disc_boundary(ir + 1, G) - disc_boundary(ir, G)) / td;
+        }
+        double a, b;
+        element_interval_fast(R, Px, Py, Pz, s, c, G.rcal, G.reff, a, b);
+        T.a[k] = a; T.b[k] = b; T.w[k] = wgt; T.wd[k] = isw; ++k;
+        const bool ecl = a < b;  // the mirror image's interval (MODEL_SPEC 7)
+        T.a[k] = ecl ? -b : 1.0; T.b[k] = ecl ? -a : -1.0; T.w[k] = wgt; T.wd[k] = isw; ++k;
+    }
+    double tot = 0.0;
+    for (int j = 0; j < NBS; ++j) {
+        const double uk = (j + 0.5) * (G.umax / NBS);
+        T.sw[j] = std::exp(G.exp1 * std::log(uk) - std::pow(uk, G.exp2) - G.lnpk);
+        tot += T.sw[j];
+        const double off = G.L * (uk - G.upk);
+        element_interval_fast(R, std::fma(off, G.caz, G.bsx), std::fma(off, G.saz, G.bsy), 0.0, s, c, G.rcal, G.reff,
+                              T.sa[j], T.sb[j]);
+    }
+    for (int j = 0; j < NBS; ++j) T.sw[j] /= tot;
+    double dn = 0.0;
+    for (int uu = 0; uu < U_DON; ++uu) {
+        const int it = uu / (NDONOR_P / 4), ip = uu - it * (NDONOR_P / 4);
+        const double dx = -kDonCt[it], dy = kDonSt[it] * kDonCp[ip], dz = kDonSt[it] * kDonSp[ip];
+        double lo = 0.0, hi = R.Rs, r = G.reff, gx, gy, gz;
+        if (!(r > lo && r < hi)) r = 0.5 * hi;
+        for (int itr = 0; itr < ROOT_MAXIT; ++itr) {
+            const double f = rpot_grad(R, std::fma(r, dx, 1.0), r * dy, r * dz, gx, gy, gz) - R.pl1;
+            const double df = gx * dx + gy * dy + gz * dz;
+            if (f > 0.0) hi = r; else lo = r;
+            if (df > 0.0 && std::fabs(f / df) <= ROOT_LAST) { r -= f / df; break; }
+            double rn = (df > 0.0) ? r - f / df : 0.5 * (lo + hi);
+            if (!(rn > lo && rn < hi)) rn = 0.5 * (lo + hi);
+            r = rn;
+        }
+        rgrad(R, std::fma(r, dx, 1.0), r * dy, r * dz, gx, gy, gz);
+        const double ig = 1.0 / std::sqrt(gx * gx + gy * gy + gz * gz);
+        const double nx = gx * ig, ny = gy * ig, nz = gz * ig;
+        const double dA = r * r * kDonOmega[it] / (nx * dx + ny * dy + nz * dz);
+        const double vx = dA * nx, vy = dA * ny, vz = dA * nz;
+        const double srho = s * std::sqrt(vx * vx + vy * vy);
+        const double kap = (srho > 0.0) ? -c * vz / srho : (c * vz > 0.0 ? -2.0 : 2.0);
+        const double cen = -std::atan2(vy, vx) / TWO_PI, hw = std::acos(std::fmin(std::fmax(kap, -1.0), 1.0)) / TWO_PI;
+        for (int mr = 0; mr < 4; ++mr) {  // mirror images (vx, +-vy, +-vz)
+            const int t = 4 * uu + mr;
+            T.dv[t][0] = vx;
+            T.dv[t][1] = (mr & 1) ? -vy : vy;
+            T.dv[t][2] = (mr & 2) ? -vz : vz;
+            T.dcen[t] = (mr & 1) ? -cen : cen;
+            T.dhw[t] = (mr & 2) ? 0.5 - hw : hw;
+            dn += std::fmax(-s * T.dv[t][1] + c * T.dv[t][2], 0.0);
+        }
+    }
+    T.dnorm = dn;
+}
+
+double wrap_phase(double ph) { return ph - std::floor(ph + 0.5); }
+
+// sorted windows [lo, hi] (1 / width iw): add wn x covered fraction of
+// [a, b] to acc (difference array d for whole-covered runs, partial
+// windows directly); zero-width windows are points, a < ph < b
+void sweep_window(const double* lo, const double* hi, const double* iw, int m, double a, double b, double wn,
+                  double* d, double* direct)
+{
+    const int P2 = int(std::lower_bound(lo, lo + m, a) - lo);   // #{lo < a}
+    const int P4 = int(std::lower_bound(lo, lo + m, b) - lo);   // #{lo < b}
+    const int P1 = int(std::upper_bound(hi, hi + m, a) - hi);   // #{hi <= a}
+    const int P3 = int(std::upper_bound(hi, hi + m, b) - hi);   // #{hi <= b}
+    int e0 = P4, s1 = P4;
+    if (P2 < P3) {
+        d[P2] += wn;
+        d[P3] -= wn;
+        e0 = P2;
+        s1 = P3;
+    }
+    for (int r = 0; r < 2; ++r)
+        for (int p = r ? s1 : P1; p < (r ? P4 : e0); ++p) {
+            if (hi[p] > lo[p]) {
+                const double ov = std::fmin(b, hi[p]) - std::fmax(a, lo[p]);
+                if (ov > 0.0) direct[p] += wn * ov * iw[p];
+            } else if (a < lo[p] && lo[p] < b) {
+                direct[p] += wn;
+            }
+        }
+}
+
+// point mode: add v (3-vector) to the phases ph (sorted) strictly inside (x1, x2)
+void sweep_points(const double* ph, int m, double x1, double x2, const double* v, std::vector<double>& d3)
+{
+    const int P = int(std::upper_bound(ph, ph + m, x1) - ph), Q = int(std::lower_bound(ph, ph + m, x2) - ph);
+    if (P < Q)
+        for (int k = 0; k < 3; ++k) {
+            d3[3 * P + k] += v[k];
+            d3[3 * Q + k] -= v[k];
+        }
+}
+
+// chi^2 of one pair against its light curve (k_lnlike restated on the host)
+double chisq(const Pair& G, const Tables& T, const double* x, const double* w, const double* y, const double* ye, int n,
+             int S, std::vector<double>& buf)
+{
+    // point windows, and the sub-bin windows / centres (flattened, sorted when
+    // the windows are)
+    const int ns = n * S;
+    buf.assign(size_t(9) * n + size_t(10) * ns + 8, 0.0);
+    double* lo = buf.data();
+    double* hi = lo + n;
+    double* iw = hi + n;
+    double* dw = iw + n;       // WD difference array [n + 1]
+    double* dd = dw + n + 1;   // disc
+    double* xw = dd + n + 1;   // WD direct
+    double* xd = xw + n;       // disc direct
+    double* slo = xd + n + 1;  // sub-bin windows
+    double* shi = slo + ns;
+    double* siw = shi + ns;
+    double* sph = siw + ns;
+    double* ds = sph + ns;      // spot difference array [ns + 1]
+    double* xs = ds + ns + 1;   // spot direct
+    bool sorted = true;
+    for (int p = 0; p < n; ++p) {
+        const double ph = wrap_phase(x[p] - G.phi0), h = w ? w[p] : 0.0;
+        lo[p] = ph - h;
+        hi[p] = ph + h;
+        iw[p] = 1.0 / (2.0 * h);
+        sorted = sorted && h >= 0.0 && (p == 0 || (lo[p] >= lo[p - 1] && hi[p] >= hi[p - 1]));
+        const double hs = h / S;
+        for (int j = 0; j < S; ++j) {
+            const int q = p * S + j;
+            sph[q] = wrap_phase(ph - h + (2 * j + 1) * hs);
+            slo[q] = sph[q] - hs;
+            shi[q] = sph[q] + hs;
+            siw[q] = 1.0 / (2.0 * hs);
+            sorted = sorted && (q == 0 || (slo[q] >= slo[q - 1] && shi[q] >= shi[q - 1] && sph[q] >= sph[q - 1]));
+        }
+    }
+    std::vector<double> d3(size_t(3) * (ns + 1), 0.0);
+    std::vector<double> eb(ns, 0.0), V(size_t(3) * ns, 0.0);
+    std::vector<double> fw(n, 0.0), fd(n, 0.0);
+    if (sorted) {
+        for (int k = 0; k < NWD + NDISC; ++k)
+            if (T.a[k] < T.b[k]) sweep_window(lo, hi, iw, n, T.a[k], T.b[k], T.w[k], T.wd[k] ? dw : dd, T.wd[k] ? xw : xd);
+        for (int k = 0; k < NBS; ++k)
+            if (T.sa[k] < T.sb[k]) sweep_window(slo, shi, siw, ns, T.sa[k], T.sb[k], T.sw[k], ds, xs);
+        for (int t = 0; t < NDONOR; ++t) {
+            const double cen = T.dcen[t], hwd = T.dhw[t];
+            if (!(hwd > 0.0)) continue;
+            if (hwd >= 0.5) { sweep_points(sph, ns, -INFINITY, INFINITY, T.dv[t], d3); continue; }
+            const double l = cen - hwd, h = cen + hwd;
+            if (l < -0.5) {
+                sweep_points(sph, ns, -INFINITY, h, T.dv[t], d3);
+                sweep_points(sph, ns, l + 1.0, INFINITY, T.dv[t], d3);
+            } else if (h > 0.5) {
+                sweep_points(sph, ns, -INFINITY, h - 1.0, T.dv[t], d3);
+                sweep_points(sph, ns, l, INFINITY, T.dv[t], d3);
+            } else {
+                sweep_points(sph, ns, l, h, T.dv[t], d3);
+            }
+        }
+        double aw = 0.0, ad = 0.0, as = 0.0, av[3] = {0.0, 0.0, 0.0};
+        for (int p = 0; p < n; ++p) {
+            aw += dw[p];
+            ad += dd[p];
+            fw[p] = aw + xw[p];
+            fd[p] = ad + xd[p];
+        }
+        for (int q = 0; q < ns; ++q) {
+            as += ds[q];
+            eb[q] = as + xs[q];
+            for (int k = 0; k < 3; ++k) {
+                av[k] += d3[3 * q + k];
+                V[3 * q + k] = av[k];
+            }
+        }
+    } else {  // unsorted windows: every element against each point
+        for (int p = 0; p < n; ++p)
+            for (int k = 0; k < NWD + NDISC; ++k) {
+                if (!(T.a[k] < T.b[k])) continue;
+                double cov;
+                if (hi[p] > lo[p]) cov = std::fmax(std::fmin(T.b[k], hi[p]) - std::fmax(T.a[k], lo[p]), 0.0) * iw[p];
+                else cov = (T.a[k] < lo[p] && lo[p] < T.b[k]) ? 1.0 : 0.0;
+                (T.wd[k] ? fw[p] : fd[p]) += T.w[k] * cov;
+            }
+        for (int q = 0; q < ns; ++q) {
+            for (int k = 0; k < NBS; ++k) {
+                if (!(T.sa[k] < T.sb[k])) continue;
+                double cov;
+                if (shi[q] > slo[q]) cov = std::fmax(std::fmin(T.sb[k], shi[q]) - std::fmax(T.sa[k], slo[q]), 0.0) * siw[q];
+                else cov = (T.sa[k] < sph[q] && sph[q] < T.sb[k]) ? 1.0 : 0.0;
+                eb[q] += T.sw[k] * cov;
+            }
+            const double e0 = G.s * std::cos(TWO_PI * sph[q]), e1 = -G.s * std::sin(TWO_PI * sph[q]);
+            for (int t = 0; t < NDONOR; ++t)
+                if (T.dv[t][0] * e0 + T.dv[t][1] * e1 + T.dv[t][2] * G.c > 0.0)
+                    for (int k = 0; k < 3; ++k) V[3 * q + k] += T.dv[t][k];
+        }
+    }
+    double chi = 0.0;
+    for (int p = 0; p < n; ++p) {
+        double sbs = 0.0, srs = 0.0;
+        for (int j = 0; j < S; ++j) {
+            const int q = p * S + j;
+            const double e0 = G.s * std::cos(TWO_PI * sph[q]), e1 = -G.s * std::sin(TWO_PI * sph[q]);
+            const double D = e0 * V[3 * q] + e1 * V[3 * q + 1] + G.c * V[3 * q + 2];
+            double beam = 0.0;
+            if (G.bden > 0.0) beam = (G.fis + (1.0 - G.fis) * std::fmax(G.nb0 * e0 + G.nb1 * e1 + G.nb2 * G.c, 0.0)) / G.bden;
+            sbs += beam * (1.0 - eb[q]);
+            srs += D / T.dnorm;
+        }
+        const double f = G.wdf * (1.0 - fw[p]) + G.df * (1.0 - fd[p]) + G.sf * sbs / S + G.rsf * srs / S;
+        if (std::isnan(f)) return INFINITY;
+        const double r = (y[p] - f) / ye[p];
+        chi += r * r;
+    }
+    return chi;
+}
+
+}  // namespace
+
+extern "C" {
+
+// ln_prob of W walkers of a compiled chi^2 tree (the oracle's
+// lfo_lnprob_batch arguments); returns the threads used
+int lfc_lnprob_batch(const double* walkers, int W, int ndim, int E, const int* gather, const int* npars,
+                     const double* consts, const int* off, const double* x, const double* y, const double* ye,
+                     const double* w, int nsub, const int* prior_type, const double* prior_p1, const double* prior_p2,
+                     const double* prior_norm, int roche_priors, double* lnp, int nthreads)
+{
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+    int used = 1;
+#pragma omp parallel num_threads(nthreads)
+    {
+#pragma omp single
+        used = omp_get_num_threads();
+        std::vector<double> buf;
+        std::vector<Pair> pairs(E);
+        std::vector<int> status(E);
+        Tables* T = new Tables;
+#pragma omp for schedule(dynamic, 1)
+        for (int iw = 0; iw < W; ++iw) {
+            const double* v = walkers + size_t(iw) * ndim;
+            double lp = 0.0;
+            auto par = [&](int g) { return g >= 0 ? v[g] : consts[-1 - g]; };
+            if (roche_priors) {  // LCModel.ln_prior: dphi <= findphi(q, 90) - 1e-6 (CVModel.py:452-473)
+                Roche R;
+                double maxphi = -INFINITY;
+                if (roche_init(R, par(gather[4])) == ST_OK && findphi_fast(R, 90.0, maxphi) != ST_OK) maxphi = -INFINITY;
+                if (!(par(gather[5]) <= maxphi - DPHI_TOL)) lp = -INFINITY;
+            }
+            for (int d = 0; d < ndim && lp > -INFINITY; ++d)
+                lp += lfg::prior_lnprob(prior_type[d], prior_p1[d], prior_p2[d], prior_norm[d], v[d]);  // Prior.ln_prob (model.py:83-113)
+            double pin[18];
+            for (int e = 0; e < E && lp > -INFINITY; ++e) {
+                for (int k = 0; k < npars[e]; ++k) pin[k] = par(gather[e * 18 + k]);
+                double rp;
+                status[e] = setup_pair(pin, npars[e], pairs[e], rp);
+                if (roche_priors) lp += rp;
+            }
+            double ll = 0.0;
+            for (int e = 0; e < E && lp > -INFINITY; ++e) {
+                if (status[e] != ST_OK) { ll = -INFINITY; break; }
+                elements(pairs[e], *T);
+                ll += -0.5 * chisq(pairs[e], *T, x + off[e], w ? w + off[e] : nullptr, y + off[e], ye + off[e],
+                                   off[e + 1] - off[e], nsub, buf);
+            }
+            lnp[iw] = lp > -INFINITY ? lp + ll : -INFINITY;
+        }
+        delete T;
+    }
+    return used;
+}
+
+}  // extern "C"
