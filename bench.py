@@ -56,23 +56,20 @@ sys.path.insert(0, ROOT)
 # MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md; FP64 vector = spec)
 HBM_PEAK_GBS = 8000.0
 FP64_PEAK_TFLOPS = 78.6
-PMC_FILES = [os.path.join(ROOT, "profiles", r, "pmc_traffic.json") for r in ("r02", "r01")]
+PMC_DIR = os.path.join(ROOT, "profiles", "r03")   # pmc_traffic_<config>.json (tools/pmc_traffic.py)
 
 NEV = 4  # LFG_NEV (include/lfg.h)
 # (name as rocprofv3 prints it, start event, end event)
 KERNELS = [("k_setup", 0, 1), ("k_elements", 1, 2), ("k_lnlike", 2, 3)]
 
-# Counted algorithmic FP64 work per walker-eclipse evaluation (MODEL_SPEC.md
-# section 11; tools/flop_count.py -> profiles/r02/flops_c2.json, the config-2
-# walker ball): setup + stream + prior lanes, per element root (900
-# symmetry-unique roots per pair), and the direct-form accumulation per
-# element per point per sub-phase
-F_SETUP = 1543.0
-F_GEOM_ROOT = 1109.0
-N_ROOTS = 900
-F_ACC_ECL, F_ACC_DON, F_POINT = 3.0, 6.0, 40.0
-N_ECL, N_DON = 1500, 400
-F_GP_POINT = 150.0   # one Kalman step (MODEL_SPEC 10.4)
+# Counted FP64 work per (walker, eclipse) pair of the algorithm the kernels
+# execute (MODEL_SPEC.md section 11; tools/flop_count.py + tools/like_count.py
+# -> profiles/r03/flops_<config>.json): per-kernel figures for the roofline's
+# kernel fraction and the whole step, and the direct-form count of SURVEY
+# 8(d) (900 roots x geometry + N S (1500 x 3 + 400 x 6 + 40)) kept apart as
+# direct_form_equivalent
+FLOPS_DIR = os.path.join(ROOT, "profiles", "r03")
+FLOPS_TABLE = {"2": "c2", "3": "c3", "4": "c2", "5": "c5", "gp": "gp"}
 
 # builder's intermediate tables per (walker, eclipse) pair:
 # what each kernel reads and writes of the tables the kernels hand each other
@@ -198,31 +195,60 @@ def build_model(args, flux_fn):
     return synthetic.config_single(npts=args.npts, flux_fn=flux_fn, nsub=args.nsub)
 
 
-def flops_per_pair(npts, nsub, gp, fused=True):
-    """Counted algorithmic FP64 FLOPs of one walker-eclipse evaluation, by
-    kernel (MODEL_SPEC.md section 11).  With the fused element phase
-    (liblfg's default) k_lnlike solves the elements too."""
-    acc = npts * nsub * (N_ECL * F_ACC_ECL + N_DON * F_ACC_DON + F_POINT)
-    if gp:
-        acc += npts * F_GP_POINT
-    geom = N_ROOTS * F_GEOM_ROOT
-    if fused:
-        return {"k_setup": F_SETUP, "k_elements": 0.0, "k_lnlike": geom + acc}
-    return {"k_setup": F_SETUP, "k_elements": geom, "k_lnlike": acc}
+def flops_per_pair(config, npts, nsub):
+    """Counted FP64 FLOPs of one walker-eclipse pair by kernel (MODEL_SPEC.md
+    section 11), from the committed table of the configuration's workload.
+    Config 4 runs config 2's light curve.  A run whose points x sub-samples
+    differ from the table's scales k_lnlike's per-point part (its tiles and
+    sub-bin work grow linearly with N S) and says so."""
+    path = os.path.join(FLOPS_DIR, "flops_%s.json" % FLOPS_TABLE[config])
+    d = json.load(open(path))
+    pk = dict(d["per_kernel"])
+    direct = float(d["F_direct_form_equivalent_per_pair"])
+    note = None
+    ns0 = d["npts"] * d["nsub"]
+    if config != "gp" and npts * nsub != ns0:
+        r = npts * nsub / float(ns0)
+        fixed = d["F_like_parts"]["prologue"] + d["F_like_parts"]["wd_disc"]
+        pk["k_lnlike"] = fixed + (pk["k_lnlike"] - fixed) * r
+        direct = (direct - d["F_acc_total"]) + d["F_acc_total"] * r
+        note = "scaled from %s's %d x %d points x sub-samples" % (os.path.basename(path), d["npts"], d["nsub"])
+    executed = float(pk["k_elements"] + pk["k_lnlike"])   # the spec path: no k_setup launch per step
+    return {"per_kernel": pk, "executed": executed, "direct": direct, "note": note,
+            "source": os.path.relpath(path, ROOT)}
 
 
-def pmc_row(kernel):
-    """Counter-derived bytes / FLOPs per launch of `kernel` (profiles/), or None."""
-    for path in PMC_FILES:
-        try:
-            d = json.load(open(path))
-        except (OSError, ValueError):
+# kernels inside each event span of the timed region (the GP pair of kernels
+# runs between k_lnlike's events)
+SPAN = {"k_setup": ("k_setup",), "k_elements": ("k_elements",),
+        "k_lnlike": ("k_lnlike", "k_gp_dcp", "k_gp_like")}
+
+
+def pmc_row(kernel, config, npts, nsub, pairs):
+    """Counter-derived bytes and executed FP64 FLOPs per launch of the event
+    span `kernel` (summed over the kernels in it; the one-off initial
+    k_lnlike<0> excluded), scaled to `pairs`, from the committed PMC summary
+    of this configuration's workload; (None, None) when there is none."""
+    path = os.path.join(PMC_DIR, "pmc_traffic_%s.json" % FLOPS_TABLE[config])
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None, None
+    meta = d.get("meta", {})
+    if config != "gp" and (meta.get("npts"), meta.get("nsub")) != (npts, nsub):
+        return None, None
+    out = {}
+    for name, row in d.get("kernels", {}).items():
+        base = name.split("<")[0]
+        if base not in SPAN[kernel] or name.startswith("k_lnlike<0"):
             continue
-        row = d.get("kernels", {}).get(kernel)
-        if row is None:
-            row = d.get("kernels", {}).get(kernel + "<1>")
-        return row, d.get("meta", {}), path
-    return None, None, None
+        for k in ("traffic_bytes", "fp64_flops"):
+            if k in row:
+                out[k] = out.get(k, 0.0) + row[k]
+    if not out:
+        return None, None
+    scale = pairs / float(meta.get("pairs_per_launch", pairs))
+    return {k: v * scale for k, v in out.items()}, os.path.relpath(path, ROOT)
 
 
 def run(args):
@@ -411,20 +437,18 @@ def run(args):
     value = W * args.steps / elapsed
     acc = float(np.mean(S.acceptance_fraction))
 
-    # ---- FP64 roofline on counted algorithmic FLOPs (MODEL_SPEC 11)
-    fused = b"fused" in L.lfg_version()
-    fpp = flops_per_pair(npts, tree.nsub, tree.gp, fused)
-    f_eval = E * sum(fpp.values())                       # per walker evaluation
-    tf = value / world * f_eval / 1e12                   # per GPU, whole step
+    # ---- FP64 roofline on the counted work of the executed algorithm (MODEL_SPEC 11)
+    fl = flops_per_pair(args.config, npts, tree.nsub)
+    fpp = fl["per_kernel"]
     pairs = shard * E
-    dom_flops = fpp[kname] * pairs
+    dom_flops = fpp[kname] * pairs                      # the dominant kernel, per launch
     dom_tf = dom_flops / (avg_dom * 1e-3) / 1e12
+    step_tf = value / world * E * fl["executed"] / 1e12   # per GPU, whole step
+    direct_tf = value / world * E * fl["direct"] / 1e12
     kern = {}
     for n, m in calib.items():
-        if fused and n == "k_elements":
-            continue  # no such launch: k_lnlike's element phase
         f = fpp[n] * pairs
-        kern[n] = {"warmup_ms": m, "alg_flops_per_launch": f,
+        kern[n] = {"warmup_ms": m, "flops_per_launch": f,
                    "tflops": f / (m * 1e-3) / 1e12 if m > 0 else None,
                    "frac": f / (m * 1e-3) / 1e12 / FP64_PEAK_TFLOPS if m > 0 else None}
 
@@ -432,24 +456,22 @@ def run(args):
     half_s = elapsed / args.steps / 2.0
     hbm_bytes = shard * (8 * tree.ndim + 8) + 32 * npts * E
     hbm_gbs = hbm_bytes / half_s / 1e9
-    mat = 0 if fused else MATERIALISED_PER_PAIR[kname] * pairs
+    mat = MATERIALISED_PER_PAIR[kname] * pairs
 
     # counter-derived traffic and executed FP64 FLOPs of the dominant kernel
-    # (rocprofv3 --pmc passes, tools/pmc_profile.sh -> profiles/r0N/pmc_traffic.json);
-    # the committed PMC pass is of the default workload (config 2, 300 points,
-    # nsub 1): per-pair counters do not carry over to other workloads
-    row, meta, pmc_path = pmc_row(kname) if (args.config == "2" and args.npts == 300 and args.nsub == 1) \
-        else (None, None, None)
+    # (rocprofv3 --pmc passes, tools/pmc_profile.sh -> tools/pmc_traffic.py ->
+    # profiles/r03/pmc_traffic_<config>.json); per-pair counters carry over only
+    # to the workload they were collected on
+    row, pmc_path = pmc_row(kname, args.config, npts, tree.nsub, pairs)
     traffic = fp64x = None
-    if row and meta:
-        scale = pairs / float(meta.get("pairs_per_launch", pairs))
-        if "traffic_bytes" in row:
-            traffic = row["traffic_bytes"] * scale
+    if row:
+        traffic = row.get("traffic_bytes")
         if "fp64_flops" in row:
-            f = row["fp64_flops"] * scale
+            f = row["fp64_flops"]
             fp64x = {"executed_flops_per_launch": f, "tflops": f / (avg_dom * 1e-3) / 1e12,
                      "frac": f / (avg_dom * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
-                     "source": os.path.relpath(pmc_path, ROOT)}
+                     "counted_over_executed": dom_flops / f if f else None,
+                     "source": pmc_path}
 
     cpu = {"cpu_baseline": None}
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -482,20 +504,27 @@ def run(args):
                        "parallelism": "walker shards x%d, replicated Philox RNG, one all_gather of ln_prob "
                                       "per half-step (%s)" % (world, xch)},
             "roofline": {
-                "bound": "fp64_valu", "achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": tf / FP64_PEAK_TFLOPS, "traffic": traffic,
-                "basis": "counted algorithmic FP64 FLOPs per walker-eclipse eval x evals/s per GPU over the "
-                         "whole step (MODEL_SPEC 11): F_setup + 900 roots x F_geom + N S (1500 x 3 + 400 x 6 + 40)",
-                "flops_per_walker_eval": f_eval,
-                "note": (None if tf <= FP64_PEAK_TFLOPS else
-                         "the direct-form count of SURVEY 8(d) exceeds the FP64 peak here: k_lnlike's sweep forms "
-                         "the same sums with O(N S + N_el) work per pair, so frac > 1 is not a utilisation "
-                         "(MODEL_SPEC 11)"),
-                "flops_per_pair": fpp,
+                "bound": "fp64_valu", "achieved": dom_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": dom_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
+                "basis": "the dominant kernel (%s): its counted FP64 work per launch (MODEL_SPEC 11, %s x %d "
+                         "pairs) / its average launch time over the timed region (HIP events on its stream)"
+                         % (kname, fl["source"], pairs),
                 "kernel": {"name": kname, "avg_launch_ms": avg_dom, "launches_timed": ncalls,
-                           "alg_flops_per_launch": dom_flops, "achieved": dom_tf,
-                           "frac": dom_tf / FP64_PEAK_TFLOPS, "executed_fp64": fp64x,
+                           "pairs_per_launch": pairs, "flops_per_pair": fpp[kname],
+                           "flops_per_launch": dom_flops, "executed_fp64": fp64x,
                            "traffic_bytes_per_launch": traffic},
+                "whole_step": {"achieved": step_tf, "frac": step_tf / FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                               "flops_per_pair": fl["executed"],
+                               "basis": "counted FP64 work of every kernel the step launches (k_elements incl. "
+                                        "its speculative setup lanes, k_lnlike incl. the GP kernels) x E pairs x "
+                                        "evals/s per GPU"},
+                "direct_form_equivalent": {
+                    "achieved": direct_tf, "flops_per_pair": fl["direct"], "unit": "TFLOP/s",
+                    "note": "SURVEY 8(d)'s direct-form count (each element against each point and sub-phase); "
+                            "the kernels form the same sums with an interval sweep, so this is a rate of "
+                            "equivalent work, not a utilisation, and may exceed the peak"},
+                "flops_per_pair": fpp,
+                **({"flops_note": fl["note"]} if fl["note"] else {}),
                 "kernels_warmup": kern,
                 "hbm": {"algorithmic_bytes_per_half_step": hbm_bytes, "achieved": hbm_gbs, "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": hbm_gbs / HBM_PEAK_GBS,

@@ -28,6 +28,7 @@ F_ACC_ECL = 3    # overlap |[a,b] n window| (1 sub) + weighted accumulate (1 fma
 F_ACC_DON = 6    # projection dA n.e (1 mul + 2 fma) + max(0, .) accumulate (1 add)
 F_POINT = 40     # per point per sub-phase: phase wrap, sincospi, beaming, donor normalisation, chi^2 share
 N_ECL, N_DON = 1500, 400
+F_GP_STEP = 150  # one Kalman step of k_gp_like (unit count gp_kalman_step)
 U_ROOTS = {"wd": 200, "disc": 500, "spot": 100, "donor": 100}
 
 
@@ -51,7 +52,10 @@ def walkers(config, n, seed=20261015):
 
     def flux_fn(p, x, w, nsub):
         return o.flux(p, x, w, nsub=nsub)[1]
-    if config == 3:
+    if config == "gp":
+        from lfit_python_amd import cvmodel
+        model = cvmodel.construct_model(os.path.join(ROOT, "tests", "golden", "ref_test_data", "mcmc_input.dat"))
+    elif config == 3:
         model = synthetic.config_tree(4, 300, flux_fn=flux_fn)
     elif config == 5:
         model = synthetic.config_single(10000, flux_fn=flux_fn, nsub=5)
@@ -82,10 +86,13 @@ def cv_pars(tree, walk, e):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--config", default="2", help="2, 3, 5 or gp")
     ap.add_argument("--walkers", type=int, default=512)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--like-walkers", type=int, default=None,
+                    help="walkers whose k_lnlike work is simulated (default: 64, config 5: 6)")
     args = ap.parse_args()
+    args.config = args.config if args.config == "gp" else int(args.config)
     lib = build()
     tree, walk = walkers(args.config, args.walkers)
     rows = []
@@ -109,6 +116,26 @@ def main():
     npts = int(np.max(np.diff(tree.offsets)))
     S = tree.nsub
     f_acc_total = npts * S * (N_ECL * F_ACC_ECL + N_DON * F_ACC_DON + F_POINT)
+    # k_lnlike as executed (tools/like_count.py: the sweep and the sub-bin
+    # tables on the oracle's element intervals of each pair)
+    import like_count
+    from oracle.oracle import Oracle
+    o = Oracle()
+    nlw = args.like_walkers or (6 if args.config == 5 else 64)
+    like, like_parts = [], []
+    for e in range(E):
+        a0, a1 = tree.offsets[e], tree.offsets[e + 1]
+        for pars in cv_pars(tree, walk[:nlw], e):
+            st, a, b, wg, donor, g16 = o.elements(pars)
+            if st != 0:
+                continue
+            f, parts = like_count.count_pair(tree.x[a0:a1], tree.w[a0:a1], S, a[:1400], b[:1400], a[1400:], b[1400:],
+                                             donor, g16[2], pars[13], gp=tree.gp)
+            like.append(f)
+            like_parts.append(parts)
+    f_like = float(np.mean(like))
+    npts_mean = float(np.mean(np.diff(tree.offsets)))
+    like_parts = {k: round(float(np.mean([p[k] for p in like_parts])), 1) for k in like_parts[0]}
     res = {
         "config": args.config, "pairs_counted": int(len(R)), "walkers": int(args.walkers), "E": E,
         "npts": npts, "nsub": S,
@@ -122,6 +149,18 @@ def main():
         "F_geom_total": round(f_geom_total, 1),
         "F_acc_ecl": F_ACC_ECL, "F_acc_don": F_ACC_DON, "F_point": F_POINT,
         "F_acc_total": f_acc_total,
+        "F_like": round(f_like, 1),
+        "F_like_parts": like_parts,
+        "like_pairs_simulated": len(like),
+        # what each kernel executes per pair on the speculative single-GPU path
+        # (bench.py's default): k_elements also forms both candidates' setup
+        # for the next half; k_setup runs only off the speculative path
+        # (GP trees: the k_lnlike event span also holds k_gp_like, one Kalman
+        # step per point)
+        "per_kernel": {"k_setup": round(f_setup, 1), "k_elements": round(f_geom_total + 2 * f_setup, 1),
+                       "k_lnlike": round(f_like + (npts_mean * F_GP_STEP if tree.gp else 0.0), 1)},
+        "F_executed_per_pair": round(2 * f_setup + f_geom_total + f_like + (npts_mean * F_GP_STEP if tree.gp else 0.0), 1),
+        "F_direct_form_equivalent_per_pair": round(f_setup + f_geom_total + f_acc_total, 1),
         "F_total_per_pair": round(f_setup + f_geom_total + f_acc_total, 1),
         "transcendentals_per_pair": round(m[1] + m[3] + m[10] + m[11] + m[12] + m[13] + m[5] / E, 1),
         "newton_steps_per_eclipsed_root": round(m[16] / max(m[14], 1), 2),

@@ -1,0 +1,7 @@
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+steps=()
+for v in main NOQ NOWDD; do
+  lib=$GRAFT_REPO_ROOT/build/exp/liblfg_$v.so; [ $v = main ] && lib=$GRAFT_REPO_ROOT/lfit_python_amd/_lib/liblfg_hip.so
+  steps+=("p5_$v:200:LFG_LIB=$lib rocprofv3 --kernel-trace -d gpurun_out/g_prof5_$v -o run --output-format csv -- python3 bench.py --config 5 --steps 4 --warmup 1 --no-cpu")
+done
+tools/gpu_steps.sh "${steps[@]}"

@@ -1,7 +1,7 @@
 """HBM traffic per launch from the FETCH_SIZE / WRITE_SIZE passes of
 tools/pmc_profile.sh, for bench.py's roofline.traffic.
 
-  python tools/pmc_traffic.py gpurun_out/pmc_<tag> profiles/r01/pmc_traffic.json [pairs]
+  python tools/pmc_traffic.py gpurun_out/pmc_<tag> profiles/r03/pmc_traffic_c2.json [pairs [npts nsub]]
 
 pairs = (walker, eclipse) pairs per launch of the profiled run (bench.py
 defaults: 512 = 1024 walkers / 2 halves x 1 eclipse); bench.py scales by it.
@@ -77,6 +77,8 @@ if __name__ == "__main__":
     pairs = int(sys.argv[3]) if len(sys.argv) > 3 else 512
     res = summarise(src)
     meta = {"source": os.path.basename(os.path.normpath(src)), "pairs_per_launch": pairs,
+            "npts": int(sys.argv[4]) if len(sys.argv) > 4 else 300,
+            "nsub": int(sys.argv[5]) if len(sys.argv) > 5 else 1,
             "note": "median per dispatch of the bench's timed launches; FETCH_SIZE x2 (gfx950); KiB -> bytes"}
     with open(dst, "w") as fh:
         json.dump({"meta": meta, "kernels": res}, fh, indent=1)
