@@ -1522,25 +1522,40 @@ __device__ __forceinline__ double sub_spot(const SubTables& T, const double2* sa
     return pt ? e : fma(corr, 1.0 / (hi - lo), e);
 }
 
-// donor sum vector V (fixed point) at phase th
-__device__ __forceinline__ void sub_donor(const SubTables& T, const SubEntries& D, const double* sdq, double ivs,
-                                          double th, long long& vx, long long& vy, long long& vz)
+// donor entries sorted (after step (e) of the table build) by position,
+// an end before a start at equal positions: the entries counted at phase th
+// (starts with pos < th, ends with pos <= th) are then a prefix of the list,
+// and a lane walking up in phase keeps a cursor into it
+__device__ __forceinline__ bool donor_counted(double pos, int code, double th)
+{
+    return (code & 1) ? pos <= th : pos < th;
+}
+
+__device__ __forceinline__ void donor_apply(const double* sdq, int code, double ivs, long long& vx, long long& vy,
+                                            long long& vz)
+{
+    long long qx, qy, qz;
+    donor_q(sdq, code >> 1, ivs, qx, qy, qz);
+    if (code & 1) { vx -= qx; vy -= qy; vz -= qz; }
+    else { vx += qx; vy += qy; vz += qz; }
+}
+
+// donor sum vector V (fixed point) at phase th, and the cursor: the first
+// entry not counted at th
+__device__ __forceinline__ int sub_donor(const SubTables& T, const SubEntries& D, const double* sdq, double ivs,
+                                         double th, long long& vx, long long& vy, long long& vz)
 {
     const int g = tcell(th, T.dt0, T.dginv);
     vx = T.dpre[g][0];
     vy = T.dpre[g][1];
     vz = T.dpre[g][2];
-    for (int i = g ? T.dend[g - 1] : 0; i < T.dend[g]; ++i) {
-        const double pos = D.dpos[i];
+    int i = g ? T.dend[g - 1] : 0;
+    for (const int ie = T.dend[g]; i < ie; ++i) {
         const int code = D.dcode[i];
-        const bool end = code & 1;
-        if (end ? pos <= th : pos < th) {
-            long long qx, qy, qz;
-            donor_q(sdq, code >> 1, ivs, qx, qy, qz);
-            if (end) { vx -= qx; vy -= qy; vz -= qz; }
-            else { vx += qx; vy += qy; vz += qz; }
-        }
+        if (!donor_counted(D.dpos[i], code, th)) break;
+        donor_apply(sdq, code, ivs, vx, vy, vz);
     }
+    return i;
 }
 
 
@@ -1590,31 +1605,14 @@ __device__ __forceinline__ void lane_breakpoints(int tid, const double* sdq, con
 }
 
 
-// donor entries with (start: th0 <= pos < th1, end: th0 < pos <= th1): what
-// V gains from th0 to th1 > th0 (cells g(th0) .. g(th1))
-__device__ __forceinline__ void sub_donor_step(const SubTables& T, const SubEntries& D, const double* sdq, double ivs,
-                                               double th0, double th1, long long& vx, long long& vy, long long& vz)
-{
-    const int g0 = tcell(th0, T.dt0, T.dginv), g1 = tcell(th1, T.dt0, T.dginv);
-    for (int i = g0 ? T.dend[g0 - 1] : 0; i < T.dend[g1]; ++i) {
-        const double pos = D.dpos[i];
-        const int code = D.dcode[i];
-        const bool end = code & 1;
-        if (end ? (pos > th0 && pos <= th1) : (pos >= th0 && pos < th1)) {
-            long long qx, qy, qz;
-            donor_q(sdq, code >> 1, ivs, qx, qy, qz);
-            if (end) { vx -= qx; vy -= qy; vz -= qz; }
-            else { vx += qx; vy += qy; vz += qz; }
-        }
-    }
-}
-
 // S > 1: the spot and donor terms of one point, summed over its S sub-bins
 // (spot eclipse over each sub-bin window, donor at each sub-bin centre, from
 // the tables).  The donor vector is looked up at the first sub-bin and
-// carried forward over the breakpoints between sub-bins (usually none), and
-// the line of sight is rotated from sub-bin to sub-bin (one sincospi per
-// point); a sub-bin past +-1/2 starts over.
+// carried forward by the sorted-entry cursor (the next entry's position in
+// registers: usually one compare per sub-bin), and the line of sight is
+// rotated from sub-bin to sub-bin (one sincospi per point); a sub-bin past
+// +-1/2 starts over.  The beaming denominator and the donor normalisation
+// divide the point's sums once.
 __device__ __forceinline__ double2 sub_point(const SubTables& T, const SubEntries& D, const double2* sab, const double* sbw,
                                              const double* sdq, const double* snorm, const double* shull, const double* SG,
                                              double ph0, double wk, int S)
@@ -1623,39 +1621,54 @@ __device__ __forceinline__ double2 sub_point(const SubTables& T, const SubEntrie
     // registers over the loop they pushed k_lnlike past its budget)
     const volatile double* VG = SG;
     const volatile double* VN = snorm;
+    const int nd = T.dend[TCELLS - 1];
     const double h = wk / S;
     double sbs = 0.0, srs = 0.0, ph = 0.0, sn = 0.0, cs = 1.0, rs = 0.0, rc = 1.0;
+    double fx = 0.0, fy = 0.0, fz = 0.0, npos = INFINITY;
     long long vx = 0, vy = 0, vz = 0;
+    int cur = 0, ncode = 0;
     for (int j = 0; j < S; ++j) {
         const double phn = wrap_phase(ph0 - wk + (2 * j + 1) * h);
+        bool chg = false;
         if (j == 0 || !(phn >= ph)) {  // a fresh lookup
-            sub_donor(T, D, sdq, VN[1], phn, vx, vy, vz);
+            cur = sub_donor(T, D, sdq, VN[1], phn, vx, vy, vz);
+            chg = true;
             const double4 e4 = sincospi2_ool(2.0 * phn, 4.0 * h);  // the turn per sub-bin: 2 pi (2 h)
             sn = e4.x;
             cs = e4.y;
             rs = e4.z;
             rc = e4.w;
         } else {
-            if (phn > ph) sub_donor_step(T, D, sdq, VN[1], ph, phn, vx, vy, vz);
+            while (donor_counted(npos, ncode, phn)) {  // npos = inf past the last entry
+                donor_apply(sdq, ncode, VN[1], vx, vy, vz);
+                chg = true;
+                ++cur;
+                npos = cur < nd ? D.dpos[cur] : INFINITY;
+                ncode = cur < nd ? D.dcode[cur] : 0;
+            }
             const double c2 = fma(cs, rc, -sn * rs);
             sn = fma(sn, rc, cs * rs);
             cs = c2;
+        }
+        if (chg) {
+            if (j == 0 || !(phn >= ph)) {
+                npos = cur < nd ? D.dpos[cur] : INFINITY;
+                ncode = cur < nd ? D.dcode[cur] : 0;
+            }
+            fx = double(vx);
+            fy = double(vy);
+            fz = double(vz);
         }
         ph = phn;
         const double ebj = sub_spot(T, sab, sbw, VN[0], ph - h, ph + h, shull[2], shull[3]);
         const double sg = VG[G_S], cg = VG[G_C];
         const double e0 = sg * cs, e1 = -sg * sn;
-        const double Dv = (e0 * double(vx) + e1 * double(vy) + cg * double(vz)) * (FX_INV * VN[3]);
-        double beam = 0.0;
-        const double bden = VG[G_BDEN];
-        if (bden > 0.0) {
-            const double fis = VG[G_FIS];
-            beam = (fis + (1.0 - fis) * fmax(VG[G_NB0] * e0 + VG[G_NB1] * e1 + VG[G_NB2] * cg, 0.0)) / bden;
-        }
-        sbs += beam * (1.0 - ebj);
-        srs += Dv / VN[2];
+        srs = fma(e0, fx, fma(e1, fy, fma(cg, fz, srs)));
+        const double fis = VG[G_FIS];
+        sbs = fma(fis + (1.0 - fis) * fmax(VG[G_NB0] * e0 + VG[G_NB1] * e1 + VG[G_NB2] * cg, 0.0), 1.0 - ebj, sbs);
     }
-    return make_double2(sbs, srs);
+    const double bden = VG[G_BDEN];
+    return make_double2(bden > 0.0 ? sbs / bden : 0.0, srs * (FX_INV * VN[3]) / VN[2]);
 }
 
 #ifdef LFG_PROFILE_LIKE  // diagnostic build only: phase stamps (first tile) into spare geo slots 41..46
@@ -2056,6 +2069,26 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
             }
         }
         __syncthreads();
+        // (e) each cell's donor entries in order (sub_point's cursor): position,
+        // an end before a start at equal positions; a few entries per cell
+        if (tid < TCELLS) {
+            const int i0 = tid ? T.dend[tid - 1] : 0, i1 = T.dend[tid];
+            for (int i = i0 + 1; i < i1; ++i) {
+                const double p = DE.dpos[i];
+                const int c = DE.dcode[i];
+                int k = i;
+                for (; k > i0; --k) {
+                    const double pk = DE.dpos[k - 1];
+                    const int ck = DE.dcode[k - 1];
+                    if (!(pk > p || (pk == p && (c & 1) && !(ck & 1)))) break;
+                    DE.dpos[k] = pk;
+                    DE.dcode[k] = ck;
+                }
+                DE.dpos[k] = p;
+                DE.dcode[k] = c;
+            }
+        }
+        __syncthreads();
     }
     for (int t0 = 0; t0 < n; t0 += LIKE_TILE) {
         double chi = 0.0;  // this tile's chi^2 (summed per wave into red[1] at the tile's end)
@@ -2269,133 +2302,362 @@ __global__ __launch_bounds__(64) void k_gp_dcp(double* __restrict__ geo, const i
 
 // -------------------------------------------------------------- k_gp_like
 // GP trees (MODEL_SPEC 10.4): the Kalman filter over each pair's residuals
-// (k_lnlike<2> wrote them), one LANE per pair.  The recursion is serial in
-// the points, so a pair's cost is its dependent-latency chain whatever its
-// width; run as wave-uniform code on 64 lanes it cost 64x the VALU issue
-// and, with thousands of pairs, the SIMDs' issue rate set the time.  Lanes
-// of a wave take consecutive pairs (the eclipses of a few walkers); each
-// lane runs its pair's filter on its own points, the state-independent
-// work of a point (transition e^{-u}, changepoint block, log S) off the
-// recursion's dependent chain.  Then ln_like = -1/2 (sum v^2/S + sum ln S
-// + n ln 2 pi) and, as k_lnlike does, ln_prob and the acceptance of the
-// walker once its last eclipse is in.
+// (k_lnlike<2> wrote them), parallel in time.  The recursion is serial in
+// the points and its dependent chain (D -> S -> 1/S -> D, ~14 FP64 ops of
+// 32-48 cycles each for a lone wave, tools/lat_probe.hip) set the time when
+// one lane or one quad ran a pair's 300 points.  So a pair's points are cut
+// into GP_SEG segments, each filtered by a quad of lanes at once:
+//  * element pass (per segment s, its quad): the filter conditioned on the
+//    unknown prior state x_s at the segment's first point -- the mean is
+//    A x_s + c, the covariance starts at 0, and the segment's data give
+//    exp(-1/2 x_s^T J x_s + eta^T x_s - kappa / 2).  Lane r owns row r of
+//    D (= P - P_inf), column r of A, c_r, row r of J and eta_r; rows and
+//    gains travel by DPP quad permutes.
+//  * combine (one lane per pair, serial over the segments, 4x4 algebra):
+//    integrate x_s against its prior N(mu, Sigma), add the segment's ln_like,
+//    carry the filtered end state (A mu_post + c, A Sigma_post A^T + P_end)
+//    through the gap's transition (and a block start) to the next segment.
+// tests/gp_kalman.py:gp_lnlike_segments restates it; equal to the dense
+// likelihood to ~1e-15.
+//
+// Coordinates: Jordan form of each 2-state block.  With K = [[lam, 1],
+// [-lam^2, -lam]] (K^2 = 0), Phi(d) = e^{-u} (I + d K); z = (x0, lam x0 + x1)
+// turns it into e^{-u} T, T = [[1, d], [0, 1]].  The observation is still z0
+// and P_inf = a [[1, lam], [lam, 2 lam^2]] per block.
+//
+// Then ln_like = sum of the segments' and, as k_lnlike does, ln_prob and the
+// acceptance of the walker once its last eclipse is in.  Pairs of a wave
+// take one eclipse of consecutive walkers (equal point counts, shared x / ye).
 constexpr int GP_BLOCK = 64;
 #ifndef LFG_GP_CHUNK
 #define LFG_GP_CHUNK 8
 #endif
 constexpr int GP_CHUNK = LFG_GP_CHUNK;
-#ifndef GP_LANES
-#define GP_LANES 64  // pairs per wave (the other lanes idle)
-#endif
+constexpr int GP_SEG = 8;                     // segments per pair
+constexpr int GP_LPP = 4 * GP_SEG;            // lanes per pair: a quad per segment
+constexpr int GP_PAIRS = GP_BLOCK / GP_LPP;   // pairs per wave
+constexpr int GP_EL = 16;                     // doubles of a lane's element row in LDS
 
-__global__ __launch_bounds__(GP_BLOCK) void k_gp_like(LikeArgs L)
+// v of lane (quad base + PERM's selector for this lane): DPP quad_perm on both halves
+template <int PERM>
+__device__ __forceinline__ double quad_perm(double v)
 {
-    const int pair = blockIdx.x * GP_LANES + threadIdx.x;
-    if (threadIdx.x >= GP_LANES || pair >= L.npairs) return;
-    const int e = pair % L.E;
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(static_cast<int>(b), static_cast<int>(b), PERM, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(static_cast<int>(b >> 32), static_cast<int>(b >> 32), PERM, 0xf, 0xf,
+                                               false);
+    return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
+}
+constexpr int QP_NEXT = 0xF5;  // [1, 1, 3, 3]: the odd row of each block
+constexpr int QP_B0 = 0x00, QP_B1 = 0x55, QP_B2 = 0xAA, QP_B3 = 0xFF;  // broadcast lane 0 / 1 / 2 / 3
+
+// P_inf (z coordinates) entry (i, j) of a pair: blocks ain, aout
+__device__ __forceinline__ double gp_pinf(int i, int j, double ain, double aout, double lam)
+{
+    if ((i >> 1) != (j >> 1)) return 0.0;
+    const double a = (i >> 1) ? aout : ain;
+    const int k = (i & 1) + (j & 1);
+    return k == 0 ? a : (k == 1 ? a * lam : 2.0 * a * lam * lam);
+}
+
+// inverse of a 4x4 by its adjugate (2x2 minors of the top and bottom row
+// pairs); returns the determinant
+__device__ __forceinline__ double inv4(const double (&m)[4][4], double (&o)[4][4])
+{
+    const double s0 = fma(m[0][0], m[1][1], -m[1][0] * m[0][1]), s1 = fma(m[0][0], m[1][2], -m[1][0] * m[0][2]);
+    const double s2 = fma(m[0][0], m[1][3], -m[1][0] * m[0][3]), s3 = fma(m[0][1], m[1][2], -m[1][1] * m[0][2]);
+    const double s4 = fma(m[0][1], m[1][3], -m[1][1] * m[0][3]), s5 = fma(m[0][2], m[1][3], -m[1][2] * m[0][3]);
+    const double c5 = fma(m[2][2], m[3][3], -m[3][2] * m[2][3]), c4 = fma(m[2][1], m[3][3], -m[3][1] * m[2][3]);
+    const double c3 = fma(m[2][1], m[3][2], -m[3][1] * m[2][2]), c2 = fma(m[2][0], m[3][3], -m[3][0] * m[2][3]);
+    const double c1 = fma(m[2][0], m[3][2], -m[3][0] * m[2][2]), c0 = fma(m[2][0], m[3][1], -m[3][0] * m[2][1]);
+    const double det = (fma(s0, c5, -s1 * c4) + fma(s2, c3, s3 * c2)) + fma(s5, c0, -s4 * c1);
+    const double id = 1.0 / det;
+    o[0][0] = id * fma(m[1][1], c5, fma(-m[1][2], c4, m[1][3] * c3));
+    o[0][1] = id * fma(-m[0][1], c5, fma(m[0][2], c4, -m[0][3] * c3));
+    o[0][2] = id * fma(m[3][1], s5, fma(-m[3][2], s4, m[3][3] * s3));
+    o[0][3] = id * fma(-m[2][1], s5, fma(m[2][2], s4, -m[2][3] * s3));
+    o[1][0] = id * fma(-m[1][0], c5, fma(m[1][2], c2, -m[1][3] * c1));
+    o[1][1] = id * fma(m[0][0], c5, fma(-m[0][2], c2, m[0][3] * c1));
+    o[1][2] = id * fma(-m[3][0], s5, fma(m[3][2], s2, -m[3][3] * s1));
+    o[1][3] = id * fma(m[2][0], s5, fma(-m[2][2], s2, m[2][3] * s1));
+    o[2][0] = id * fma(m[1][0], c4, fma(-m[1][1], c2, m[1][3] * c0));
+    o[2][1] = id * fma(-m[0][0], c4, fma(m[0][1], c2, -m[0][3] * c0));
+    o[2][2] = id * fma(m[3][0], s4, fma(-m[3][1], s2, m[3][3] * s0));
+    o[2][3] = id * fma(-m[2][0], s4, fma(m[2][1], s2, -m[2][3] * s0));
+    o[3][0] = id * fma(-m[1][0], c3, fma(m[1][1], c1, -m[1][2] * c0));
+    o[3][1] = id * fma(m[0][0], c3, fma(-m[0][1], c1, m[0][2] * c0));
+    o[3][2] = id * fma(-m[3][0], s3, fma(m[3][1], s1, -m[3][2] * s0));
+    o[3][3] = id * fma(m[2][0], s3, fma(-m[2][1], s1, m[2][2] * s0));
+    return det;
+}
+
+__global__ __launch_bounds__(GP_BLOCK) __attribute__((amdgpu_waves_per_eu(2))) void k_gp_like(LikeArgs L)
+{
+    __shared__ double sel[GP_PAIRS][GP_SEG][4][GP_EL];
+    const int nw = L.npairs / L.E, nwb = (nw + GP_PAIRS - 1) / GP_PAIRS;
+    const int e = int(blockIdx.x) / nwb;
+    const int lane = int(threadIdx.x), pp = lane / GP_LPP, sg = (lane / 4) % GP_SEG, r = lane & 3;
+    const int w = (int(blockIdx.x) - e * nwb) * GP_PAIRS + pp;
+    const bool live = w < nw;
+    const int pair = live ? w * L.E + e : 0;
     const int o0 = L.off ? L.off[e] : 0;
     const int n = L.off ? L.off[e + 1] - o0 : L.N;
     const double* G = L.geo + size_t(pair) * LFG_NGEO;
-    double lle = -INFINITY;
-    if (L.status[pair] == ST_OK && G[G_GP_OK] != 0.0 && !(L.prior && prior_rejects(L.prior[pair / L.E], G))) {
-        const double ain = G[G_GP_AIN], aout = G[G_GP_AOUT], lam = G[G_GP_LAM];
-        const double dcp = G[G_GP_DCP], phi0 = G[G_PHI0];
-        const int e0 = L.gp_ecl[2 * e], e1 = L.gp_ecl[2 * e + 1];
-        const double* r = L.res + size_t(pair) * L.N;
-        const double* gx = L.gpx + size_t(pair) * L.N;
-        const int* gb = L.gpb + size_t(pair) * L.N;
-        const double* xs = L.x + o0;
-        const double* yes = L.ye + o0;
-        (void)dcp; (void)phi0; (void)e0; (void)e1;
-        // state (D = P - Pinf, MODEL_SPEC 10.4)
-        double m0 = 0.0, m1 = 0.0, m2 = 0.0, m3 = 0.0;
-        double d00 = 0.0, d01 = 0.0, d11 = 0.0, d22 = 0.0, d23 = 0.0, d33 = 0.0;
-        double d02 = 0.0, d03 = 0.0, d12 = 0.0, d13 = 0.0;
-        double q2 = 0.0, lnS = 0.0, xprev = 0.0;
-        int bp = -1;
+    const bool run = live && L.status[pair] == ST_OK && G[G_GP_OK] != 0.0 &&
+                     !(L.prior && prior_rejects(L.prior[pair / L.E], G));
+    const double ain = G[G_GP_AIN], aout = G[G_GP_AOUT], lam = G[G_GP_LAM];
+    const double* res = L.res + size_t(pair) * L.N;
+    const double* gx = L.gpx + size_t(pair) * L.N;
+    const int* gb = L.gpb + size_t(pair) * L.N;
+    const double* xs = L.x + o0;
+    const double* yes = L.ye + o0;
+    if (run) {
+        // ---- element pass: segment sg of the pair, lane r of its quad
+        const int i0 = (n * sg) / GP_SEG, i1 = (n * (sg + 1)) / GP_SEG;
+        const double pc0 = gp_pinf(r, 0, ain, aout, lam), pc2 = gp_pinf(r, 2, ain, aout, lam);
+        const bool even = (r & 1) == 0, hrow = r >= 2;
+        // P starts at 0: D = -P_inf; A = I; c = 0
+        double D0 = -gp_pinf(r, 0, ain, aout, lam), D1 = -gp_pinf(r, 1, ain, aout, lam);
+        double D2 = -gp_pinf(r, 2, ain, aout, lam), D3 = -gp_pinf(r, 3, ain, aout, lam);
+        double A0 = r == 0 ? 1.0 : 0.0, A1 = r == 1 ? 1.0 : 0.0, A2 = r == 2 ? 1.0 : 0.0, A3 = r == 3 ? 1.0 : 0.0;
+        double c = 0.0, J0 = 0.0, J1 = 0.0, J2 = 0.0, J3 = 0.0, eta = 0.0;
+        double q2 = 0.0, lnS = 0.0, xprev = (i0 > 0 && i0 < n) ? xs[i0 - 1] : 0.0;
+        int bp = (i0 > 0 && i0 < n) ? gb[i0 - 1] : -1;
         bool bad = false;
-        // points in chunks of GP_CHUNK: the chunk's loads are issued one
-        // chunk ahead, its transitions and blocks computed side by side,
-        // so that only the recursion itself is serial
         double cx[GP_CHUNK], cy[GP_CHUNK], cr[GP_CHUNK], ce[GP_CHUNK];
         int cb[GP_CHUNK];
         auto fetch = [&](int p0) {
 #pragma unroll
             for (int k = 0; k < GP_CHUNK; ++k) {
-                const int q = min(p0 + k, n - 1);
+                const int q = min(p0 + k, i1 - 1);
                 cx[k] = xs[q];
                 cy[k] = yes[q];
-                cr[k] = r[q];
+                cr[k] = res[q];
                 ce[k] = gx[q];
                 cb[k] = gb[q];
             }
         };
-        if (n > 0) fetch(0);
-        for (int p0 = 0; p0 < n; p0 += GP_CHUNK) {
-            double a00[GP_CHUNK], a01[GP_CHUNK], a10[GP_CHUNK], a11[GP_CHUNK], ye2[GP_CHUNK], rv[GP_CHUNK];
+        if (i1 > i0) fetch(i0);
+        for (int p0 = i0; p0 < i1; p0 += GP_CHUNK) {
+            double dk[GP_CHUNK], ek[GP_CHUNK], Ek[GP_CHUNK], ye2[GP_CHUNK], rv[GP_CHUNK];
             int blk[GP_CHUNK];
 #pragma unroll
             for (int k = 0; k < GP_CHUNK; ++k) {
                 const double dd = cx[k] - (k ? cx[k - 1] : xprev);
-                const double u = lam * dd, ex = ce[k];  // e^{-u}, formed in k_lnlike<2>
-                a00[k] = ex * (1.0 + u);
-                a01[k] = ex * dd;
-                a10[k] = -ex * lam * u;
-                a11[k] = ex * (1.0 - u);
+                dk[k] = dd;
+                ek[k] = ce[k];  // e^{-lam dd}, formed in k_lnlike<2>
+                Ek[k] = ce[k] * ce[k];
                 ye2[k] = cy[k] * cy[k];
                 rv[k] = cr[k];
                 blk[k] = cb[k];
-                bad = bad || (p0 + k < n && p0 + k > 0 && !(dd >= 0.0)) || (p0 + k < n && !isfinite(cr[k]));
+                bad = bad || (p0 + k < i1 && p0 + k > 0 && !(dd >= 0.0)) || (p0 + k < i1 && !isfinite(cr[k]));
             }
             xprev = cx[GP_CHUNK - 1];
-            if (p0 + GP_CHUNK < n) fetch(p0 + GP_CHUNK);  // in flight during the recursion
+            if (p0 + GP_CHUNK < i1) fetch(p0 + GP_CHUNK);  // in flight during the recursion
             double prodS = 1.0;  // one log per chunk (S ~ ye^2: eight factors stay far from underflow)
 #pragma unroll
             for (int k = 0; k < GP_CHUNK; ++k) {
-                if (p0 + k >= n) break;
-                if (p0 + k > 0) {  // predict: m <- Phi m, D <- Phi D Phi^T per 2x2 block
-                    const double f00 = a00[k], f01 = a01[k], f10 = a10[k], f11 = a11[k];
-                    double t0 = f00 * m0 + f01 * m1;
-                    m1 = f10 * m0 + f11 * m1;
-                    m0 = t0;
-                    t0 = f00 * m2 + f01 * m3;
-                    m3 = f10 * m2 + f11 * m3;
-                    m2 = t0;
-                    GPFilter::sym(f00, f01, f10, f11, d00, d01, d11);
-                    GPFilter::sym(f00, f01, f10, f11, d22, d23, d33);
-                    const double t00 = f00 * d02 + f01 * d12, t01 = f00 * d03 + f01 * d13;
-                    const double t10 = f10 * d02 + f11 * d12, t11 = f10 * d03 + f11 * d13;
-                    d02 = t00 * f00 + t01 * f01;
-                    d03 = t00 * f10 + t01 * f11;
-                    d12 = t10 * f00 + t11 * f01;
-                    d13 = t10 * f10 + t11 * f11;
-                }
-                if (blk[k] >= 0 && blk[k] != bp) {  // a new block: its process starts stationary, independent
-                    m2 = m3 = 0.0;
-                    d22 = d23 = d33 = d02 = d03 = d12 = d13 = 0.0;
-                }
+                if (p0 + k >= i1) break;
+                // a new block: its process starts stationary and independent
+                // of x_s: rows / columns 2, 3 of D and rows 2, 3 of A and c
+                // restart at 0 (zero scales in the prediction; the block
+                // start at the segment's first point is the combine's)
+                const bool fresh = blk[k] >= 0 && blk[k] != bp;
                 bp = blk[k];
+                if (p0 + k > i0) {  // predict: D <- e^{-2u} T D T^T, A <- e^{-u} T A, c <- e^{-u} T c
+                    const double d = dk[k], dr = even ? d : 0.0, ex = ek[k];
+                    const double kr = (fresh && hrow) ? 0.0 : 1.0, kc = fresh ? 0.0 : 1.0;
+                    const double n0 = quad_perm<QP_NEXT>(D0), n1 = quad_perm<QP_NEXT>(D1);
+                    const double n2 = quad_perm<QP_NEXT>(D2), n3 = quad_perm<QP_NEXT>(D3);
+                    const double nc = quad_perm<QP_NEXT>(c);
+                    const double t0 = fma(dr, n0, D0), t1 = fma(dr, n1, D1);
+                    const double t2 = fma(dr, n2, D2), t3 = fma(dr, n3, D3);
+                    const double Eg = Ek[k] * kr, Eh = Eg * kc;
+                    D0 = Eg * fma(d, t1, t0);
+                    D1 = Eg * t1;
+                    D2 = Eh * fma(d, t3, t2);
+                    D3 = Eh * t3;
+                    const double exh = ex * kc;
+                    A0 = ex * fma(d, A1, A0);
+                    A1 = ex * A1;
+                    A2 = exh * fma(d, A3, A2);
+                    A3 = exh * A3;
+                    c = (ex * kr) * fma(dr, nc, c);
+                }
                 const double a = (blk[k] >= 0) ? 1.0 : 0.0;
-                const double k0 = (d00 + ain) + a * d02, k1 = d01 + a * d12;
-                const double k2 = d02 + a * (d22 + aout), k3 = d03 + a * d23;
+                // k = P h, h = (1, 0, a, 0), P = D + P_inf: this row's gain
+                const double kk = (D0 + pc0) + a * (D2 + pc2);
+                const double k0 = quad_perm<QP_B0>(kk), k1 = quad_perm<QP_B1>(kk);
+                const double k2 = quad_perm<QP_B2>(kk), k3 = quad_perm<QP_B3>(kk);
+                const double c0 = quad_perm<QP_B0>(c), c2 = quad_perm<QP_B2>(c);
+                const double hA = fma(a, A2, A0);  // (h^T A)_r
+                const double h0 = quad_perm<QP_B0>(hA), h1 = quad_perm<QP_B1>(hA);
+                const double h2 = quad_perm<QP_B2>(hA), h3 = quad_perm<QP_B3>(hA);
                 const double S = fma(a, k2, k0) + ye2[k];
-                const double v = rv[k] - fma(a, m2, m0);
-                const double iS = rcp_fast(S);  // v_rcp_f64 + one Newton step: ~1 ulp, off the IEEE divide's chain
-                bad = bad || !(S > 0.0) || !isfinite(v);
-                q2 = fma(v * v, iS, q2);
+                const double vt = rv[k] - fma(a, c2, c0);
+                const double iS = rcp_fast(S);  // v_rcp_f64 (2.5e-8) + one Newton step: ~1 ulp
+                bad = bad || !(S > 0.0) || !isfinite(vt);
+                q2 = fma(vt * vt, iS, q2);
                 prodS *= S;
-                const double g = v * iS;
-                m0 = fma(k0, g, m0);
-                m1 = fma(k1, g, m1);
-                m2 = fma(k2, g, m2);
-                m3 = fma(k3, g, m3);
-                d00 -= k0 * k0 * iS; d01 -= k0 * k1 * iS; d11 -= k1 * k1 * iS;
-                d22 -= k2 * k2 * iS; d23 -= k2 * k3 * iS; d33 -= k3 * k3 * iS;
-                d02 -= k0 * k2 * iS; d03 -= k0 * k3 * iS; d12 -= k1 * k2 * iS; d13 -= k1 * k3 * iS;
+                const double g = hA * iS;
+                J0 = fma(g, h0, J0);
+                J1 = fma(g, h1, J1);
+                J2 = fma(g, h2, J2);
+                J3 = fma(g, h3, J3);
+                eta = fma(g, vt, eta);
+                c = fma(kk, vt * iS, c);
+                A0 = fma(-k0, g, A0);
+                A1 = fma(-k1, g, A1);
+                A2 = fma(-k2, g, A2);
+                A3 = fma(-k3, g, A3);
+                const double j = kk * iS;
+                D0 = fma(-j, k0, D0);
+                D1 = fma(-j, k1, D1);
+                D2 = fma(-j, k2, D2);
+                D3 = fma(-j, k3, D3);
             }
             lnS += log(prodS);
         }
-        const double v = -0.5 * (q2 + lnS + n * 1.8378770664093454836);  // log(2 pi)
+        double* o = sel[pp][sg][r];
+        o[0] = D0; o[1] = D1; o[2] = D2; o[3] = D3;
+        o[4] = A0; o[5] = A1; o[6] = A2; o[7] = A3;
+        o[8] = c;
+        o[9] = J0; o[10] = J1; o[11] = J2; o[12] = J3;
+        o[13] = eta;
+        o[14] = q2 + lnS;
+        o[15] = bad ? 1.0 : 0.0;
+    }
+    __syncthreads();
+    if (!live || (lane % GP_LPP) != 0) return;
+    double lle = -INFINITY;
+    if (run) {
+        // ---- combine: serial over the segments, one lane
+        double mu[4] = {0.0, 0.0, 0.0, 0.0}, Sg[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) Sg[i][j] = gp_pinf(i, j, ain, aout, lam);
+        double ll = 0.0;
+        bool bad = false;
+        for (int s = 0; s < GP_SEG; ++s) {
+            const int i0 = (n * s) / GP_SEG, i1 = (n * (s + 1)) / GP_SEG;
+            if (i1 <= i0) continue;  // an empty segment: nothing observed, no transition
+            const double* El = &sel[pp][s][0][0];
+            bad = bad || El[15] != 0.0 || El[GP_EL + 15] != 0.0;
+            if (s > 0 && i0 > 0) {  // the gap from the previous segment's last point
+                const double d = xs[i0] - xs[i0 - 1], ex = gx[i0], E = ex * ex;
+                const int b1 = gb[i0];
+                const bool fresh = b1 >= 0 && b1 != gb[i0 - 1];
+                mu[0] = ex * fma(d, mu[1], mu[0]);
+                mu[1] = ex * mu[1];
+                mu[2] = ex * fma(d, mu[3], mu[2]);
+                mu[3] = ex * mu[3];
+                double T[4][4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i)  // rows of T (Sigma - P_inf)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const double v = Sg[i][j] - gp_pinf(i, j, ain, aout, lam);
+                        const double vn = (i & 1) ? 0.0 : Sg[i + 1][j] - gp_pinf(i + 1, j, ain, aout, lam);
+                        T[i][j] = fma(d, vn, v);
+                    }
+#pragma unroll
+                for (int i = 0; i < 4; ++i)  // columns, scaling, + P_inf
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        Sg[i][j] = fma(E, (j & 1) ? T[i][j] : fma(d, T[i][j + 1], T[i][j]), gp_pinf(i, j, ain, aout, lam));
+                if (fresh) {
+                    mu[2] = mu[3] = 0.0;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            if (i >= 2 || j >= 2) Sg[i][j] = gp_pinf(i, j, ain, aout, lam);
+                }
+            }
+            // the element's A, P_end, J, c, eta are read from LDS where they
+            // are used (held in registers they pushed the combine into spills)
+            auto EA = [&](int i, int j) { return El[j * GP_EL + 4 + i]; };  // lane j wrote column j of A
+            auto EJ = [&](int i, int j) { return El[i * GP_EL + 9 + j]; };
+            auto EP = [&](int i, int j) { return El[i * GP_EL + j] + gp_pinf(i, j, ain, aout, lam); };
+            auto Ec = [&](int i) { return El[i * GP_EL + 8]; };
+            auto Ee = [&](int i) { return El[i * GP_EL + 13]; };
+            const double kap = El[14];
+            // posterior of x_s: C = I + J Sigma (det C = det(I + Sigma J) > 0),
+            // Sigma_post = Sigma C^-1 = (Sigma^-1 + J)^-1; C^-1 by its
+            // adjugate (2x2 minors: a shallow dependent chain, one reciprocal)
+            double C[4][4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    double v = (i == j) ? 1.0 : 0.0;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) v = fma(EJ(i, k), Sg[k][j], v);
+                    C[i][j] = v;
+                }
+            double Ci[4][4];
+            const double det = inv4(C, Ci);
+            bad = bad || !(det > 0.0);
+            const double logdet = 0.5 * log(det);  // 1/2 ln det(I + Sigma J)
+            double Sp[4][4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    double v = 0.0;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) v = fma(Sg[i][k], Ci[k][j], v);
+                    Sp[i][j] = v;
+                }
+            double u[4], Jm[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                double v = 0.0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) v = fma(EJ(i, k), mu[k], v);
+                Jm[i] = v;
+                u[i] = Ee(i) - v;
+            }
+            double emu = 0.0, mJm = 0.0, uSu = 0.0, mp[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                double su = 0.0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) su = fma(Sp[i][k], u[k], su);
+                emu = fma(Ee(i), mu[i], emu);
+                mJm = fma(mu[i], Jm[i], mJm);
+                uSu = fma(u[i], su, uSu);
+                mp[i] = mu[i] + su;
+            }
+            ll += (emu - logdet) + 0.5 * (uSu - mJm - kap);
+            // the filtered end state: A mp + c, A Sigma_post A^T + P_end
+            double AS[4][4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                double v = Ec(i);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) v = fma(EA(i, k), mp[k], v);
+                mu[i] = v;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    double t = 0.0;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) t = fma(EA(i, k), Sp[k][j], t);
+                    AS[i][j] = t;
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    double t = EP(i, j);
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) t = fma(AS[i][k], EA(j, k), t);
+                    Sg[i][j] = t;
+                }
+        }
+        const double v = ll - 0.5 * n * 1.8378770664093454836;  // log(2 pi)
         lle = (bad || !isfinite(v)) ? -INFINITY : v;
     }
     L.lle[pair] = lle;
@@ -2851,7 +3113,7 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
         if (T->nsub > 1) hipLaunchKernelGGL((k_lnlike<2, true>), dim3(npairs), dim3(LIKE_THREADS), 0, st, L);
         else hipLaunchKernelGGL((k_lnlike<2, false>), dim3(npairs), dim3(LIKE_THREADS), 0, st, L);
         if ((rc = launch_ok())) return rc;
-        hipLaunchKernelGGL(k_gp_like, dim3((npairs + GP_LANES - 1) / GP_LANES), dim3(GP_BLOCK), 0, st, L);
+        hipLaunchKernelGGL(k_gp_like, dim3(T->E * ((W + GP_PAIRS - 1) / GP_PAIRS)), dim3(GP_BLOCK), 0, st, L);
     } else {
         if (T->nsub > 1) hipLaunchKernelGGL((k_lnlike<1, true>), dim3(npairs), dim3(LIKE_THREADS), 0, st, L);
         else hipLaunchKernelGGL((k_lnlike<1, false>), dim3(npairs), dim3(LIKE_THREADS), 0, st, L);

@@ -136,7 +136,7 @@ def test_gp_changepoints_and_kernel_match_reference(oracle):
 def test_gp_kalman_matches_dense_oracle(oracle):
     """The O(N) state-space likelihood the kernels run (tests/gp_kalman.py)
     equals the dense Cholesky likelihood: ties, empty and edge blocks."""
-    from tests.gp_kalman import gp_lnlike_kalman
+    from tests.gp_kalman import gp_lnlike_kalman, gp_lnlike_kalman_jordan, gp_lnlike_segments
     rng = np.random.default_rng(7)
     for trial in range(6):
         n = int(rng.integers(2, 120))
@@ -156,6 +156,11 @@ def test_gp_kalman_matches_dense_oracle(oracle):
         dense = oracle.gp_lnlike(x, r, ye, a1, a2, tau, blocks)
         kal = gp_lnlike_kalman(x, r, ye, a1, a2, tau, blocks)
         assert abs(dense - kal) <= 1e-10 * max(1.0, abs(dense)), (trial, dense, kal)
+        jor = gp_lnlike_kalman_jordan(x, r, ye, a1, a2, tau, blocks)  # k_gp_like's coordinates
+        assert abs(dense - jor) <= 1e-10 * max(1.0, abs(dense)), (trial, dense, jor)
+        for K in (1, 3, 8):  # k_gp_like's parallel-in-time form (8 segments), empty segments included
+            seg = gp_lnlike_segments(x, r, ye, a1, a2, tau, blocks, K)
+            assert abs(dense - seg) <= 1e-10 * max(1.0, abs(dense)), (trial, K, dense, seg)
 
 
 def test_oracle_gp_lnprob_matches_reference(oracle):
