@@ -28,7 +28,15 @@ F_ACC_ECL = 3    # overlap |[a,b] n window| (1 sub) + weighted accumulate (1 fma
 F_ACC_DON = 6    # projection dA n.e (1 mul + 2 fma) + max(0, .) accumulate (1 add)
 F_POINT = 40     # per point per sub-phase: phase wrap, sincospi, beaming, donor normalisation, chi^2 share
 N_ECL, N_DON = 1500, 400
-F_GP_STEP = 150  # one Kalman step of k_gp_like (unit count gp_kalman_step)
+# k_gp_like (lfg.hip), parallel in time: per point, the element pass of its
+# segment on a lane quad -- per lane: prediction of its D row, A column and
+# c_r 31, gain / innovation / J, eta, c, A, D updates 52, the point's
+# transition factors 3 -> 4 x 86; per segment (8 per pair) the 4x4 combine
+# in one lane: gap prediction 136, C = I + J Sigma 128, adjugate inverse 144,
+# Sigma_post 128, u / ll terms / posterior mean 104, end state 304
+F_GP_POINT = 4 * (31 + 52 + 3)
+F_GP_SEG, GP_SEG = 944, 8
+F_GP_STEP = 150  # one serial Kalman step (unit count gp_kalman_step; the k_gp helper of lfg_gp_lnlike)
 U_ROOTS = {"wd": 200, "disc": 500, "spot": 100, "donor": 100}
 
 
@@ -135,6 +143,7 @@ def main():
             like_parts.append(parts)
     f_like = float(np.mean(like))
     npts_mean = float(np.mean(np.diff(tree.offsets)))
+    f_gp = (npts_mean * F_GP_POINT + GP_SEG * F_GP_SEG) if tree.gp else 0.0
     like_parts = {k: round(float(np.mean([p[k] for p in like_parts])), 1) for k in like_parts[0]}
     res = {
         "config": args.config, "pairs_counted": int(len(R)), "walkers": int(args.walkers), "E": E,
@@ -158,8 +167,8 @@ def main():
         # (GP trees: the k_lnlike event span also holds k_gp_like, one Kalman
         # step per point)
         "per_kernel": {"k_setup": round(f_setup, 1), "k_elements": round(f_geom_total + 2 * f_setup, 1),
-                       "k_lnlike": round(f_like + (npts_mean * F_GP_STEP if tree.gp else 0.0), 1)},
-        "F_executed_per_pair": round(2 * f_setup + f_geom_total + f_like + (npts_mean * F_GP_STEP if tree.gp else 0.0), 1),
+                       "k_lnlike": round(f_like + f_gp, 1)},
+        "F_executed_per_pair": round(2 * f_setup + f_geom_total + f_like + f_gp, 1),
         "F_direct_form_equivalent_per_pair": round(f_setup + f_geom_total + f_acc_total, 1),
         "F_total_per_pair": round(f_setup + f_geom_total + f_acc_total, 1),
         "transcendentals_per_pair": round(m[1] + m[3] + m[10] + m[11] + m[12] + m[13] + m[5] / E, 1),

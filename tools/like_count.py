@@ -70,10 +70,10 @@ C_TAB_PT0 = 2       # a0 = x - phi0, hp = w / S
 C_TAB_SUB = 5       # a sub-bin centre: (2j + 1) hp, a0 - wp, +, wrap (2)
 C_TAB_DON = 3       # lane_breakpoints' arc (lo, hi, 0.5 - hw of mirrored tiles) x 2 calls + donor_q (3)
 C_TCELL = 2         # tcell: (x - t0) ginv
-C_SUBPT = 1         # h = wk / S
-C_SUBJ = 5 + 2 + 2 + 7 + 9 + 3 + 2   # centre (5), window lo / hi (2), e0 e1 (2), D (7), beam (9), sums (5)
+C_SUBPT = 1 + 4     # h = wk / S; the point's sums: / bden (1), x FX_INV VN[3] / VN[2] (3)
+C_SUBJ = 5 + 2 + 2 + 6 + 8 + 3       # centre (5), window lo / hi (2), e0 e1 (2), D (3 fma), beam (8), sbs (3)
 C_FRESH = 2 + 6     # a fresh lookup: tcell (2) + sincospi2 (2 muls + 4)
-C_STEP = 4 + 6      # a carried sub-bin: two tcell (4) + the rotation (6)
+C_STEP = 6          # a carried sub-bin: the cursor's compare (0) + the rotation (6)
 C_DQ = 3            # donor_q of a counted entry
 C_SPOT_IN = 4 + 5   # the sub-bin window inside the spot hull: two tcell (4), E (5)
 C_SPOT_C = 2        # a covering-weight entry: to_fx(sbw itb)
