@@ -1468,6 +1468,11 @@ __device__ __forceinline__ double wave_ext(double v)
     const int hi = __builtin_amdgcn_readlane(static_cast<int>(t >> 32), 63);
     return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
 }
+// OR of the low four bits of v over the wave (four ballots)
+__device__ __forceinline__ int wave_or4(int v)
+{
+    return (__ballot(v & 1) ? 1 : 0) | (__ballot(v & 2) ? 2 : 0) | (__ballot(v & 4) ? 4 : 0) | (__ballot(v & 8) ? 8 : 0);
+}
 __device__ __forceinline__ double wave_min(double v) { return wave_ext<false>(v); }
 __device__ __forceinline__ double wave_max(double v) { return wave_ext<true>(v); }
 
@@ -2122,22 +2127,27 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
         }
         if (tid == 0)
             for (int i = 0; i < (TAB ? 2 : 6); ++i) sacc[i][nt] = 0ull;
-        // does this point's window reach the WD/disc hull?  (any does: the tile sweeps)
-        if (own && (!hull || (wk >= 0.0 && !(phc + wk < shull[0] || phc - wk > shull[1])))) flA |= 8;
+        // does this point's window reach the WD/disc hull?  (any does: the tile
+        // sweeps; one tile and no sub-bins: always)
+        if (hull && own && wk >= 0.0 && !(phc + wk < shull[0] || phc - wk > shull[1])) flA |= 8;
         __syncthreads();
         flA |= check_sorted(TA, tid, own);
-        if (flA) atomicOr(&sflag[0], flA);
+        // the flags OR-ed over the wave first: one LDS atomic per wave
+        // (a same-address atomic per point serialised the hull bit)
+        const int wfA = wave_or4(flA);
+        if (lane == 0 && wfA) atomicOr(&sflag[0], wfA);
         build_cells(TA.lo, m, TA.cell, tid);
         if (!TAB) {
             const int flB = (flA & 7) | ((own && tid && sph[tid] < sph[tid - 1]) ? 4 : 0);
-            if (flB) atomicOr(&sflag[1], flB);
+            const int wfB = wave_or4(flB);
+            if (lane == 0 && wfB) atomicOr(&sflag[1], wfB);
             build_cells(sph, m, scp, tid);
         }
         __syncthreads();
         // any unsorted / mixed window (or invalid width) of the tile: the
         // pass goes point-major (every element against each point)
         const bool dir = (sflag[0] & 7) != 0 || (!TAB && sflag[1] != 0);
-        const bool wdd = (sflag[0] & 8) != 0;  // the WD/disc elements touch the tile
+        const bool wdd = !hull || (sflag[0] & 8) != 0;  // the WD/disc elements touch the tile
         LIKE_STAMP(1);
         double eb = 0.0, R3 = 0.0, R4 = 0.0, R5 = 0.0;
         if (dir) {
