@@ -34,12 +34,14 @@ class CpuPort:
         f.restype = ctypes.c_int
         f.argtypes = [_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _ip, _ip, _dp, _ip, _dp, _dp, _dp, _dp,
                       ctypes.c_int, _ip, _dp, _dp, _dp, ctypes.c_int, _dp, ctypes.c_int]
+        g = self.lib.lfc_lnprob_batch_gp
+        g.restype = ctypes.c_int
+        g.argtypes = [_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _ip, _ip, _dp, _ip, _dp, _dp, _dp, _dp,
+                      ctypes.c_int, _ip, _dp, _dp, _dp, ctypes.c_int, _ip, _dp, _ip, _dp, ctypes.c_int]
 
     def lnprob_batch(self, walkers, tree, nthreads=0):
-        """ln_prob of walkers [W, ndim] of a compiled chi^2 tree
-        (lfit_python_amd.batch.CompiledTree)."""
-        if getattr(tree, "gp", False):
-            raise ValueError("the CPU port runs chi^2 trees only")
+        """ln_prob of walkers [W, ndim] of a compiled tree
+        (lfit_python_amd.batch.CompiledTree), chi^2 or GP."""
         keep = []
 
         def F(a):
@@ -54,11 +56,14 @@ class CpuPort:
         w = np.ascontiguousarray(walkers, dtype=np.float64)
         W, ndim = w.shape
         lnp = np.empty(W)
-        used = self.lib.lfc_lnprob_batch(
+        gp = bool(getattr(tree, "gp", False))
+        used = self.lib.lfc_lnprob_batch_gp(
             F(w), W, ndim, tree.E, I(tree.gather.reshape(-1)), I(tree.npars),
             F(tree.consts if len(tree.consts) else np.zeros(1)), I(tree.offsets), F(tree.x), F(tree.y), F(tree.ye),
             F(tree.w), int(tree.nsub), I(tree.prior_type), F(tree.prior_p1), F(tree.prior_p2), F(tree.prior_norm),
-            int(tree.roche_priors), lnp.ctypes.data_as(_dp), int(nthreads))
+            int(tree.roche_priors), I(tree.gp_gather.reshape(-1)) if gp else None,
+            F(tree.gp_base.reshape(-1)) if gp else None, I(tree.gp_ecl.reshape(-1)) if gp else None,
+            lnp.ctypes.data_as(_dp), int(nthreads))
         if getattr(tree, "fixed_invalid", False):
             lnp[:] = -np.inf
         return lnp, used

@@ -34,6 +34,7 @@ struct Pair {
     Roche R;
     double s, c, rwd_a, rdisc_a, reff, rcal, ulimb, dexp, L, upk, umax, lnpk, exp1, exp2;
     double bsx, bsy, caz, saz, nb0, nb1, nb2, bden, fis, phi0, wdf, df, sf, rsf;
+    double inc;  // degrees (findi)
 };
 
 int wd_ring_of(int u)
@@ -117,6 +118,7 @@ int setup_pair(const double* pin, int np, Pair& G, double& rprior)
     const double sce = G.s * std::cos(PI * p[5]);
     G.rcal = std::sqrt(1.0 - sce * sce);
     G.wdf = p[0]; G.df = p[1]; G.sf = p[2]; G.rsf = p[3];
+    G.inc = inc;
     return ST_OK;
 }
 
@@ -251,7 +253,7 @@ void sweep_points(const double* ph, int m, double x1, double x2, const double* v
 
 // chi^2 of one pair against its light curve (k_lnlike restated on the host)
 double chisq(const Pair& G, const Tables& T, const double* x, const double* w, const double* y, const double* ye, int n,
-             int S, std::vector<double>& buf)
+             int S, std::vector<double>& buf, double* fout = nullptr)
 {
     // point windows, and the sub-bin windows / centres (flattened, sorted when
     // the windows are)
@@ -361,11 +363,66 @@ double chisq(const Pair& G, const Tables& T, const double* x, const double* w, c
             srs += D / T.dnorm;
         }
         const double f = G.wdf * (1.0 - fw[p]) + G.df * (1.0 - fd[p]) + G.sf * sbs / S + G.rsf * srs / S;
+        if (fout) {  // GP trees: the model flux, the residuals are the caller's
+            fout[p] = f;
+            continue;
+        }
         if (std::isnan(f)) return INFINITY;
         const double r = (y[p] - f) / ye[p];
         chi += r * r;
     }
     return chi;
+}
+
+// SimpleGPEclipse.calcChangepoints when the cache rule trips (k_gp_dcp):
+// dist_cp = (dphi + phi4 - phi3) / 2, phi3 / phi4 the extreme egress phases
+// of ten limb points of a sphere of radius rwd (units of x_L1, as the
+// reference passes it) at the WD-centre egress phase; NaN when none is
+// eclipsed or a solve fails
+double gp_dcp(const Pair& G, double dphi, double rwd)
+{
+    const Roche& R = G.R;
+    double dphi_c;
+    if (!(rwd > 0.0) || findphi_fast(R, G.inc, dphi_c) != ST_OK) return NAN;
+    const double sth = std::sin(PI * dphi_c), cth = std::cos(PI * dphi_c);
+    double lo = INFINITY, hi = -INFINITY;
+    for (int k = 0; k < 10; ++k) {
+        const double sp = std::sin(TWO_PI * k / 10), cp = std::cos(TWO_PI * k / 10);
+        double a, b;
+        if (element_interval(R, rwd * (cp * sth - sp * G.c * cth), rwd * (cp * cth + sp * G.c * sth), rwd * (sp * G.s),
+                             G.s, G.c, eggleton(R.q), a, b)) {
+            lo = std::fmin(lo, b);
+            hi = std::fmax(hi, b);
+        }
+    }
+    return lo <= hi ? (dphi + (hi - lo)) / 2.0 : NAN;
+}
+
+// the GP ln_like of one pair (SimpleGPEclipse.ln_like, CVModel.py:650-696)
+double gp_lnlike(const Pair& G, const Tables& T, const double* v, const double* consts, const double* pin, int e,
+                 const int* gp_gather, const double* gp_base, const int* gp_ecl, const double* x, const double* w,
+                 const double* y, const double* ye, int n, int S, std::vector<double>& buf, std::vector<double>& res)
+{
+    auto par = [&](int g) { return g >= 0 ? v[g] : consts[-1 - g]; };
+    const int* gg = gp_gather + 3 * e;
+    const double ain = std::exp(par(gg[0])), aout = std::exp(par(gg[1])), tau = std::exp(par(gg[2]));
+    if (!(tau > 0.0 && std::isfinite(ain) && std::isfinite(aout))) return -INFINITY;
+    const double* B = gp_base + 4 * e;
+    const double q = G.R.q, dphi = pin[5], rwd = pin[8];
+    const bool pend = std::fabs(B[1] - dphi) / dphi > 1.2 || std::fabs(B[0] - q) / q > 1.2 ||
+                      std::fabs(B[2] - rwd) / rwd > 1.2;
+    const double dcp = pend ? gp_dcp(G, dphi, rwd) : B[3];
+    if (!std::isfinite(dcp)) return -INFINITY;
+    res.resize(n > 0 ? n : 1);
+    chisq(G, T, x, w, y, ye, n, S, buf, res.data());
+    GPFilter F;
+    F.init(ain, aout, tau);
+    for (int p = 0; p < n; ++p) {
+        const double r = y[p] - res[p];
+        if (!std::isfinite(r)) return -INFINITY;
+        F.step(x[p], ye[p], r, gp_block(x[p], gp_ecl[2 * e], gp_ecl[2 * e + 1], dcp, G.phi0));
+    }
+    return F.lnlike();
 }
 
 }  // namespace
@@ -374,19 +431,57 @@ extern "C" {
 
 // ln_prob of W walkers of a compiled chi^2 tree (the oracle's
 // lfo_lnprob_batch arguments); returns the threads used
+int lfc_lnprob_batch_gp(const double* walkers, int W, int ndim, int E, const int* gather, const int* npars,
+                        const double* consts, const int* off, const double* x, const double* y, const double* ye,
+                        const double* w, int nsub, const int* prior_type, const double* prior_p1,
+                        const double* prior_p2, const double* prior_norm, int roche_priors, const int* gp_gather,
+                        const double* gp_base, const int* gp_ecl, double* lnp, int nthreads);
+
 int lfc_lnprob_batch(const double* walkers, int W, int ndim, int E, const int* gather, const int* npars,
                      const double* consts, const int* off, const double* x, const double* y, const double* ye,
                      const double* w, int nsub, const int* prior_type, const double* prior_p1, const double* prior_p2,
                      const double* prior_norm, int roche_priors, double* lnp, int nthreads)
 {
+    return lfc_lnprob_batch_gp(walkers, W, ndim, E, gather, npars, consts, off, x, y, ye, w, nsub, prior_type,
+                               prior_p1, prior_p2, prior_norm, roche_priors, nullptr, nullptr, nullptr, lnp, nthreads);
+}
+
+// the same with a GP likelihood per eclipse (gp_gather [E][3]: ln_ampin,
+// ln_ampout, ln_tau; gp_base [E][4]: the changepoint cache q, dphi, rwd,
+// dist_cp; gp_ecl [E][2]: first and last eclipse number); all null: chi^2
+int lfc_lnprob_batch_gp(const double* walkers, int W, int ndim, int E, const int* gather, const int* npars,
+                        const double* consts, const int* off, const double* x, const double* y, const double* ye,
+                        const double* w, int nsub, const int* prior_type, const double* prior_p1,
+                        const double* prior_p2, const double* prior_norm, int roche_priors, const int* gp_gather,
+                        const double* gp_base, const int* gp_ecl, double* lnp, int nthreads)
+{
     if (nthreads <= 0) nthreads = omp_get_max_threads();
+    // a changepoint cache the host never filled (dist_cp NaN): findi +
+    // wdphases at the cache's q, dphi, rwd (as the evaluator does)
+    std::vector<double> base;
+    if (gp_gather) {
+        base.assign(gp_base, gp_base + 4 * E);
+        for (int e = 0; e < E; ++e) {
+            double* B = &base[4 * e];
+            if (std::isfinite(B[3])) continue;
+            Pair G{};
+            double inc;
+            if (roche_init(G.R, B[0]) != ST_OK || findi_fast(G.R, B[1], inc) != ST_OK) continue;
+            G.inc = inc;
+            G.s = std::sin(inc * DEG);
+            G.c = std::cos(inc * DEG);
+            B[3] = gp_dcp(G, B[1], B[2]);
+        }
+        gp_base = base.data();
+    }
     int used = 1;
 #pragma omp parallel num_threads(nthreads)
     {
 #pragma omp single
         used = omp_get_num_threads();
-        std::vector<double> buf;
+        std::vector<double> buf, res;
         std::vector<Pair> pairs(E);
+        std::vector<double> pins(size_t(18) * E);
         std::vector<int> status(E);
         Tables* T = new Tables;
 #pragma omp for schedule(dynamic, 1)
@@ -405,6 +500,7 @@ int lfc_lnprob_batch(const double* walkers, int W, int ndim, int E, const int* g
             double pin[18];
             for (int e = 0; e < E && lp > -INFINITY; ++e) {
                 for (int k = 0; k < npars[e]; ++k) pin[k] = par(gather[e * 18 + k]);
+                std::copy(pin, pin + 18, pins.begin() + 18 * e);
                 double rp;
                 status[e] = setup_pair(pin, npars[e], pairs[e], rp);
                 if (roche_priors) lp += rp;
@@ -413,8 +509,13 @@ int lfc_lnprob_batch(const double* walkers, int W, int ndim, int E, const int* g
             for (int e = 0; e < E && lp > -INFINITY; ++e) {
                 if (status[e] != ST_OK) { ll = -INFINITY; break; }
                 elements(pairs[e], *T);
-                ll += -0.5 * chisq(pairs[e], *T, x + off[e], w ? w + off[e] : nullptr, y + off[e], ye + off[e],
-                                   off[e + 1] - off[e], nsub, buf);
+                const int n = off[e + 1] - off[e];
+                if (gp_gather)
+                    ll += gp_lnlike(pairs[e], *T, v, consts, &pins[18 * e], e, gp_gather, gp_base, gp_ecl, x + off[e],
+                                    w ? w + off[e] : nullptr, y + off[e], ye + off[e], n, nsub, buf, res);
+                else
+                    ll += -0.5 * chisq(pairs[e], *T, x + off[e], w ? w + off[e] : nullptr, y + off[e], ye + off[e], n,
+                                       nsub, buf);
             }
             lnp[iw] = lp > -INFINITY ? lp + ll : -INFINITY;
         }
