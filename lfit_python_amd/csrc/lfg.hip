@@ -67,9 +67,6 @@ __device__ __forceinline__ double2 sweep_ab(const double2* __restrict__ AB, int 
 constexpr int DON_STRIDE = 5;
 
 
-__device__ const int kIdentityGather[18] = {0, 1, 2, 3, 4, 5, 6, 7, 8,
-                                            9, 10, 11, 12, 13, 14, 15, 16, 17};
-
 struct Ws {
     double* geo;
     int* status;
@@ -214,6 +211,15 @@ __device__ inline Prop make_prop(const SetupArgs& A, int w)
 // CV parameter count of eclipse e.  P is pinned to a register first: written
 // as `npars ? npars[e] : P` the compiler selected between the two ADDRESSES
 // and, to give the kernel argument P one, copied it into scratch
+// column of eclipse parameter k of (walker-eclipse) gather row r: the tree's
+// gather map, or the identity (lfg_flux / lfg_lnprob without a tree).  A
+// branch, not a pointer select: a select between the kernel argument and the
+// constant identity table made every read a flat load
+__device__ __forceinline__ int gat_at(const SetupArgs& A, int i)
+{
+    return A.gather ? A.gather[i] : i % 18;
+}
+
 __device__ __forceinline__ int npars_of(const SetupArgs& A, int e)
 {
     int P = A.P;
@@ -255,15 +261,14 @@ __device__ unsigned long long g_setup_cyc[11][4096];
 __device__ inline void bspot_lane(const SetupArgs& A, int t)
 {
     LFG_T0(tl);
-    const int* gat = A.gather ? A.gather : kIdentityGather;
     const int w = t / A.E, e = t - w * A.E;
     const Prop P = make_prop(A, w);
     const int np = npars_of(A, e);
-    const double q = gather_par(A, P, gat[e * 18 + 4]);
-    const double rdisc = gather_par(A, P, gat[e * 18 + 6]);
-    const double az = gather_par(A, P, gat[e * 18 + 10]);
-    const double a1 = (np == 18) ? gather_par(A, P, gat[e * 18 + 14]) : 2.0;  // MODEL_SPEC 5.3 simple: 2, 1
-    const double a2 = (np == 18) ? gather_par(A, P, gat[e * 18 + 15]) : 1.0;
+    const double q = gather_par(A, P, gat_at(A, e * 18 + 4));
+    const double rdisc = gather_par(A, P, gat_at(A, e * 18 + 6));
+    const double az = gather_par(A, P, gat_at(A, e * 18 + 10));
+    const double a1 = (np == 18) ? gather_par(A, P, gat_at(A, e * 18 + 14)) : 2.0;  // MODEL_SPEC 5.3 simple: 2, 1
+    const double a2 = (np == 18) ? gather_par(A, P, gat_at(A, e * 18 + 15)) : 1.0;
     double* G = A.geo + size_t(t) * LFG_NGEO;
 #ifdef LFG_PROFILE_SETUP
     unsigned long long tb = tl;
@@ -311,14 +316,13 @@ __device__ inline void prior_lane(const SetupArgs& A, int w)
 #ifdef LFG_PROFILE_SETUP
     unsigned long long trl = __builtin_amdgcn_s_memrealtime(), tr = tl;  // 100 MHz: calibrates s_memtime
 #endif
-    const int* gat = A.gather ? A.gather : kIdentityGather;
     const Prop P = make_prop(A, w);
     double lp = 0.0;
     if (A.roche_priors) {
         // LCModel.ln_prior: dphi <= findphi(q, 90) - 1e-6, findphi from the
         // q series of the stream table (~1e-16; the solver outside its range)
-        const double q = gather_par(A, P, gat[4]);
-        const double dphi = gather_par(A, P, gat[5]);
+        const double q = gather_par(A, P, gat_at(A, 4));
+        const double dphi = gather_par(A, P, gat_at(A, 5));
         const QPatch qp = q_patch(q);
         double maxphi;
         if (qp.iq >= 0) {
@@ -408,7 +412,6 @@ __device__ __forceinline__ void setup_any(const SetupArgs& A, int t)
 
     // setup lane: one per (walker, eclipse)
     LFG_T0(tl);
-    const int* gat = A.gather ? A.gather : kIdentityGather;
     const int w = t / A.E, e = t - (t / A.E) * A.E;
     const Prop P = make_prop(A, w);
     const int np = npars_of(A, e);
@@ -416,7 +419,7 @@ __device__ __forceinline__ void setup_any(const SetupArgs& A, int t)
     bool finite = (np == 14 || np == 18);
 #pragma unroll  // p[] stays in registers (a rolled loop kept it in scratch)
     for (int k = 0; k < 18; ++k) {
-        p[k] = (k < np) ? gather_par(A, P, gat[e * 18 + k]) : 0.0;
+        p[k] = (k < np) ? gather_par(A, P, gat_at(A, e * 18 + k)) : 0.0;
         finite = finite && isfinite(p[k]);
     }
     if (np == 14) { p[14] = 2.0; p[15] = 1.0; p[16] = 90.0; p[17] = 0.0; }  // MODEL_SPEC 5.3
@@ -1624,8 +1627,11 @@ __device__ __forceinline__ double2 sub_point(const SubTables& T, const SubEntrie
 {
     // the pair's constants are read from LDS at each use (volatile: held in
     // registers over the loop they pushed k_lnlike past its budget)
-    const volatile double* VG = SG;
-    const volatile double* VN = snorm;
+    // (LDS address space spelled out: through volatile generic pointers the
+    // reads were flat loads, which wait on the vector-memory counter too)
+    using lds_cvd = const volatile __attribute__((address_space(3))) double*;
+    const lds_cvd VG = (lds_cvd)SG;
+    const lds_cvd VN = (lds_cvd)snorm;
     const int nd = T.dend[TCELLS - 1];
     const double h = wk / S;
     double sbs = 0.0, srs = 0.0, ph = 0.0, sn = 0.0, cs = 1.0, rs = 0.0, rc = 1.0;
