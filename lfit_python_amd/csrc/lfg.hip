@@ -880,9 +880,17 @@ __global__ void k_expand(const double* __restrict__ geo, const int* __restrict__
 template <int CTRL, int RM>
 __device__ __forceinline__ long long dpp64(long long v)
 {
-    const int lo = __builtin_amdgcn_update_dpp(0, static_cast<int>(v), CTRL, RM, 0xf, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, static_cast<int>(v >> 32), CTRL, RM, 0xf, false);
-    return (static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo);
+    if constexpr (RM == 0xf) {
+        // every row enabled: bound_ctrl writes the 0 itself where the source
+        // lane is outside the row (no v_mov of an "old" 0 per move)
+        const int lo = __builtin_amdgcn_mov_dpp(static_cast<int>(v), CTRL, 0xf, 0xf, true);
+        const int hi = __builtin_amdgcn_mov_dpp(static_cast<int>(v >> 32), CTRL, 0xf, 0xf, true);
+        return (static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo);
+    } else {  // disabled rows keep the old value: 0
+        const int lo = __builtin_amdgcn_update_dpp(0, static_cast<int>(v), CTRL, RM, 0xf, false);
+        const int hi = __builtin_amdgcn_update_dpp(0, static_cast<int>(v >> 32), CTRL, RM, 0xf, false);
+        return (static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo);
+    }
 }
 
 template <int CTRL, int RM>
@@ -1530,6 +1538,22 @@ __device__ __forceinline__ double sub_spot(const SubTables& T, const double2* sa
     return pt ? e : fma(corr, 1.0 / (hi - lo), e);
 }
 
+// covering weight C(lo) of the spot (fixed point) from the cell table, and
+// the cursor: the first entry (cells sorted by position) past lo
+__device__ __forceinline__ long long spot_C(const SubTables& T, const double* sbw, double itb, double lo, int& cur)
+{
+    const int g = tcell(lo, T.st0, T.sginv);
+    long long C = T.spre[g];
+    int i = g ? T.send[g - 1] : 0;
+    for (const int ie = T.send[g]; i < ie && T.spos[i] <= lo; ++i) {
+        const int code = T.scode[i];
+        const long long W = to_fx(sbw[code >> 1] * itb);
+        C += (code & 1) ? -W : W;
+    }
+    cur = i;
+    return C;
+}
+
 // donor entries sorted (after step (e) of the table build) by position,
 // an end before a start at equal positions: the entries counted at phase th
 // (starts with pos < th, ends with pos <= th) are then a prefix of the list,
@@ -1632,16 +1656,18 @@ __device__ __forceinline__ double2 sub_point(const SubTables& T, const SubEntrie
     using lds_cvd = const volatile __attribute__((address_space(3))) double*;
     const lds_cvd VG = (lds_cvd)SG;
     const lds_cvd VN = (lds_cvd)snorm;
-    const int nd = T.dend[TCELLS - 1];
-    const double h = wk / S;
+    const int nd = T.dend[TCELLS - 1], nsp = T.send[TCELLS - 1];
+    const double h = wk / S, ih = 0.5 / h;
     double sbs = 0.0, srs = 0.0, ph = 0.0, sn = 0.0, cs = 1.0, rs = 0.0, rc = 1.0;
     double fx = 0.0, fy = 0.0, fz = 0.0, npos = INFINITY;
-    long long vx = 0, vy = 0, vz = 0;
-    int cur = 0, ncode = 0;
+    long long vx = 0, vy = 0, vz = 0, Cs = 0;
+    int cur = 0, ncode = 0, scur = 0;
+    bool sv = false;  // Cs / scur hold C at this sub-bin's lo
     for (int j = 0; j < S; ++j) {
         const double phn = wrap_phase(ph0 - wk + (2 * j + 1) * h);
         bool chg = false;
         if (j == 0 || !(phn >= ph)) {  // a fresh lookup
+            sv = false;
             cur = sub_donor(T, D, sdq, VN[1], phn, vx, vy, vz);
             chg = true;
             const double4 e4 = sincospi2_ool(2.0 * phn, 4.0 * h);  // the turn per sub-bin: 2 pi (2 h)
@@ -1671,7 +1697,37 @@ __device__ __forceinline__ double2 sub_point(const SubTables& T, const SubEntrie
             fz = double(vz);
         }
         ph = phn;
-        const double ebj = sub_spot(T, sab, sbw, VN[0], ph - h, ph + h, shull[2], shull[3]);
+        // spot: windows of a point abut, so C(lo) is carried from window to
+        // window by a cursor over the position-sorted entries (the entries
+        // inside a window give its partial overlaps); zero widths: points
+        double ebj = 0.0;
+        const double lo = ph - h, hi = ph + h;
+        if (!(h > 0.0)) {
+            ebj = sub_spot(T, sab, sbw, VN[0], lo, hi, shull[2], shull[3]);
+        } else if (hi > shull[2] && lo < shull[3]) {
+            const double itb = VN[0];
+            if (!sv) Cs = spot_C(T, sbw, itb, lo, scur);
+            sv = true;
+            long long Cn = Cs;
+            double corr = 0.0;
+            for (; scur < nsp && T.spos[scur] <= hi; ++scur) {
+                const int code = T.scode[scur], k = code >> 1;
+                const double wn = sbw[k] * itb;
+                const double2 ab = sab[k];
+                const long long W = to_fx(wn);
+                if (!(code & 1)) {
+                    Cn += W;
+                    corr = fma(wn, fmin(ab.y, hi) - ab.x, corr);
+                } else {
+                    Cn -= W;
+                    if (ab.x <= lo) corr = fma(-wn, hi - ab.y, corr);
+                }
+            }
+            ebj = fma(corr, ih, double(Cs) * FX_INV);
+            Cs = Cn;
+        } else {
+            sv = false;
+        }
         const double sg = VG[G_S], cg = VG[G_C];
         const double e0 = sg * cs, e1 = -sg * sn;
         srs = fma(e0, fx, fma(e1, fy, fma(cg, fz, srs)));
@@ -2081,7 +2137,8 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
         }
         __syncthreads();
         // (e) each cell's donor entries in order (sub_point's cursor): position,
-        // an end before a start at equal positions; a few entries per cell
+        // an end before a start at equal positions; a few entries per cell.
+        // The spot's entries by position too
         if (tid < TCELLS) {
             const int i0 = tid ? T.dend[tid - 1] : 0, i1 = T.dend[tid];
             for (int i = i0 + 1; i < i1; ++i) {
@@ -2097,6 +2154,19 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
                 }
                 DE.dpos[k] = p;
                 DE.dcode[k] = c;
+            }
+            // the spot's entries of the cell by position (sub_point's spot cursor)
+            const int j0 = tid ? T.send[tid - 1] : 0, j1 = T.send[tid];
+            for (int i = j0 + 1; i < j1; ++i) {
+                const double p = T.spos[i];
+                const int c = T.scode[i];
+                int k = i;
+                for (; k > j0 && T.spos[k - 1] > p; --k) {
+                    T.spos[k] = T.spos[k - 1];
+                    T.scode[k] = T.scode[k - 1];
+                }
+                T.spos[k] = p;
+                T.scode[k] = c;
             }
         }
         __syncthreads();
@@ -2358,10 +2428,11 @@ constexpr int GP_EL = 16;                     // doubles of a lane's element row
 template <int PERM>
 __device__ __forceinline__ double quad_perm(double v)
 {
+    // every lane of a quad is a valid source: no "old" value (update_dpp's
+    // copy of it cost a v_mov per permute)
     const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_update_dpp(static_cast<int>(b), static_cast<int>(b), PERM, 0xf, 0xf, false);
-    const int hi = __builtin_amdgcn_update_dpp(static_cast<int>(b >> 32), static_cast<int>(b >> 32), PERM, 0xf, 0xf,
-                                               false);
+    const int lo = __builtin_amdgcn_mov_dpp(static_cast<int>(b), PERM, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_mov_dpp(static_cast<int>(b >> 32), PERM, 0xf, 0xf, false);
     return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
 }
 constexpr int QP_NEXT = 0xF5;  // [1, 1, 3, 3]: the odd row of each block
@@ -2374,37 +2445,6 @@ __device__ __forceinline__ double gp_pinf(int i, int j, double ain, double aout,
     const double a = (i >> 1) ? aout : ain;
     const int k = (i & 1) + (j & 1);
     return k == 0 ? a : (k == 1 ? a * lam : 2.0 * a * lam * lam);
-}
-
-// inverse of a 4x4 by its adjugate (2x2 minors of the top and bottom row
-// pairs); returns the determinant
-__device__ __forceinline__ double inv4(const double (&m)[4][4], double (&o)[4][4])
-{
-    const double s0 = fma(m[0][0], m[1][1], -m[1][0] * m[0][1]), s1 = fma(m[0][0], m[1][2], -m[1][0] * m[0][2]);
-    const double s2 = fma(m[0][0], m[1][3], -m[1][0] * m[0][3]), s3 = fma(m[0][1], m[1][2], -m[1][1] * m[0][2]);
-    const double s4 = fma(m[0][1], m[1][3], -m[1][1] * m[0][3]), s5 = fma(m[0][2], m[1][3], -m[1][2] * m[0][3]);
-    const double c5 = fma(m[2][2], m[3][3], -m[3][2] * m[2][3]), c4 = fma(m[2][1], m[3][3], -m[3][1] * m[2][3]);
-    const double c3 = fma(m[2][1], m[3][2], -m[3][1] * m[2][2]), c2 = fma(m[2][0], m[3][3], -m[3][0] * m[2][3]);
-    const double c1 = fma(m[2][0], m[3][2], -m[3][0] * m[2][2]), c0 = fma(m[2][0], m[3][1], -m[3][0] * m[2][1]);
-    const double det = (fma(s0, c5, -s1 * c4) + fma(s2, c3, s3 * c2)) + fma(s5, c0, -s4 * c1);
-    const double id = 1.0 / det;
-    o[0][0] = id * fma(m[1][1], c5, fma(-m[1][2], c4, m[1][3] * c3));
-    o[0][1] = id * fma(-m[0][1], c5, fma(m[0][2], c4, -m[0][3] * c3));
-    o[0][2] = id * fma(m[3][1], s5, fma(-m[3][2], s4, m[3][3] * s3));
-    o[0][3] = id * fma(-m[2][1], s5, fma(m[2][2], s4, -m[2][3] * s3));
-    o[1][0] = id * fma(-m[1][0], c5, fma(m[1][2], c2, -m[1][3] * c1));
-    o[1][1] = id * fma(m[0][0], c5, fma(-m[0][2], c2, m[0][3] * c1));
-    o[1][2] = id * fma(-m[3][0], s5, fma(m[3][2], s2, -m[3][3] * s1));
-    o[1][3] = id * fma(m[2][0], s5, fma(-m[2][2], s2, m[2][3] * s1));
-    o[2][0] = id * fma(m[1][0], c4, fma(-m[1][1], c2, m[1][3] * c0));
-    o[2][1] = id * fma(-m[0][0], c4, fma(m[0][1], c2, -m[0][3] * c0));
-    o[2][2] = id * fma(m[3][0], s4, fma(-m[3][1], s2, m[3][3] * s0));
-    o[2][3] = id * fma(-m[2][0], s4, fma(m[2][1], s2, -m[2][3] * s0));
-    o[3][0] = id * fma(-m[1][0], c3, fma(m[1][1], c1, -m[1][2] * c0));
-    o[3][1] = id * fma(m[0][0], c3, fma(-m[0][1], c1, m[0][2] * c0));
-    o[3][2] = id * fma(-m[3][0], s3, fma(m[3][1], s1, -m[3][2] * s0));
-    o[3][3] = id * fma(m[2][0], s3, fma(-m[2][1], s1, m[2][2] * s0));
-    return det;
 }
 
 __global__ __launch_bounds__(GP_BLOCK) __attribute__((amdgpu_waves_per_eu(2))) void k_gp_like(LikeArgs L)
@@ -2544,135 +2584,139 @@ __global__ __launch_bounds__(GP_BLOCK) __attribute__((amdgpu_waves_per_eu(2))) v
         o[15] = bad ? 1.0 : 0.0;
     }
     __syncthreads();
-    if (!live || (lane % GP_LPP) != 0) return;
+    // ---- combine: serial over the segments, the 4x4 algebra spread over 16
+    // lanes of the pair (lane (ci, cj) holds entry (ci, cj) of Sigma and of
+    // each product; rows / columns are exchanged through LDS; vectors are
+    // formed in every lane).  Every lane of the wave runs it (barriers):
+    // lanes 16..31 of a pair repeat 0..15 without writing, and pairs that
+    // are not evaluated compute on unset data and are discarded.
+    __shared__ double smat[GP_PAIRS][5][16];
+    double* const SGb = smat[pp][0];  // Sigma
+    double* const CBb = smat[pp][1];  // C = I + J Sigma
+    double* const CIb = smat[pp][2];  // C^-1
+    double* const SPb = smat[pp][3];  // Sigma_post
+    double* const ASb = smat[pp][4];  // A Sigma_post
+    const int q16 = lane % GP_LPP, e16 = q16 & 15, ci = e16 >> 2, cj = e16 & 3;
+    const bool wr = q16 < 16;
+    const double pij = gp_pinf(ci, cj, ain, aout, lam);
+    double sgm = pij;  // Sigma_{ci cj}: the stationary prior of the first point
+    double mu[4] = {0.0, 0.0, 0.0, 0.0};
+    double ll = 0.0;
+    bool bad = false;
+    for (int s = 0; s < GP_SEG; ++s) {
+        const int i0 = (n * s) / GP_SEG, i1 = (n * (s + 1)) / GP_SEG;
+        if (i1 <= i0) continue;  // an empty segment: nothing observed, no transition (n is the wave's)
+        const double* El = &sel[pp][s][0][0];
+        bad = bad || El[15] != 0.0 || El[GP_EL + 15] != 0.0;
+        if (s > 0 && i0 > 0) {  // the gap from the previous segment's last point
+            const double d = xs[i0] - xs[i0 - 1], ex = gx[i0], E = ex * ex;
+            const int b1 = gb[i0];
+            const bool fresh = b1 >= 0 && b1 != gb[i0 - 1];
+            mu[0] = ex * fma(d, mu[1], mu[0]);
+            mu[1] = ex * mu[1];
+            mu[2] = fresh ? 0.0 : ex * fma(d, mu[3], mu[2]);
+            mu[3] = fresh ? 0.0 : ex * mu[3];
+            // Sigma <- E T (Sigma - P_inf) T^T + P_inf, T = [[1, d], [0, 1]] per block
+            if (wr) SGb[e16] = sgm - pij;
+            __syncthreads();
+            const bool ei = (ci & 1) == 0, ej = (cj & 1) == 0;
+            const double t0 = SGb[e16] + (ei ? d * SGb[e16 + 4] : 0.0);
+            const double t1 = ej ? SGb[e16 + 1] + (ei ? d * SGb[e16 + 5] : 0.0) : 0.0;
+            const double sgx = fma(E, ej ? fma(d, t1, t0) : t0, pij);
+            sgm = (fresh && (ci >= 2 || cj >= 2)) ? pij : sgx;
+            __syncthreads();
+        }
+        // C = I + J Sigma
+        if (wr) SGb[e16] = sgm;
+        __syncthreads();
+        {
+            double v = (ci == cj) ? 1.0 : 0.0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v = fma(El[ci * GP_EL + 9 + k], SGb[k * 4 + cj], v);
+            if (wr) CBb[e16] = v;
+        }
+        __syncthreads();
+        // det C by 2x2 minors (every lane), C^-1_{ci cj} = cof_{cj ci} / det
+        // with the cofactor a 3x3 determinant of C less row cj, column ci
+        double det;
+        {
+            const double* m = CBb;
+            const double s0 = fma(m[0], m[5], -m[4] * m[1]), s1 = fma(m[0], m[6], -m[4] * m[2]);
+            const double s2 = fma(m[0], m[7], -m[4] * m[3]), s3 = fma(m[1], m[6], -m[5] * m[2]);
+            const double s4 = fma(m[1], m[7], -m[5] * m[3]), s5 = fma(m[2], m[7], -m[6] * m[3]);
+            const double c5 = fma(m[10], m[15], -m[14] * m[11]), c4 = fma(m[9], m[15], -m[13] * m[11]);
+            const double c3 = fma(m[9], m[14], -m[13] * m[10]), c2 = fma(m[8], m[15], -m[12] * m[11]);
+            const double c1 = fma(m[8], m[14], -m[12] * m[10]), c0 = fma(m[8], m[13], -m[12] * m[9]);
+            det = (fma(s0, c5, -s1 * c4) + fma(s2, c3, s3 * c2)) + fma(s5, c0, -s4 * c1);
+            const int r0 = cj == 0 ? 1 : 0, r1 = cj <= 1 ? 2 : 1, r2 = cj <= 2 ? 3 : 2;
+            const int k0 = ci == 0 ? 1 : 0, k1 = ci <= 1 ? 2 : 1, k2 = ci <= 2 ? 3 : 2;
+            const double a00 = m[r0 * 4 + k0], a01 = m[r0 * 4 + k1], a02 = m[r0 * 4 + k2];
+            const double a10 = m[r1 * 4 + k0], a11 = m[r1 * 4 + k1], a12 = m[r1 * 4 + k2];
+            const double a20 = m[r2 * 4 + k0], a21 = m[r2 * 4 + k1], a22 = m[r2 * 4 + k2];
+            const double d3 = a00 * fma(a11, a22, -a12 * a21) - a01 * fma(a10, a22, -a12 * a20) +
+                              a02 * fma(a10, a21, -a11 * a20);
+            const double cof = ((ci + cj) & 1) ? -d3 : d3;
+            if (wr) CIb[e16] = cof / det;
+        }
+        bad = bad || !(det > 0.0);
+        __syncthreads();
+        // Sigma_post = Sigma C^-1
+        {
+            double v = 0.0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v = fma(SGb[ci * 4 + k], CIb[k * 4 + cj], v);
+            if (wr) SPb[e16] = v;
+        }
+        __syncthreads();
+        // vectors (every lane): u = eta - J mu, Sigma_post u, the segment's ln_like
+        double u[4], emu = 0.0, mJm = 0.0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            double jm = 0.0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) jm = fma(El[i * GP_EL + 9 + k], mu[k], jm);
+            const double et = El[i * GP_EL + 13];
+            u[i] = et - jm;
+            emu = fma(et, mu[i], emu);
+            mJm = fma(mu[i], jm, mJm);
+        }
+        double uSu = 0.0, mp[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            double su = 0.0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) su = fma(SPb[i * 4 + k], u[k], su);
+            uSu = fma(u[i], su, uSu);
+            mp[i] = mu[i] + su;
+        }
+        ll += (emu - 0.5 * log(det)) + 0.5 * (uSu - mJm - El[14]);
+        // the filtered end state: A mp + c (every lane), A Sigma_post A^T + P_end
+        // (lane j of the element's quad wrote column j of A: A_ik = El[k][4 + i])
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            double v = El[i * GP_EL + 8];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v = fma(El[k * GP_EL + 4 + i], mp[k], v);
+            mu[i] = v;
+        }
+        {
+            double v = 0.0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v = fma(El[k * GP_EL + 4 + ci], SPb[k * 4 + cj], v);
+            if (wr) ASb[e16] = v;
+        }
+        __syncthreads();
+        {
+            double v = El[ci * GP_EL + cj] + pij;  // P_end = D_end + P_inf
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v = fma(ASb[ci * 4 + k], El[k * GP_EL + 4 + cj], v);
+            sgm = v;
+        }
+        __syncthreads();
+    }
+    if (!live || q16 != 0) return;
     double lle = -INFINITY;
     if (run) {
-        // ---- combine: serial over the segments, one lane
-        double mu[4] = {0.0, 0.0, 0.0, 0.0}, Sg[4][4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) Sg[i][j] = gp_pinf(i, j, ain, aout, lam);
-        double ll = 0.0;
-        bool bad = false;
-        for (int s = 0; s < GP_SEG; ++s) {
-            const int i0 = (n * s) / GP_SEG, i1 = (n * (s + 1)) / GP_SEG;
-            if (i1 <= i0) continue;  // an empty segment: nothing observed, no transition
-            const double* El = &sel[pp][s][0][0];
-            bad = bad || El[15] != 0.0 || El[GP_EL + 15] != 0.0;
-            if (s > 0 && i0 > 0) {  // the gap from the previous segment's last point
-                const double d = xs[i0] - xs[i0 - 1], ex = gx[i0], E = ex * ex;
-                const int b1 = gb[i0];
-                const bool fresh = b1 >= 0 && b1 != gb[i0 - 1];
-                mu[0] = ex * fma(d, mu[1], mu[0]);
-                mu[1] = ex * mu[1];
-                mu[2] = ex * fma(d, mu[3], mu[2]);
-                mu[3] = ex * mu[3];
-                double T[4][4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i)  // rows of T (Sigma - P_inf)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const double v = Sg[i][j] - gp_pinf(i, j, ain, aout, lam);
-                        const double vn = (i & 1) ? 0.0 : Sg[i + 1][j] - gp_pinf(i + 1, j, ain, aout, lam);
-                        T[i][j] = fma(d, vn, v);
-                    }
-#pragma unroll
-                for (int i = 0; i < 4; ++i)  // columns, scaling, + P_inf
-#pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        Sg[i][j] = fma(E, (j & 1) ? T[i][j] : fma(d, T[i][j + 1], T[i][j]), gp_pinf(i, j, ain, aout, lam));
-                if (fresh) {
-                    mu[2] = mu[3] = 0.0;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-#pragma unroll
-                        for (int j = 0; j < 4; ++j)
-                            if (i >= 2 || j >= 2) Sg[i][j] = gp_pinf(i, j, ain, aout, lam);
-                }
-            }
-            // the element's A, P_end, J, c, eta are read from LDS where they
-            // are used (held in registers they pushed the combine into spills)
-            auto EA = [&](int i, int j) { return El[j * GP_EL + 4 + i]; };  // lane j wrote column j of A
-            auto EJ = [&](int i, int j) { return El[i * GP_EL + 9 + j]; };
-            auto EP = [&](int i, int j) { return El[i * GP_EL + j] + gp_pinf(i, j, ain, aout, lam); };
-            auto Ec = [&](int i) { return El[i * GP_EL + 8]; };
-            auto Ee = [&](int i) { return El[i * GP_EL + 13]; };
-            const double kap = El[14];
-            // posterior of x_s: C = I + J Sigma (det C = det(I + Sigma J) > 0),
-            // Sigma_post = Sigma C^-1 = (Sigma^-1 + J)^-1; C^-1 by its
-            // adjugate (2x2 minors: a shallow dependent chain, one reciprocal)
-            double C[4][4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    double v = (i == j) ? 1.0 : 0.0;
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) v = fma(EJ(i, k), Sg[k][j], v);
-                    C[i][j] = v;
-                }
-            double Ci[4][4];
-            const double det = inv4(C, Ci);
-            bad = bad || !(det > 0.0);
-            const double logdet = 0.5 * log(det);  // 1/2 ln det(I + Sigma J)
-            double Sp[4][4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    double v = 0.0;
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) v = fma(Sg[i][k], Ci[k][j], v);
-                    Sp[i][j] = v;
-                }
-            double u[4], Jm[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                double v = 0.0;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) v = fma(EJ(i, k), mu[k], v);
-                Jm[i] = v;
-                u[i] = Ee(i) - v;
-            }
-            double emu = 0.0, mJm = 0.0, uSu = 0.0, mp[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                double su = 0.0;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) su = fma(Sp[i][k], u[k], su);
-                emu = fma(Ee(i), mu[i], emu);
-                mJm = fma(mu[i], Jm[i], mJm);
-                uSu = fma(u[i], su, uSu);
-                mp[i] = mu[i] + su;
-            }
-            ll += (emu - logdet) + 0.5 * (uSu - mJm - kap);
-            // the filtered end state: A mp + c, A Sigma_post A^T + P_end
-            double AS[4][4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                double v = Ec(i);
-#pragma unroll
-                for (int k = 0; k < 4; ++k) v = fma(EA(i, k), mp[k], v);
-                mu[i] = v;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    double t = 0.0;
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) t = fma(EA(i, k), Sp[k][j], t);
-                    AS[i][j] = t;
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    double t = EP(i, j);
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) t = fma(AS[i][k], EA(j, k), t);
-                    Sg[i][j] = t;
-                }
-        }
         const double v = ll - 0.5 * n * 1.8378770664093454836;  // log(2 pi)
         lle = (bad || !isfinite(v)) ? -INFINITY : v;
     }

@@ -70,14 +70,15 @@ C_TAB_PT0 = 2       # a0 = x - phi0, hp = w / S
 C_TAB_SUB = 5       # a sub-bin centre: (2j + 1) hp, a0 - wp, +, wrap (2)
 C_TAB_DON = 3       # lane_breakpoints' arc (lo, hi, 0.5 - hw of mirrored tiles) x 2 calls + donor_q (3)
 C_TCELL = 2         # tcell: (x - t0) ginv
-C_SUBPT = 1 + 4     # h = wk / S; the point's sums: / bden (1), x FX_INV VN[3] / VN[2] (3)
+C_SUBPT = 2 + 4     # h = wk / S, 1 / (2 h); the point's sums: / bden (1), x FX_INV VN[3] / VN[2] (3)
 C_SUBJ = 5 + 2 + 2 + 6 + 8 + 3       # centre (5), window lo / hi (2), e0 e1 (2), D (3 fma), beam (8), sbs (3)
 C_FRESH = 2 + 6     # a fresh lookup: tcell (2) + sincospi2 (2 muls + 4)
 C_STEP = 6          # a carried sub-bin: the cursor's compare (0) + the rotation (6)
 C_DQ = 3            # donor_q of a counted entry
-C_SPOT_IN = 4 + 5   # the sub-bin window inside the spot hull: two tcell (4), E (5)
-C_SPOT_C = 2        # a covering-weight entry: to_fx(sbw itb)
-C_SPOT_CORR = 4     # a partial-overlap entry: wn (1), overlap (1), fma (2)
+C_SPOT_IN = 3       # a sub-bin window inside the spot hull: E = C FX_INV + corr / (2 h) (fma)
+C_SPOT_INIT = 2     # the spot cursor's start: tcell (2) ...
+C_SPOT_C = 1        # ... and each counted entry of the cell: wn = sbw itb
+C_SPOT_CORR = 4     # an entry inside the window: wn (1), overlap (1), fma (2)
 
 
 def wrap(ph):
@@ -225,15 +226,19 @@ def _subbins(ph_all, hw_all, S, cen, hw, ssa, ssb, parts):
         u = (v - sa_min) * sginv
         return np.where(u <= 0, 0, np.where(u >= TCELLS - 1, TCELLS - 1, np.floor(u))).astype(int)
     scl = scell(spos) if len(spos) else np.zeros(0, int)
+    order = np.argsort(spos, kind="stable") if len(spos) else np.zeros(0, int)
+    spos_s = spos[order] if len(spos) else spos
     f = 0.0
     for p in range(n):
         f += C_SUBPT
         h = hw_all[p] / S
         prev = None
+        sv = False
         for j in range(S):
             th = cs[p, j]
             f += C_SUBJ
             if prev is None or not th >= prev:
+                sv = False
                 g = cell(np.array([th]))[0]
                 sel = bcell == g
                 cnt = int(np.sum(np.where(kinds[sel] == 1, bps[sel] <= th, bps[sel] < th)))
@@ -244,15 +249,15 @@ def _subbins(ph_all, hw_all, S, cen, hw, ssa, ssb, parts):
                 f += C_STEP + C_DQ * cnt
             prev = th
             lo, hi = th - h, th + h
-            inside = (lo > sa_min and lo < sb_max) if not hi > lo else (hi > sa_min and lo < sb_max)
-            if inside and len(spos):
-                g0, g1 = scell(np.array([lo, hi]))
+            inside = (hi > sa_min and lo < sb_max) and h > 0 and len(spos)
+            if inside:  # the spot cursor (sub_point)
                 f += C_SPOT_IN
-                for g in range(g0, g1 + 1):
-                    for pos, k_isa in zip(spos[scl == g], sfrom_a[scl == g]):
-                        if g == g0 and pos <= lo:
-                            f += C_SPOT_C
-                        elif hi > lo and pos < hi:
-                            f += C_SPOT_CORR
+                if not sv:
+                    g0 = scell(np.array([lo]))[0]
+                    f += C_SPOT_INIT + C_SPOT_C * int(np.sum(spos[scl == g0] <= lo))
+                sv = True
+                f += C_SPOT_CORR * int(np.searchsorted(spos_s, hi, "right") - np.searchsorted(spos_s, lo, "right"))
+            else:
+                sv = False
     parts["subbins"] += f
     return f
