@@ -529,6 +529,7 @@ __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
 // vectors; weights depend on ring only and are formed in k_lnlike.
 #ifdef LFG_COUNT_ITERS
 __device__ unsigned long long g_iter_dbg[64];
+
 #endif
 constexpr int U_WD = NWD / 2, U_DISC = NDISC / 2, U_BS = NBS, U_DON = NDONOR / 4;
 constexpr int NUNIQ = U_WD + U_DISC + U_BS + U_DON;
@@ -747,11 +748,29 @@ __device__ __forceinline__ void element_lane(int v, int pair, int npairs, const 
     AB[size_t(pair) * NELU + (u >= U_MAIN ? NU_WDD + (u - U_MAIN) : uslot(u))] = make_double2(a, b);
 }
 
+#ifdef LFG_PROFILE_ELEM  // diagnostic build only: per-wave start / end (s_memrealtime, 100 MHz), HW_ID, kind
+__device__ unsigned long long g_elem_wav[4][32768];
+__device__ __forceinline__ void elem_stamp(unsigned long long t0, int kind)
+{
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 32768) {
+        unsigned hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        g_elem_wav[0][blockIdx.x] = t0;
+        g_elem_wav[1][blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+        g_elem_wav[2][blockIdx.x] = hw;
+        g_elem_wav[3][blockIdx.x] = kind;
+    }
+}
+#endif
+
 __global__ __launch_bounds__(ELEM_BLOCK) __attribute__((amdgpu_waves_per_eu(ELEM_MINW))) void k_elements(const double* __restrict__ geo, int* status, int npairs,
                                                          double2* __restrict__ AB, double* __restrict__ DON,
                                                          double* __restrict__ WT, const int* __restrict__ bstatus,
                                                          ElemSpec X)
 {
+#ifdef LFG_PROFILE_ELEM
+    const unsigned long long pt0 = __builtin_amdgcn_s_memrealtime();
+#endif
     if (int(blockIdx.x) < X.nspecblk) {  // speculative setup lanes of the next half
         // candidate c's lanes fill blocks [c * nb, (c + 1) * nb): c is uniform
         // in a block, so X.S[c] is selected in scalar registers (a lane-varying
@@ -760,6 +779,9 @@ __global__ __launch_bounds__(ELEM_BLOCK) __attribute__((amdgpu_waves_per_eu(ELEM
         const int c = int(blockIdx.x) < nb ? 0 : 1;
         const int t = (int(blockIdx.x) - c * nb) * int(blockDim.x) + int(threadIdx.x);
         if (t < X.nspec) setup_any(X.S[__builtin_amdgcn_readfirstlane(c)], t);
+#ifdef LFG_PROFILE_ELEM
+        elem_stamp(pt0, 0);
+#endif
         return;
     }
     const unsigned bid = blockIdx.x - unsigned(X.nspecblk);
@@ -802,6 +824,9 @@ __global__ __launch_bounds__(ELEM_BLOCK) __attribute__((amdgpu_waves_per_eu(ELEM
 #pragma unroll 1
     for (int k = 0; k < LFG_ELEM_IPL; ++k)
         element_lane(v0 + k * int(blockDim.x), pair, npairs, G, st0, bst, status, AB, DON, WT, X);
+#ifdef LFG_PROFILE_ELEM
+    elem_stamp(pt0, 1 + int(bid / unsigned(npairs)));  // 1 + chunk of the pair's items
+#endif
 }
 
 // interval of element k (MODEL_SPEC 5 numbering) from a pair's table: the
@@ -3450,6 +3475,14 @@ int lfg_debug_like_waves(unsigned long long* host)
         return hipMemcpyToSymbol(HIP_SYMBOL(g_like_wav), buf, sizeof(buf)) == hipSuccess ? 0 : -1;
     }
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_like_wav), sizeof(g_like_wav)) == hipSuccess ? 0 : -1;
+}
+#endif
+
+#ifdef LFG_PROFILE_ELEM
+// diagnostic build only: k_elements' per-wave stamps of the last launch, host [4][32768]
+int lfg_debug_elem_waves(unsigned long long* host)
+{
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_elem_wav), sizeof(g_elem_wav)) == hipSuccess ? 0 : -1;
 }
 #endif
 
