@@ -68,14 +68,7 @@ def test_lnprob_configs_match_oracle(oracle, cfg):
     _same(got, ref, LNP_RTOL)
 
 
-@pytest.mark.parametrize("cfg", ["c2_complex", "c3_tree"])
-def test_prior_rejected_walkers_skip_the_model(oracle, cfg):
-    """Walkers with ln_prior = -inf get -inf without the model being run
-    (Node.ln_prob, model.py:476-498): k_elements and k_lnlike skip them.  An
-    exp2 -> 0 proposal puts the bright-spot strip at ~1e270 (bs_umax), whose
-    elements once sent whole waves into ms-long nested solves."""
-    import time
-    import torch
+def _prior_rejection_case(cfg):
     from lfit_python_amd import batch, synthetic
     if cfg == "c2_complex":
         m, W = synthetic.config_single(300, flux_fn=_flux_fn), 512
@@ -93,20 +86,45 @@ def test_prior_rejected_walkers_skip_the_model(oracle, cfg):
     walk[3::8, az[0]] = 200.0       # prior uniform(50, 175): out
     bad[1::4] = True
     bad[3::8] = True
-    ev = batch.LnProbEvaluator(t)
-    x = torch.as_tensor(walk, device="cuda")
-    got = ev(x).cpu().numpy()
+    return t, walk, bad
+
+
+@pytest.mark.parametrize("cfg", ["c2_complex", "c3_tree"])
+def test_prior_rejected_walkers_skip_the_model(oracle, cfg):
+    """Walkers with ln_prior = -inf get -inf without the model being run
+    (Node.ln_prob, model.py:476-498): k_elements and k_lnlike skip them.  An
+    exp2 -> 0 proposal puts the bright-spot strip at ~1e270 (bs_umax), whose
+    elements once sent whole waves into ms-long nested solves."""
+    import torch
+    from lfit_python_amd import batch
+    t, walk, bad = _prior_rejection_case(cfg)
+    got = batch.LnProbEvaluator(t)(torch.as_tensor(walk, device="cuda")).cpu().numpy()
     assert np.all(np.isneginf(got[bad]))
     ref, _, _ = oracle.lnprob_batch(walk, t)
     _same(got, ref, LNP_RTOL)
     assert np.isfinite(got[~bad]).sum() >= (~bad).sum() // 2
+
+
+@pytest.mark.perf
+@pytest.mark.parametrize("cfg", ["c2_complex", "c3_tree"])
+def test_prior_rejected_walkers_stay_fast(cfg):
+    """The wall-clock side of the test above (a shared box can slow it for
+    other reasons, hence the perf marker): a batch with prior-rejected absurd
+    strips stays far below the ms-long nested solves it once caused."""
+    import time
+    import torch
+    from lfit_python_amd import batch
+    t, walk, _ = _prior_rejection_case(cfg)
+    ev = batch.LnProbEvaluator(t)
+    x = torch.as_tensor(walk, device="cuda")
+    ev(x)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(5):
         ev(x)
     torch.cuda.synchronize()
     per = (time.perf_counter() - t0) / 5
-    assert per < 2e-3, "ln_prob of %d walkers took %.2f ms" % (W, per * 1e3)
+    assert per < 2e-3, "ln_prob of %d walkers took %.2f ms" % (len(walk), per * 1e3)
 
 
 @pytest.mark.parametrize("cfg", ["c2_complex", "c3_tree", "gp"])

@@ -139,24 +139,17 @@ def test_flux_matches_oracle(oracle, complex_bs, nsub):
     assert n_ok >= 18
 
 
-def test_absurd_geometry_stays_fast_and_matches(oracle):
+def test_absurd_geometry_matches(oracle):
     """lfg_flux has no prior to reject with: a bright-spot exponent exp2 ->
     0 places the strip at ~1e270 (bs_umax), and such elements must leave
     both solvers at once as uneclipsed (the !(cos D < 1) test) instead of
     iterating on non-finite geometry -- on the GPU and in the oracle alike."""
-    import time
-    import torch
     from lfit_python_amd.lfit import flux_batch
     pars = np.array(random_pars(16, complex_bs=True, seed=5))
     pars[::2, 15] = 3e-3          # exp2 (cv_parlist slot 15)
     pars[1::4, 14] = 1e-3         # and a tiny exp1 beside it
     x, w = phase_grid(300)
-    flux_batch(pars, x, w)        # warm
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
     flux, status = flux_batch(pars, x, w)
-    torch.cuda.synchronize()
-    assert time.perf_counter() - t0 < 0.05
     flux, status = flux.cpu().numpy(), status.cpu().numpy()
     for i, p in enumerate(pars):
         st, f = oracle.flux(p, x, w)
@@ -167,6 +160,26 @@ def test_absurd_geometry_stays_fast_and_matches(oracle):
         assert np.array_equal(np.isfinite(flux[i]), ok)
         if ok.any():
             assert _rel(flux[i][ok], f[ok], np.max(np.abs(f[ok]))) < FLUX_RTOL
+
+
+@pytest.mark.perf
+def test_absurd_geometry_stays_fast():
+    """The wall-clock side of test_absurd_geometry_matches (perf marker: a
+    shared box can slow it for other reasons): absurd strips leave the
+    solvers at once instead of iterating on non-finite geometry."""
+    import time
+    import torch
+    from lfit_python_amd.lfit import flux_batch
+    pars = np.array(random_pars(16, complex_bs=True, seed=5))
+    pars[::2, 15] = 3e-3
+    pars[1::4, 14] = 1e-3
+    x, w = phase_grid(300)
+    flux_batch(pars, x, w)        # warm
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    flux_batch(pars, x, w)
+    torch.cuda.synchronize()
+    assert time.perf_counter() - t0 < 0.05
 
 
 def test_cv_object_api(oracle):
