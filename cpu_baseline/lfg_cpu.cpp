@@ -133,8 +133,69 @@ struct Tables {
     double dnorm;  // donor flux at quadrature
 };
 
+#ifdef LFC_COUNT  // diagnostic build: Newton steps per lane and per 64-lane chunk (k_elements' waves)
+static unsigned long long g_cnt[4 + 3 * 8];  // lanes, sum of lane steps, chunks, sum of chunk maxima; per region (WD, disc, spot) histogram of lane steps
+extern "C" void lfc_counts(unsigned long long* o) { for (int i = 0; i < 4 + 24; ++i) o[i] = g_cnt[i]; }
+static unsigned long long g_ucost[U_WD + U_DISC + NBS];  // per unique item: sum of lane steps over pairs
+extern "C" void lfc_ucost(unsigned long long* o) { for (int i = 0; i < U_WD + U_DISC + NBS; ++i) { o[i] = g_ucost[i]; g_ucost[i] = 0; } }
+static void count_pair(const int* cost, int n)
+{
+    unsigned long long ls = 0, cm = 0, nc = 0;
+    for (int k = 0; k < n; k += 64) {
+        int m = 0;
+        for (int i = k; i < std::min(n, k + 64); ++i) {
+            m = std::max(m, cost[i]);
+            ls += cost[i];
+            const int reg = i < U_WD ? 0 : (i < U_WD + U_DISC ? 1 : 2);
+#pragma omp atomic
+            g_ucost[i] += cost[i];
+#pragma omp atomic
+            g_cnt[4 + reg * 8 + std::min(cost[i], 7)] += 1;
+        }
+        cm += m; ++nc;
+    }
+#pragma omp atomic
+    g_cnt[0] += n;
+#pragma omp atomic
+    g_cnt[1] += ls;
+#pragma omp atomic
+    g_cnt[2] += nc;
+#pragma omp atomic
+    g_cnt[3] += cm;
+}
+#define LFC_NIT int nit[3] = {0, 0, 0}; bool fb = false; double gs[2] = {0.0, 0.0};
+#define LFC_NITARGS , &fb, nit, gs
+#define LFC_COST(v) cost[v] = nit[0] + std::max(nit[1], nit[2]) + (fb ? 30 : 0)
+// element intervals in solve order (run with one thread to compare variants)
+static std::vector<double> g_ab;
+extern "C" long lfc_dump(double* o, long n)
+{
+    const long m = std::min<long>(n, long(g_ab.size()));
+    for (long i = 0; i < m; ++i) o[i] = g_ab[i];
+    g_ab.clear();
+    return m;
+}
+#define LFC_AB(a, b) do { _Pragma("omp critical") { g_ab.push_back(a); g_ab.push_back(b); g_gs.push_back(gs[0]); g_gs.push_back(gs[1]); } } while (0)
+static std::vector<double> g_gs;  // the initial guesses (rad) of the same solves
+extern "C" long lfc_dump_guess(double* o, long n)
+{
+    const long m = std::min<long>(n, long(g_gs.size()));
+    for (long i = 0; i < m; ++i) o[i] = g_gs[i];
+    g_gs.clear();
+    return m;
+}
+#else
+#define LFC_NIT
+#define LFC_NITARGS
+#define LFC_COST(v)
+#define LFC_AB(a, b)
+#endif
+
 void elements(const Pair& G, Tables& T)
 {
+#ifdef LFC_COUNT
+    int cost[U_WD + U_DISC + NBS] = {0};
+#endif
     const Roche& R = G.R;
     const double s = G.s, c = G.c;
     const double twd = TWO_PI * ((1.0 - G.ulimb) * 0.5 + G.ulimb / 3.0);
@@ -159,7 +220,10 @@ void elements(const Pair& G, Tables& T)
             wgt = (TWO_PI / NDISC_AZ) * (disc_boundary(ir + 1, G) - disc_boundary(ir, G)) / td;
         }
         double a, b;
-        element_interval_fast(R, Px, Py, Pz, s, c, G.rcal, G.reff, a, b);
+        LFC_NIT
+        element_interval_fast(R, Px, Py, Pz, s, c, G.rcal, G.reff, a, b LFC_NITARGS);
+        LFC_COST(u);
+        LFC_AB(a, b);
         T.a[k] = a; T.b[k] = b; T.w[k] = wgt; T.wd[k] = isw; ++k;
         const bool ecl = a < b;  // the mirror image's interval (MODEL_SPEC 7)
         T.a[k] = ecl ? -b : 1.0; T.b[k] = ecl ? -a : -1.0; T.w[k] = wgt; T.wd[k] = isw; ++k;
@@ -170,9 +234,15 @@ void elements(const Pair& G, Tables& T)
         T.sw[j] = std::exp(G.exp1 * std::log(uk) - std::pow(uk, G.exp2) - G.lnpk);
         tot += T.sw[j];
         const double off = G.L * (uk - G.upk);
+        LFC_NIT
         element_interval_fast(R, std::fma(off, G.caz, G.bsx), std::fma(off, G.saz, G.bsy), 0.0, s, c, G.rcal, G.reff,
-                              T.sa[j], T.sb[j]);
+                              T.sa[j], T.sb[j] LFC_NITARGS);
+        LFC_COST(U_WD + U_DISC + j);
+        LFC_AB(T.sa[j], T.sb[j]);
     }
+#ifdef LFC_COUNT
+    count_pair(cost, U_WD + U_DISC + NBS);
+#endif
     for (int j = 0; j < NBS; ++j) T.sw[j] /= tot;
     double dn = 0.0;
     for (int uu = 0; uu < U_DON; ++uu) {

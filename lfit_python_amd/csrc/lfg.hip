@@ -631,8 +631,8 @@ __device__ __forceinline__ void element_lane(int v, int pair, int npairs, const 
         return;
     }
     static_assert((NUNIQ % ELEM_BLOCK) + NDISC_R + 1 <= ELEM_BLOCK, "ring-weight lanes fit in the last chunk");
-    // launch order WD, disc, spot, donor: the last chunk, dispatched last,
-    // holds the cheap donor items (one 1-D root) instead of spot tangencies
+    // item order WD, disc, spot, donor (v); k_elements deals the chunks of
+    // 64 items out in its own dispatch order (kOrder)
     constexpr int V_BS = U_WD + U_DISC;
     const int u = (v < V_BS) ? v : (v < V_BS + U_BS ? U_MAIN + (v - V_BS) : v - U_BS);
     if (st0 != ST_OK) return;
@@ -661,8 +661,9 @@ __device__ __forceinline__ void element_lane(int v, int pair, int npairs, const 
             const double f = rpot_grad(R, X0, X1, X2, gx, gy, gz) - R.pl1;
             const double df = gx * dx + gy * dy + gz * dz;
             if (f > 0.0) hi = r; else lo = r;
-            if (df > 0.0 && fabs(f / df) <= ROOT_LAST) { r -= f / df; break; }  // last Newton step
-            double rn = (df > 0.0) ? r - f / df : 0.5 * (lo + hi);
+            const double stp = f * rcp_fast(df);  // (an IEEE quotient: ~10 dependent issue slots more a step)
+            if (df > 0.0 && fabs(stp) <= ROOT_LAST) { r -= stp; break; }  // last Newton step
+            double rn = (df > 0.0) ? r - stp : 0.5 * (lo + hi);
             if (!(rn > lo && rn < hi)) rn = 0.5 * (lo + hi);
             r = rn;
         }
@@ -771,6 +772,7 @@ __global__ __launch_bounds__(ELEM_BLOCK) __attribute__((amdgpu_waves_per_eu(ELEM
 #ifdef LFG_PROFILE_ELEM
     const unsigned long long pt0 = __builtin_amdgcn_s_memrealtime();
 #endif
+#ifndef LFG_NO_SPEC_LANES  // (experiment: the element path alone, with LFG_SPEC=0)
     if (int(blockIdx.x) < X.nspecblk) {  // speculative setup lanes of the next half
         // candidate c's lanes fill blocks [c * nb, (c + 1) * nb): c is uniform
         // in a block, so X.S[c] is selected in scalar registers (a lane-varying
@@ -784,6 +786,7 @@ __global__ __launch_bounds__(ELEM_BLOCK) __attribute__((amdgpu_waves_per_eu(ELEM
 #endif
         return;
     }
+#endif
     const unsigned bid = blockIdx.x - unsigned(X.nspecblk);
     // blocks cover the NUNIQ unique items of every pair in chunks of
     // blockDim.x (the spot items fill the last chunk); block b takes pair
@@ -795,7 +798,15 @@ __global__ __launch_bounds__(ELEM_BLOCK) __attribute__((amdgpu_waves_per_eu(ELEM
     const int pair = int(bid % unsigned(npairs));
     // LFG_ELEM_IPL items per lane, one after the other (chunks of
     // ELEM_BLOCK * LFG_ELEM_IPL items)
-    const int v0 = int(bid / unsigned(npairs)) * (int(blockDim.x) * LFG_ELEM_IPL) + int(threadIdx.x);
+    // chunks in dispatch order: the donor's (latency-bound 1-D roots, few
+    // VALU instructions) and the spot's and outer disc's (four Newton steps)
+    // first, the WD's and inner disc's (three) last, so that the second
+    // round of waves ends on short ones (profiles/r03/elem_timeline_*.txt:
+    // the kernel span 27.4 -> 25.2 us at config 2)
+    static_assert(ELEM_BLOCK * LFG_ELEM_IPL == 64 && (NUNIQ + NDISC_R + 1 + 63) / 64 == 15, "chunk order table");
+    constexpr int kOrder[15] = {13, 14, 12, 11, 10, 9, 8, 7, 6, 5, 4, 3, 2, 1, 0};
+    const int ck = kOrder[bid / unsigned(npairs)];
+    const int v0 = ck * (int(blockDim.x) * LFG_ELEM_IPL) + int(threadIdx.x);
     const double* G = geo + size_t(pair) * LFG_NGEO;
     int st0, bst;
     if (X.jk) {
@@ -825,7 +836,7 @@ __global__ __launch_bounds__(ELEM_BLOCK) __attribute__((amdgpu_waves_per_eu(ELEM
     for (int k = 0; k < LFG_ELEM_IPL; ++k)
         element_lane(v0 + k * int(blockDim.x), pair, npairs, G, st0, bst, status, AB, DON, WT, X);
 #ifdef LFG_PROFILE_ELEM
-    elem_stamp(pt0, 1 + int(bid / unsigned(npairs)));  // 1 + chunk of the pair's items
+    elem_stamp(pt0, 1 + ck);  // 1 + chunk of the pair's items
 #endif
 }
 
@@ -2923,7 +2934,18 @@ __global__ void k_accept_regen(double* __restrict__ pos, double* __restrict__ ln
         const int j = int(__umulhi(r0.z, unsigned(ns)));
         double* p = pos + size_t(w) * ndim;
         const double* cj = pos + size_t((1 - half) * ns + j) * ndim;
-        for (int d = 0; d < ndim; ++d) p[d] = fma(p[d] - cj[d], z, cj[d]);
+        // p and cj are rows of one array: the loads of a chunk are issued
+        // together before its stores (a load-fma-store loop waited on every
+        // load in turn)
+        for (int d0 = 0; d0 < ndim; d0 += 8) {
+            double pv[8], cv[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if (d0 + k < ndim) { pv[k] = p[d0 + k]; cv[k] = cj[d0 + k]; }
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if (d0 + k < ndim) p[d0 + k] = fma(pv[k] - cv[k], z, cv[k]);
+        }
         lnp[w] = lnp_new[i];
         if (naccept) naccept[w] += 1;
     }

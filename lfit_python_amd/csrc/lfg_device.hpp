@@ -428,21 +428,35 @@ __device__ __forceinline__ void rotate(double& cs, double& sn, double d)
 // at one point: t moves to the ray's minimum of Phi (dt0 = -F2 / J22), which
 // lowers F1 by F2^2 / (2 J22), and th takes the Newton step of that corrected
 // F1 with the envelope slope J11 + J21 dt0; t then follows th along the
-// valley (dt = dt0 - J21 / J22 dth).  The t guess (closest approach to the
-// donor centre) is ~1e-2 off the tangent point; in the joint 2-D step that
-// error leaks into th at first order, here only at second order, so th
-// converges one step earlier (tools/newton_emul statistics in DESIGN.md).
-// Stop once |dth| <= TH_LAST (th error ~TH_LAST^2 after the step) and
-// |dt| <= T_LAST (t errors reach th squared): ~1e-14 rad (MODEL_SPEC 7).
-constexpr double TH_LAST = 3e-8;
-constexpr double T_LAST = 1e-5;
+// valley (dt = dt0 - J21 / J22 dth).  In the joint 2-D step a t error leaks
+// into th at first order, here only at second order.
+// The first step is Halley's on the envelope (g'' = F1_thth - F1_tht^2 /
+// F1_tt, the Schur complement; F1_thth = t^2 e_th.H.e_th + t grad.e_thth):
+// from the sphere guesses (1e-3..1e-2 rad off) it lands ~1e-7..1e-5 off, so
+// most contacts stop after a second, Newton, step.  t starts at the ray's
+// minimum of Phi to first order (element_interval_fast), not at the closest
+// approach to D (~1e-2 off): with t that far off the second step's |dt| kept
+// a third step in play (tools/tol_study.py: k_elements' wave-max steps per
+// lane 4.27 -> 3.43 at config 2, interval errors < 3e-12 in phase).
+// Stop once |dth| <= TH_LAST (th error ~TH_LAST^2 after a Newton step) and
+// |dt| <= T_LAST (t errors reach th at second order): ~1e-12 rad (MODEL_SPEC 7).
+#ifndef LFG_TH_LAST
+#define LFG_TH_LAST 1e-6
+#endif
+#ifndef LFG_T_LAST
+#define LFG_T_LAST 3e-5
+#endif
+constexpr double TH_LAST = LFG_TH_LAST;
+constexpr double T_LAST = LFG_T_LAST;
 
 struct Tan {
     double th, cs, sn, t;
     int st;
 };
 
-// one branch-free step (two solves can run interleaved in one lane)
+// one branch-free step (two solves can run interleaved in one lane);
+// HALLEY: the curvature-corrected first step
+template <bool HALLEY = false>
 __device__ __forceinline__ void tangency_step(const Roche& R, double Px, double Py, double Pz, double s, double c,
                                               bool ingress, Tan& T)
 {
@@ -456,7 +470,13 @@ __device__ __forceinline__ void tangency_step(const Roche& R, double Px, double 
     const double F1m = fma(0.5 * o.F2, dt0, F1);  // F1 - F2^2 / (2 J22)
     const double den = fma(J21, dt0, J11);
     const bool bad = !(J22 != 0.0) || !(den != 0.0);
-    double dth = -F1m * rcp_step(den);
+    const double iden = rcp_step(den);
+    double dth = -F1m * iden;
+    if (HALLEY) {  // dth / (1 + dth g'' / (2 g')); plain Newton where that factor is far from 1
+        const double g2 = fma(T.t, fma(T.t, o.ethHeth, o.gtt), -J21 * J21 * iJ22);
+        const double h = 0.5 * dth * g2 * iden;
+        if (fabs(h) < 0.5) dth = dth * rcp_step(1.0 + h);
+    }
     dth = fmin(fmax(dth, -0.05), 0.05);
     const double dt = fma(-J21 * iJ22, dth, dt0);
     T.th += dth;
@@ -485,7 +505,11 @@ __device__ inline bool tangency(const Roche& R, double Px, double Py, double Pz,
 __device__ inline void tangency_pair(const Roche& R, double Px, double Py, double Pz, double s, double c, Tan& A,
                                      Tan& B, int* nit = nullptr)
 {
-    for (int it = 0; it < 16; ++it) {
+    tangency_step<true>(R, Px, Py, Pz, s, c, true, A);  // both start running: no lockstep copies
+    tangency_step<true>(R, Px, Py, Pz, s, c, false, B);
+    if (nit) { nit[0] += 1; nit[1] += 1; }  // diagnostic builds only
+    if (A.st != 0 && B.st != 0) return;
+    for (int it = 1; it < 16; ++it) {
         Tan A2 = A, B2 = B;
         tangency_step(R, Px, Py, Pz, s, c, true, A2);
         tangency_step(R, Px, Py, Pz, s, c, false, B2);
@@ -569,6 +593,24 @@ __device__ inline bool element_interval_fast(const Roche& R, double Px, double P
                 Tan In{thc - de, ci, si, s * (ux * ci - uy * si) + uz * c, 0};
                 Tan Out{thc + de, co, so, s * (ux * co - uy * so) + uz * c, 0};
                 if (guess) { guess[0] = In.th; guess[1] = Out.th; }  // diagnostic builds only
+                // t at the ray's minimum of Phi, one Newton step from the
+                // closest approach X_c to D: there the donor's own term has
+                // no slope along e, so e.grad Phi = e.grad(-cA/r1 - (x-mu)^2
+                // - y^2), and e.H.e = cB/d^3 + the WD's and the centrifugal
+                // parts, with d = Rcal (the guess rays graze that sphere)
+                {
+                    const double icb = R.cB / (Rcal * Rcal * Rcal) - 2.0 * s * s;
+                    for (Tan* T : {&In, &Out}) {
+                        const double ex = s * T->cs, ey = -s * T->sn;
+                        const double x = fma(T->t, ex, Px), y = fma(T->t, ey, Py), z = fma(T->t, c, Pz);
+                        const double ir1 = rsqrt_pos(x * x + y * y + z * z), ir1s = ir1 * ir1;
+                        const double eX = x * ex + y * ey + z * c;
+                        const double i1 = R.cA * ir1s * ir1;
+                        const double slope = fma(i1, eX, -2.0 * fma(x - R.mu, ex, y * ey));
+                        const double curv = fma(i1, fma(-3.0 * eX * eX, ir1s, 1.0), icb);
+                        T->t -= slope * rcp_fast(curv);
+                    }
+                }
                 tangency_pair(R, Px, Py, Pz, s, c, In, Out, nit ? nit + 1 : nullptr);
                 // both contacts within Dm of thc (where the ray meets the
                 // donor's sphere), tested as cos(th - thc) > cos Dm with the
