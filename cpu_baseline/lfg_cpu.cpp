@@ -165,7 +165,13 @@ static void count_pair(const int* cost, int n)
 }
 #define LFC_NIT int nit[3] = {0, 0, 0}; bool fb = false; double gs[2] = {0.0, 0.0};
 #define LFC_NITARGS , &fb, nit, gs
+#if LFC_COST_MODE == 1  // FP32 lockstep steps only (LFG_F32_FIRST counts them x 1000 in nit[0])
+#define LFC_COST(v) cost[v] = nit[0] / 1000
+#elif LFC_COST_MODE == 2  // everything else
+#define LFC_COST(v) cost[v] = nit[0] % 1000 + std::max(nit[1], nit[2]) + (fb ? 30 : 0)
+#else
 #define LFC_COST(v) cost[v] = nit[0] + std::max(nit[1], nit[2]) + (fb ? 30 : 0)
+#endif
 // element intervals in solve order (run with one thread to compare variants)
 static std::vector<double> g_ab;
 extern "C" long lfc_dump(double* o, long n)

@@ -15,3 +15,4 @@
 using std::max;  // the device code's integer min / max
 using std::min;
 inline double rsqrt(double x) { return 1.0 / std::sqrt(x); }
+inline float rsqrtf(float x) { return 1.0f / std::sqrt(x); }
