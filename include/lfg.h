@@ -62,7 +62,9 @@ struct lfg_tree {
     int E;                    /* eclipses (leaves)                          */
     int ndim;                 /* walker vector length                       */
     int nsub;                 /* exposure sub-bins S >= 1 (1 = native)      */
-    int max_n;                /* max data points of any eclipse            */
+    int max_n;                /* max data points of any eclipse: the max
+                                 of off[e+1] - off[e] (off[0] = 0; with one
+                                 eclipse the kernels take {0, max_n})       */
     const int* gather;        /* [dev] E*18                                 */
     const int* npars;         /* [dev] E, 14 or 18                          */
     const double* consts;     /* [dev] constant parameter values            */

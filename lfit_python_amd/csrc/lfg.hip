@@ -1889,8 +1889,11 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
     const int pair = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int e = (L.E == 1) ? 0 : pair % L.E;  // (one eclipse: no division constants held)
-    const int o0 = L.off ? L.off[e] : 0;
-    const int n = L.off ? L.off[e + 1] - o0 : L.N;
+    // one eclipse: off = {0, max_n} (lfg.h), so the point loads need not
+    // wait on a load of the offsets (one memory round trip of the prologue)
+    const bool offs = L.off && L.E > 1;
+    const int o0 = offs ? L.off[e] : 0;
+    const int n = offs ? L.off[e + 1] - o0 : L.N;
     const double* G = L.geo + size_t(pair) * LFG_NGEO;
     const double* Wt = L.WT + size_t(pair) * WT_N;
     const double2* AB = L.AB + size_t(pair) * NELU;
@@ -2215,7 +2218,7 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
         if (t0 > 0 && own) {
             // the point index re-formed from a fresh (volatile) read of the
             // offset: o0 + tid would otherwise be held, spilled, over the tiles
-            const int p = (L.off ? *reinterpret_cast<const volatile int*>(L.off + e) : 0) + t0 + tid;
+            const int p = (offs ? *reinterpret_cast<const volatile int*>(L.off + e) : 0) + t0 + tid;
             px = L.x[p];
             pw = L.w ? L.w[p] : 0.0;
             if (CHI) {

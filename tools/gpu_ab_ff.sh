@@ -10,3 +10,6 @@ tools/gpu_steps.sh \
  "ff_p2:200:rocprofv3 --kernel-trace --stats -d gpurun_out/ff_prof2 -o run --output-format csv -- python3 bench.py --steps 100 --warmup 5 --no-cpu" \
  "ff_p2p:200:LFG_LIB=$E/liblfg_PREV.so rocprofv3 --kernel-trace --stats -d gpurun_out/ff_prof2_prev -o run --output-format csv -- python3 bench.py --steps 100 --warmup 5 --no-cpu"
 bash tools/gpu_emu_weak.sh
+tools/gpu_steps.sh \
+ "ff_gloo2:300:LFG_BENCH_BACKEND=gloo python3 bench.py --gpus 2 --steps 20 --warmup 3 --no-cpu > gpurun_out/ff_c2_gloo2.json" \
+ "ff_gloo4:300:LFG_BENCH_BACKEND=gloo python3 bench.py --gpus 4 --steps 20 --warmup 3 --no-cpu > gpurun_out/ff_c2_gloo4.json"
