@@ -13,7 +13,7 @@ from tests.helpers import TRUTH14, TRUTH18, ECL1, random_pars, phase_grid
 pytestmark = pytest.mark.gpu
 
 FLUX_RTOL = 1e-6      # north_star contract, relative to the flux scale
-PHASE_ATOL = 1e-9     # eclipse contact phases
+PHASE_ATOL = 1e-10    # eclipse contact phases (the tangency Newton stops at |dth| <= 1e-6: ~1e-12 in phase)
 
 
 def _rel(a, b, scale):
