@@ -126,7 +126,7 @@ def parse(argv=None):
                          "W/2/N walkers evaluated per half, a one-rank RCCL exchange of the shard, the acceptance "
                          "over the whole half); also times the fused one-GPU step and reports the implied 1->N ratio")
     ap.add_argument("--seed", type=int, default=20261015)
-    ap.add_argument("--time-every", type=int, default=4,
+    ap.add_argument("--time-every", type=int, default=8,
                     help="record the dominant kernel's event pair on every k-th ln_prob call of the timed region")
     args = ap.parse_args(argv)
     cfg = CONFIGS[args.config]
