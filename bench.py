@@ -320,7 +320,11 @@ def run(args):
         ncall[0] += 1
         return (ncall[0] - 1) % every[0] == 0
 
+    pool = []  # event sets made before the timed region (hipEventCreate is host work in the loop)
+
     def make_evs():
+        if pool:
+            return pool.pop()
         evs = (ctypes.c_void_p * NEV)()
         for i in range(NEV):
             if want[i]:
@@ -386,6 +390,8 @@ def run(args):
     want[:] = [i in (ea, eb) for i in range(NEV)]
     every[0] = max(1, args.time_every)
     ncall[0] = 0
+    calls = 2 * args.steps  # ln_prob calls of the timed region (one per half-step)
+    pool.extend(make_evs() for _ in range((calls + every[0] - 1) // every[0]))
     set_timing(True)
 
     if dist:
@@ -408,6 +414,11 @@ def run(args):
     # the dominant kernel's device time over the timed region
     shard = events[0][1] if events else W // 2   # walkers per launch
     dom_ms, ncalls = kernel_ms([KERNELS[dom]])
+    for evs in pool:  # unused sets of the timed region
+        for i in range(NEV):
+            if evs[i]:
+                L.lfg_event_destroy(evs[i])
+    pool.clear()
     emu = None
     if args.emu:
         # the same ensemble on one GPU through the fused single-process path
