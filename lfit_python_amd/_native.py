@@ -5,7 +5,9 @@ package goes through the HIP kernels, and fails loudly when the library or a
 GPU is missing.
 """
 import ctypes
+import hashlib
 import os
+import re
 import subprocess
 import threading
 
@@ -13,8 +15,15 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(_HERE)
 LIB_DIR = os.path.join(_HERE, "_lib")
 LIB_PATH = os.path.join(LIB_DIR, "liblfg_hip.so")
-# diagnostic builds (e.g. -DLFG_PROFILE_SETUP) are loaded through LFG_LIB
-LOAD_PATH = os.environ.get("LFG_LIB", LIB_PATH)
+# diagnostic builds (e.g. -DLFG_PROFILE_SETUP) are loaded through LFG_LIB,
+# and only with LFG_DIAGNOSTIC=1 set as well: a stray LFG_LIB must not swap
+# the product library silently
+LOAD_PATH = LIB_PATH
+if os.environ.get("LFG_LIB"):
+    if os.environ.get("LFG_DIAGNOSTIC") != "1":
+        raise RuntimeError("LFG_LIB=%s is set without LFG_DIAGNOSTIC=1: diagnostic builds are loaded only on "
+                           "request (unset LFG_LIB to load %s)" % (os.environ["LFG_LIB"], LIB_PATH))
+    LOAD_PATH = os.environ["LFG_LIB"]
 SOURCES = [os.path.join(_HERE, "csrc", "lfg.hip"), os.path.join(_HERE, "csrc", "lfg_components.hip")]
 HEADERS = [os.path.join(_HERE, "csrc", "lfg_device.hpp"),
            os.path.join(_HERE, "csrc", "lfg_tables.hpp"),
@@ -68,20 +77,71 @@ EXPORTS = ("lfg_workspace_size", "lfg_workspace_size_tree", "lfg_flux", "lfg_lnp
            "lfg_component", "lfg_version")
 
 
+FLAGS = ["--offload-arch=%s" % ARCH, "-O3", "-std=c++17", "-fPIC", "-shared"]
+HASH_TAG = b"lfg-src-hash:"
+
+
+def source_hash():
+    """16 hex digits of SHA-256 over the library's sources, headers and
+    compile flags: compiled into the library (lfg_version, and a tag string
+    build() reads back), so a stale or foreign binary is told apart from
+    the one this tree builds."""
+    h = hashlib.sha256()
+    for p in SOURCES + HEADERS:
+        h.update(os.path.relpath(p, REPO).encode())
+        with open(p, "rb") as fh:
+            h.update(fh.read())
+    h.update(" ".join(FLAGS).encode())
+    return h.hexdigest()[:16]
+
+
+def file_hash(path):
+    """the source hash compiled into the library at `path` (None: no tag)"""
+    try:
+        with open(path, "rb") as fh:
+            data = fh.read()
+    except OSError:
+        return None
+    m = re.search(re.escape(HASH_TAG) + rb"([0-9a-f]{16})", data)
+    return m.group(1).decode() if m else None
+
+
+def needs_build():
+    return file_hash(LIB_PATH) != source_hash()
+
+
 def build(force=False, verbose=False):
-    """Compile liblfg_hip.so in-tree for gfx950 (hipcc cross-compiles offline)."""
+    """Compile liblfg_hip.so in-tree for gfx950 (hipcc cross-compiles
+    offline) unless the library there was built from exactly these sources
+    and flags (its compiled-in source hash, not file times, decides)."""
     os.makedirs(LIB_DIR, exist_ok=True)
-    newest = max(os.path.getmtime(p) for p in SOURCES + HEADERS)
-    if not force and os.path.exists(LIB_PATH) and os.path.getmtime(LIB_PATH) >= newest:
+    want = source_hash()
+    if not force and file_hash(LIB_PATH) == want:
         return LIB_PATH
     tmp = LIB_PATH + ".tmp"
-    cmd = ["hipcc", "--offload-arch=%s" % ARCH, "-O3", "-std=c++17", "-fPIC",
-           "-shared", "-I", INCLUDE, "-o", tmp] + SOURCES
+    cmd = ["hipcc"] + FLAGS + ['-DLFG_SRC_HASH="%s"' % want, "-I", INCLUDE, "-o", tmp] + SOURCES
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
     os.replace(tmp, LIB_PATH)
     return LIB_PATH
+
+
+def loaded_hash():
+    """the source hash of the library this process loaded (lfg_version's src=)"""
+    v = lib().lfg_version().decode()
+    m = re.search(r"src=([0-9a-f]{16}|unhashed)", v)
+    return m.group(1) if m else None
+
+
+def verify():
+    """Raise unless the loaded library is the one this tree's sources build
+    (smoke() and the GPU test session check it before any kernel runs)."""
+    got, want = loaded_hash(), source_hash()
+    if got != want:
+        raise RuntimeError("loaded %s carries source hash %s, the tree's sources hash to %s: a stale or foreign "
+                           "library (rebuild with __graft_entry__.build())" % (LOAD_PATH, got, want))
+    return got
 
 
 _lib = None

@@ -16,6 +16,7 @@
 // (model.py:476-498) -> lfit.CV.calcFlux (CVModel.py:138).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <type_traits>
 
@@ -89,8 +90,13 @@ struct Ws {
     double* qC;     // [2][2][W][ndim]
     double* zfC;    // [2][2][W]
     int* jk;        // [2][W] the partner (in the other half) of walker w's proposal
-    int* accflag;   // [max(W, nacc)] 1: walker j of the last half accepted its move (a rank's
-                    // shard of W walkers needs every partner's: nacc = the half)
+    int* accflag;   // [2][accstride] by the parity of the half that wrote it: 1 where walker
+                    // j accepted its move (a rank's shard of W walkers needs every partner's:
+                    // nacc = the half); two copies, so a launch that accepts moves of half h
+                    // while it selects candidates by half 1 - h's flags reads one, writes the other
+    size_t accstride;
+    double* snap;   // [2][accstride][ndim] k_pair: the rows of each half of pos as they were
+                    // when the launch that reads them began (SetupArgs.ppos)
     size_t total;
 };
 
@@ -122,7 +128,9 @@ Ws carve(void* base, int W, int E, int gp_n = 0, int ndim_spec = 0, int nacc = 0
         ws.qC = reinterpret_cast<double*>(take(4 * size_t(W) * ndim_spec * sizeof(double)));
         ws.zfC = reinterpret_cast<double*>(take(4 * size_t(W) * sizeof(double)));
         ws.jk = reinterpret_cast<int*>(take(2 * size_t(W) * sizeof(int)));
-        ws.accflag = reinterpret_cast<int*>(take(size_t(W > nacc ? W : nacc) * sizeof(int)));
+        ws.accstride = size_t(W > nacc ? W : nacc);
+        ws.accflag = reinterpret_cast<int*>(take(2 * ws.accstride * sizeof(int)));
+        ws.snap = reinterpret_cast<double*>(take(2 * ws.accstride * ndim_spec * sizeof(double)));
     }
     ws.total = off;
     return ws;
@@ -172,6 +180,10 @@ struct SetupArgs {
     int cand;
     unsigned long long step_prev;
     int* jkout;
+    // nullable: the partner half's positions as they were when this launch
+    // began ([ns][ndim]; k_pair's speculative lanes, whose launch accepts
+    // moves of that half while they read it)
+    const double* ppos;
 };
 
 // where a lane reads walker w's parameters: the walker row, or the
@@ -195,8 +207,9 @@ __device__ inline Prop make_prop(const SetupArgs& A, int w)
     const double zr = (A.a - 1.0) * u + 1.0;
     const int j = int(__umulhi(r.z, unsigned(ns)));
     if (A.jkout && A.cand == 0) A.jkout[w] = j;
-    Prop P{A.pos + size_t(A.half * ns + i) * A.ndim, A.pos + size_t((1 - A.half) * ns + j) * A.ndim,
-           zr * zr / A.a, nullptr, 0.0};
+    Prop P{A.pos + size_t(A.half * ns + i) * A.ndim,
+           A.ppos ? A.ppos + size_t(j) * A.ndim : A.pos + size_t((1 - A.half) * ns + j) * A.ndim, zr * zr / A.a,
+           nullptr, 0.0};
     if (A.cand) {  // partner j's proposal in the other half (step_prev), as its own make_prop forms it
         const int hp = 1 - A.half;
         const uint4 rj = draw(A.seed, A.step_prev, hp, 0, j);
@@ -549,7 +562,8 @@ __device__ inline double wd_ring_weight(int ir, double ul) { return fma(kWdA[ir]
 
 // radial integral of r^(1 - dexp) dr over the disc annuli (MODEL_SPEC 5.2):
 // the boundary term P(r) = r^ex / ex, or ln r when ex = 2 - dexp vanishes
-__device__ inline double disc_boundary(int i, const double* G)
+template <typename GPtr>
+__device__ inline double disc_boundary(int i, GPtr G)
 {
     const double rin = G[G_RWD];
     const double r = rin + i * ((G[G_RDISC] - rin) / NDISC_R);
@@ -557,12 +571,14 @@ __device__ inline double disc_boundary(int i, const double* G)
     return (fabs(ex) < 1e-10) ? log(r) : pow(r, ex) / ex;
 }
 
-__device__ inline double disc_ring_weight(int ir, const double* G)
+template <typename GPtr>
+__device__ inline double disc_ring_weight(int ir, GPtr G)
 {
     return (TWO_PI / NDISC_AZ) * (disc_boundary(ir + 1, G) - disc_boundary(ir, G));
 }
 
-__device__ inline double bs_weight(int j, const double* G)
+template <typename GPtr>
+__device__ inline double bs_weight(int j, GPtr G)
 {
     const double uk = (j + 0.5) * (G[G_UMAX] / NBS);
     return exp(G[G_EXP1] * log(uk) - pow(uk, G[G_EXP2]) - G[G_LNPK]);
@@ -608,36 +624,52 @@ struct ElemSpec {
     int nspecblk;  // leading blocks that run them
 };
 
+// where one pair's element results go: the global workspace tables
+// (k_elements) or the block's LDS (k_pair)
+struct ElemOut {
+    double2* abw;  // [NU_WDD] WD/disc intervals, slot uslot(u)
+    double2* abs;  // [NBS] spot intervals
+    double* don;   // [U_DON][DON_STRIDE] donor tiles
+    double* wtd;   // [NDISC_R + 1] disc ring weights, then the disc total
+    double* wbs;   // [NBS] spot element weights
+};
+
+// the disc ring weights (MODEL_SPEC 5.2) by the lanes of items v = NUNIQ +
+// i, i = 0..NDISC_R, consecutive lanes of one wave: lane i holds the boundary
+// term P(r_i) and ring i's weight is the difference of neighbours (one pow
+// per lane of one wave, instead of two in a ring-start lane of every disc wave)
+template <typename GPtr>
+__device__ __forceinline__ void ring_weight_lane(int rb, GPtr G, double* __restrict__ wtd)
+{
+    const double P = disc_boundary(rb, G);
+    const int lane = int(threadIdx.x) & 63, l0 = lane - rb;  // lane of P(r_0)
+    const double Pn = __shfl(P, min(lane + 1, l0 + NDISC_R), 64);
+    const double Pt = __shfl(P, l0 + NDISC_R, 64);
+    if (rb < NDISC_R) wtd[rb] = (TWO_PI / NDISC_AZ) * (Pn - P);
+    if (rb == 0) wtd[NDISC_R] = TWO_PI * (Pt - P);
+}
+
+template <typename GPtr>
+__device__ __forceinline__ void element_item(int v, GPtr G, const ElemOut& O);
+
 // one k_elements lane's item v of pair `pair` (v >= NUNIQ: the disc ring
 // weights of the last chunk's spare lanes)
 __device__ __forceinline__ void element_lane(int v, int pair, int npairs, const double* __restrict__ G, int st0, int bst,
                                              int* status, double2* __restrict__ AB, double* __restrict__ DON,
                                              double* __restrict__ WT, const ElemSpec& X)
 {
-    if (v >= NUNIQ) {
-        // the last chunk's spare lanes: the disc ring weights (MODEL_SPEC
-        // 5.2).  Lane NUNIQ + i holds the boundary term P(r_i), i = 0..NDISC_R;
-        // ring i's weight is the difference of neighbours: one pow per lane
-        // of one wave, instead of two in a ring-start lane of every disc wave
+    double* Wp = WT + size_t(pair) * WT_N;
+    if (v >= NUNIQ) {  // the last chunk's spare lanes
         const int rb = v - NUNIQ;
         if (rb > NDISC_R || st0 != ST_OK) return;
-        const double P = disc_boundary(rb, G);
-        const int lane = int(threadIdx.x) & 63, l0 = lane - rb;  // lane of P(r_0)
-        const double Pn = __shfl(P, min(lane + 1, l0 + NDISC_R), 64);
-        const double Pt = __shfl(P, l0 + NDISC_R, 64);
-        double* Wp = WT + size_t(pair) * WT_N;
-        if (rb < NDISC_R) Wp[WT_DISC + rb] = (TWO_PI / NDISC_AZ) * (Pn - P);
-        if (rb == 0) Wp[WT_TD] = TWO_PI * (Pt - P);
+        ring_weight_lane(rb, G, Wp + WT_DISC);
         return;
     }
     static_assert((NUNIQ % ELEM_BLOCK) + NDISC_R + 1 <= ELEM_BLOCK, "ring-weight lanes fit in the last chunk");
-    // item order WD, disc, spot, donor (v); k_elements deals the chunks of
-    // 64 items out in its own dispatch order (kOrder)
-    constexpr int V_BS = U_WD + U_DISC;
-    const int u = (v < V_BS) ? v : (v < V_BS + U_BS ? U_MAIN + (v - V_BS) : v - U_BS);
+    static_assert(WT_TD == WT_DISC + NDISC_R, "disc total follows the ring weights");
     if (st0 != ST_OK) return;
     if (bst != ST_OK) {
-        if (u == 0 && !X.jk) status[pair] = bst;
+        if (v == 0 && !X.jk) status[pair] = bst;
         return;
     }
     if (X.lprior) {  // the walker's ln_prior is -inf: nothing to evaluate (k_lnlike skips it too)
@@ -645,6 +677,17 @@ __device__ __forceinline__ void element_lane(int v, int pair, int npairs, const 
         const double lp = X.jk ? X.priorC[size_t(X.accflag[X.jk[w]]) * (npairs / X.E) + w] : X.lprior[w];
         if (prior_rejects(lp, G)) return;
     }
+    double2* ABp = AB + size_t(pair) * NELU;
+    element_item(v, G, ElemOut{ABp, ABp + NU_WDD, DON + size_t(pair) * U_DON * DON_STRIDE, Wp + WT_DISC, Wp + WT_BS});
+}
+
+// item v (v < NUNIQ) of a pair: item order WD, disc, spot, donor; k_elements
+// deals the chunks of 64 items out in its own dispatch order (kOrder)
+template <typename GPtr>
+__device__ __forceinline__ void element_item(int v, GPtr G, const ElemOut& O)
+{
+    constexpr int V_BS = U_WD + U_DISC;
+    const int u = (v < V_BS) ? v : (v < V_BS + U_BS ? U_MAIN + (v - V_BS) : v - U_BS);
     const Roche R{G[G_Q], G[G_CA], G[G_CB], G[G_MU], G[G_XL1], G[G_PL1], G[G_RS], G[G_RS2]};
     const double s = G[G_S], c = G[G_C];
 
@@ -676,7 +719,7 @@ __device__ __forceinline__ void element_lane(int v, int pair, int npairs, const 
         // rho cos(alpha) = vx, rho sin(alpha) = vy  ->  |theta + alpha| < acos(kappa)
         const double srho = s * sqrt(vx * vx + vy * vy);
         const double kap = (srho > 0.0) ? -c * vz / srho : (c * vz > 0.0 ? -2.0 : 2.0);
-        double* D = DON + (size_t(pair) * U_DON + uu) * DON_STRIDE;
+        double* D = O.don + uu * DON_STRIDE;
         D[0] = vx;
         D[1] = vy;
         D[2] = vz;
@@ -706,7 +749,7 @@ __device__ __forceinline__ void element_lane(int v, int pair, int npairs, const 
     } else {  // bright-spot strip (MODEL_SPEC 5.3): no mirror partner
         const int j = u - U_MAIN;
         const double uk = (j + 0.5) * (G[G_UMAX] / NBS);
-        WT[size_t(pair) * WT_N + WT_BS + j] = bs_weight(j, G);
+        O.wbs[j] = bs_weight(j, G);
         const double off = G[G_L] * (uk - G[G_UPK]);
         Px = fma(off, G[G_CAZ], G[G_BSX]);
         Py = fma(off, G[G_SAZ], G[G_BSY]);
@@ -733,7 +776,7 @@ __device__ __forceinline__ void element_lane(int v, int pair, int npairs, const 
         atomicAdd(C + 6, fb ? 1ull : 0ull);
         if (fb) {  // slots 48..63: count, then up to 15 (pair << 16 | item) records
             const unsigned long long k = atomicAdd(g_iter_dbg + 48, 1ull);
-            if (k < 15) g_iter_dbg[49 + k] = (static_cast<unsigned long long>(pair) << 16) | unsigned(u);
+            if (k < 15) g_iter_dbg[49 + k] = (static_cast<unsigned long long>(blockIdx.x) << 16) | unsigned(u);
         }
         atomicAdd(C + 7, 1ull);
         atomicAdd(C + 8, (a < b) ? 1ull : 0ull);
@@ -746,7 +789,8 @@ __device__ __forceinline__ void element_lane(int v, int pair, int npairs, const 
 #else
     element_interval_fast(R, Px, Py, Pz, s, c, G[G_RCAL], G[G_REFF], a, b);
 #endif
-    AB[size_t(pair) * NELU + (u >= U_MAIN ? NU_WDD + (u - U_MAIN) : uslot(u))] = make_double2(a, b);
+    if (u >= U_MAIN) O.abs[u - U_MAIN] = make_double2(a, b);
+    else O.abw[uslot(u)] = make_double2(a, b);
 }
 
 #ifdef LFG_PROFILE_ELEM  // diagnostic build only: per-wave start / end (s_memrealtime, 100 MHz), HW_ID, kind
@@ -2382,6 +2426,353 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
     }
 }
 
+// ------------------------------------------------------------------ k_pair
+// k_elements and k_lnlike<1, false> of one (walker, eclipse) pair in ONE
+// workgroup, for trees whose eclipses fit one tile (max_n <= LIKE_TILE, S =
+// 1, no GP): the pair's element intervals, spot and donor tables go from the
+// solver lanes to the block's LDS and never through HBM, and the half-step
+// is one launch instead of two (no kernel boundary behind a 10 MB table
+// write-back, no prologue re-fetch of the tables).
+//  * element phase: waves 0-6 solve two 64-item chunks of k_elements' item
+//    numbering each (paired long with short, PAIR_CHUNKS), wave 7 the last
+//    chunk (4 donor tiles and the 21 ring-weight lanes) and, on lanes 32..,
+//    this block's share of the speculative setup lanes of the next half
+//    (setup_any, as k_elements' leading blocks run them); every lane's
+//    results are in LDS at the phase barrier
+//  * likelihood phase: k_lnlike's single-tile sweep, scan, chi^2 and fused
+//    acceptance, its per-thread items read from LDS
+// With the fused acceptance the block writes its walker's row of pos while
+// the speculative lanes of other blocks read partner rows of the same half:
+// those lanes read the snapshot (SetupArgs.ppos) that the launch before took
+// of that half, and this launch snapshots the other half for the next one.
+constexpr int PAIR_SPEC_LANE0 = 32;  // wave 7 lanes of the speculative setup
+#ifndef PAIR_XWAVE
+#define PAIR_XWAVE 1  // the wave that also takes the last chunk (7: wave 7, before the speculative lanes)
+#endif
+typedef const __attribute__((address_space(4))) double* CGeo;
+
+struct PairArgs {
+    LikeArgs L;
+    ElemSpec X;                // candidate selection (X.jk) and speculative lanes (X.nspec, X.S)
+    const double* snap_src;    // nullable: rows [ns][ndim] of the other half of pos, copied to snap_dst
+    double* snap_dst;
+    int spl;                   // speculative lanes per block (<= 64 - PAIR_SPEC_LANE0)
+    int nbc;                   // blocks [0, nbc) carry candidate 0's lanes, the rest candidate 1's
+};
+
+// chunk pairs of waves 0-6 (k_elements' 64-item chunks; chunk 14 is wave 7's):
+// the round-3 per-chunk wave durations (profiles/r03/elem_timeline_c2_w.txt)
+// paired long with short, 20.8-21.8 us each
+__constant__ int kPairChunks[7][2] = {{12, 1}, {6, 0}, {11, 2}, {10, 3}, {4, 8}, {5, 9}, {13, 7}};
+
+#ifdef LFG_PROFILE_PAIR  // diagnostic build only: s_memrealtime (100 MHz) stamps of each block's phases
+__device__ unsigned long long g_pair_t[20][4096];
+#define PAIR_STAMP(slot, cond)                                                     \
+    do {                                                                           \
+        if ((cond) && blockIdx.x < 4096) g_pair_t[slot][blockIdx.x] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define PAIR_STAMP(slot, cond)
+#endif
+
+__global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
+{
+    const LikeArgs& L = A.L;
+    const ElemSpec& X = A.X;
+    __shared__ double sgeo[LFG_NGEO];
+    __shared__ double swr[NWD_RINGS + NDISC_R];
+    __shared__ double swn[NWD_RINGS + NDISC_R];
+    __shared__ double swt[NDISC_R + 1];           // disc ring weights and the disc total (ring-weight lanes)
+    __shared__ double sbw[NBS];
+    __shared__ double2 sab[NBS];
+    __shared__ double sdq[U_DON * DON_STRIDE];
+    __shared__ double sacc1[3];
+    __shared__ double snorm[4];
+    __shared__ TileBufs TA;
+    __shared__ double sph[LIKE_TILE];
+    // the WD/disc intervals live here from the element phase until every
+    // thread has its sweep items in registers; then the second difference
+    // arrays and the point-phase cells (unless the tile goes point-major,
+    // which reads the intervals in its pass)
+    __shared__ union PairU_ {
+        struct {
+            unsigned long long X[2][LIKE_TILE + 1];
+            int scp[LIKE_NC + 1];
+        } s;
+        double2 ab[NU_WDD];
+    } SU;
+    __shared__ unsigned long long sacc[6][LIKE_TILE + 1];
+    __shared__ long long spart[6][LIKE_THREADS / 64];
+    __shared__ double red[3][LIKE_THREADS / 64];
+    __shared__ int sflag[2];
+    __shared__ double sq[ACC_LDS];
+    __shared__ double sy[LIKE_TILE], sye[LIKE_TILE];
+
+    constexpr int nt = LIKE_THREADS, nw = LIKE_THREADS / 64;
+    const int pair = blockIdx.x, npairs = L.npairs;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    PAIR_STAMP(0, tid == 0);
+#ifdef LFG_PROFILE_PAIR
+    if (tid == 0 && blockIdx.x < 4096) {
+        unsigned hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        g_pair_t[14][blockIdx.x] = hw;
+    }
+#endif
+    const int E = L.E;
+    const int w = (E == 1) ? pair : pair / E, e = (E == 1) ? 0 : pair - w * E;
+    const int nwk = npairs / E;  // walkers of the batch
+    const bool offs = L.off && E > 1;
+    const int o0 = offs ? L.off[e] : 0;
+    const int n = offs ? L.off[e + 1] - o0 : L.N;
+
+    // ---- prologue: the pair's candidate (speculative setup) or standard slots
+    const double* G;
+    int st0, bst;
+    double lpr = 0.0, zf = 0.0;
+    const double* qsrc = L.qprop ? L.qprop + size_t(w) * L.ndim : nullptr;
+    if (X.jk) {
+        const int cand = __builtin_amdgcn_readfirstlane(X.accflag[X.jk[w]]);
+        const size_t cp = size_t(cand) * npairs + pair, cw = size_t(cand) * nwk + w;
+        G = X.geoC + cp * LFG_NGEO;
+        st0 = X.statusC[cp];
+        bst = X.bstatusC[cp];
+        lpr = X.priorC[cw];
+        zf = X.zfC[cw];
+        qsrc = X.qC + cw * X.ndim;
+        // the selected candidate into the standard slots (API readers, k_combine_walkers)
+        double* Gd = const_cast<double*>(L.geo) + size_t(pair) * LFG_NGEO;
+        if (tid < LFG_NGEO) Gd[tid] = G[tid];
+        if (tid == LFG_NGEO) X.bstatus[pair] = bst;
+        if (e == 0) {
+            for (int d = tid; d < X.ndim; d += nt) X.q[size_t(w) * X.ndim + d] = qsrc[d];
+            if (tid == LFG_NGEO + 1) X.prior[w] = lpr;
+            if (tid == LFG_NGEO + 2) X.zf[w] = zf;
+        }
+    } else {
+        G = L.geo + size_t(pair) * LFG_NGEO;
+        st0 = L.status[pair];
+        bst = L.bstatus[pair];
+        if (L.prior) lpr = L.prior[w];
+        if (L.zfac) zf = L.zfac[w];
+    }
+    // the record through the constant address space: its reads are scalar
+    // loads into SGPRs, as in k_elements (the launch writes no record it
+    // reads: the standard slot it copies into is not G when X.jk is set)
+    const CGeo Gc = (CGeo)(G);
+    const int stp = (st0 != ST_OK) ? st0 : bst;  // MODEL_SPEC 6 order: setup failures first
+    if (tid == LFG_NGEO + 3) const_cast<int*>(L.status)[pair] = stp;
+    const bool prej = L.prior && prior_rejects(lpr, G);
+    const int st = (stp == ST_OK && prej) ? -1 : stp;  // -1: prior-rejected, straight to the -inf finish
+    if (tid < LFG_NGEO) sgeo[tid] = G[tid];
+    // the other half's rows for the next launch's speculative lanes
+    if (A.snap_dst && e == 0)
+        for (int d = tid; d < L.ndim; d += nt) A.snap_dst[size_t(w) * L.ndim + d] = A.snap_src[size_t(w) * L.ndim + d];
+    const bool acc1 = L.pos && E == 1;
+    if (acc1 && tid < L.ndim && tid < ACC_LDS) sq[tid] = qsrc[tid];
+    if (acc1 && tid == nt - 1) {
+        const uint4 r = draw(L.seed, L.step, L.half, 1, pair);
+        sacc1[0] = log(u53(r.x, r.y));
+        sacc1[1] = zf;
+        sacc1[2] = L.lnp_ens[L.half * npairs + pair];
+    }
+    // this thread's point (one tile: m = n points) into LDS; its window is
+    // formed after the element phase (nothing held in registers through it)
+    const bool own = tid < n;
+    if (own) {
+        sph[tid] = L.x[o0 + tid];
+        TA.iw[tid] = L.w ? L.w[o0 + tid] : 0.0;
+        sy[tid] = L.y[o0 + tid];
+        sye[tid] = L.ye[o0 + tid];
+    }
+    for (int i = 0; i < 6; ++i) sacc[i][tid] = 0ull;
+    if (tid == 0) {
+        for (int i = 0; i < 6; ++i) sacc[i][nt] = 0ull;
+        sflag[0] = 0;
+        sflag[1] = 0;
+    }
+
+    // ---- element phase
+    if (st == ST_OK) {
+        const ElemOut O{SU.ab, sab, sdq, swt, sbw};
+#define G Gc
+        if (wv < 7) {
+            // two straight calls, not a loop: a loop's invariant constants
+            // (the transcendental polynomials) would be hoisted and spilled
+            element_item(kPairChunks[wv][0] * 64 + lane, G, O);
+            element_item(kPairChunks[wv][1] * 64 + lane, G, O);
+        }
+        // the last chunk (4 donor tiles, the 21 ring-weight lanes): after
+        // the lightest pair of chunks (wave PAIR_XWAVE), or wave 7's own
+        // before its speculative lanes
+        if (wv == PAIR_XWAVE) {
+            if (lane < 4) element_item(14 * 64 + lane, G, O);
+            else if (lane < 4 + NDISC_R + 1) ring_weight_lane(lane - 4, G, swt);
+        }
+#undef G
+    }
+    static_assert(14 * 64 + 4 == NUNIQ, "wave 7 holds the last chunk");
+    PAIR_STAMP(16, wv == 7 && lane == 0);
+    if (wv == 7 && lane >= PAIR_SPEC_LANE0 && lane < PAIR_SPEC_LANE0 + A.spl && X.nspec > 0) {
+        // speculative setup lanes of the next half (candidate uniform per block)
+        const int c = pair < A.nbc ? 0 : 1;
+        const int t = (pair - c * A.nbc) * A.spl + (lane - PAIR_SPEC_LANE0);
+        if (t < X.nspec) setup_any(X.S[__builtin_amdgcn_readfirstlane(c)], t);
+#ifdef LFG_PROFILE_PAIR
+        if (lane == PAIR_SPEC_LANE0 && blockIdx.x < 4096) {
+            const int np = X.S[0].W * X.S[0].E;
+            g_pair_t[17][blockIdx.x] = t >= X.nspec ? 9 : (t < np ? 0 : (t < np + X.S[0].W ? 1 : 2));
+        }
+#endif
+    }
+    PAIR_STAMP(1 + wv, lane == 0);
+    __syncthreads();  // B1: the tables, swt, sflag reset, windows
+    PAIR_STAMP(9, tid == 0);
+
+    if (st != ST_OK) {
+        if (tid == 0) L.lle[pair] = -INFINITY;
+        finish_walker(L, pair, tid, acc1, sq, sacc1, sflag);
+        return;
+    }
+    // ---- likelihood phase (k_lnlike<1, false>, one tile)
+    const double wk = own ? TA.iw[tid] : 0.0;
+    const double phc = wrap_phase(own ? sph[tid] - sgeo[G_PHI0] : 0.0);
+    int flA = put_window(TA, tid, own, phc, wk);
+    if (own) sph[tid] = phc;
+    __syncthreads();  // B1b: the windows
+    flA |= check_sorted(TA, tid, own);
+    const int flB = (flA & 7) | ((own && tid && sph[tid] < sph[tid - 1]) ? 4 : 0);
+    {
+        const int wfA = wave_or4(flA), wfB = wave_or4(flB);
+        if (lane == 0 && wfA) atomicOr(&sflag[0], wfA);
+        if (lane == 0 && wfB) atomicOr(&sflag[1], wfB);
+    }
+    const int m = n;
+    if (m > 0) build_cells(TA.lo, m, TA.cell, tid);
+    const double s = sgeo[G_S], c = sgeo[G_C], ul = sgeo[G_ULIMB];
+    const double td = swt[NDISC_R];
+    constexpr int NI = (NWD + NDISC + nt - 1) / nt;
+    double2 abk[NI];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        const int g = tid + i * nt;
+        abk[i] = (g < NWD + NDISC) ? sweep_ab(SU.ab, g) : make_double2(1.0, -1.0);
+    }
+    double tb = 0.0, dn = 0.0, vs = 0.0, wring = 0.0;
+    if (tid < NBS) {
+        tb = sbw[tid];
+    } else if (tid >= nt - NDONOR) {
+        // donor normalisation at quadrature (theta = pi/2): e = (0, -s, c)
+        const int t = tid - (nt - NDONOR), mr = t & 3;
+        const double* dq = sdq + (t >> 2) * DON_STRIDE;
+        const double vy = (mr & 1) ? -dq[1] : dq[1], vz = (mr & 2) ? -dq[2] : dq[2];
+        dn = fmax(-s * vy + c * vz, 0.0);
+        vs = fabs(dq[0]) + fabs(dq[1]) + fabs(dq[2]);
+    }
+    if (tid >= NBS && tid < NBS + NWD_RINGS) wring = wd_ring_weight(tid - NBS, ul);
+    else if (tid >= NBS + NWD_RINGS && tid < NBS + NWD_RINGS + NDISC_R) wring = swt[tid - NBS - NWD_RINGS];
+    if (tid >= NBS && tid < NBS + NWD_RINGS + NDISC_R) swr[tid - NBS] = wring;
+    tb = wave_sum(tb);
+    dn = wave_sum(dn);
+    vs = wave_sum(vs);
+    if (lane == 0) { red[0][wv] = tb; red[1][wv] = dn; red[2][wv] = vs; }
+    __syncthreads();  // B2: every read of SU.ab (unless point-major), the flags, the partials
+    PAIR_STAMP(10, tid == 0);
+    if (wv == 0) {
+        double p0 = 0.0, p1 = 0.0, p2 = 0.0;
+        if (lane < nw) { p0 = red[0][lane]; p1 = red[1][lane]; p2 = red[2][lane]; }
+        p0 = wave_sum(p0);
+        p1 = wave_sum(p1);
+        p2 = wave_sum(p2);
+        if (lane == 0) {
+            snorm[0] = 1.0 / p0;
+            snorm[1] = 1.0 / p2;
+            snorm[2] = p1;
+            snorm[3] = p2;
+        }
+    }
+    const double twd = TWO_PI * ((1.0 - ul) * 0.5 + ul / 3.0);  // 2 pi [F(1) - F(0)]
+    if (tid >= NBS && tid < NBS + NWD_RINGS + NDISC_R)
+        swn[tid - NBS] = wring * ((tid - NBS < NWD_RINGS) ? 1.0 / twd : 1.0 / td);
+    const bool dir = (sflag[0] & 7) != 0 || sflag[1] != 0;
+    if (!dir) {
+        SU.s.X[0][tid] = 0ull;
+        SU.s.X[1][tid] = 0ull;
+        if (tid == 0) { SU.s.X[0][nt] = 0ull; SU.s.X[1][nt] = 0ull; }
+        if (m > 0) build_cells(sph, m, SU.s.scp, tid);
+    }
+    __syncthreads();  // B3
+    PAIR_STAMP(11, tid == 0);
+    double chi = 0.0;
+    if (n > 0) {
+        double fw = 0.0, fd = 0.0, eb = 0.0, R3 = 0.0, R4 = 0.0, R5 = 0.0;
+        if (dir) {
+            if (own) {
+                const double2 f2 = direct_wd_disc(SU.ab, swr, phc, wk, twd, td);
+                fw = f2.x;
+                fd = f2.y;
+                eb = direct_spot(sab, sbw, phc, wk, snorm[0]);
+            }
+        } else {
+            const PhaseIndex XI = phase_index(TA.lo, TA.cell, m);
+            double qx[2 * NI];
+            int J[2 * NI], Jb[2 * NI];
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                qx[2 * i] = abk[i].x;
+                qx[2 * i + 1] = abk[i].y;
+            }
+            count_lt_multi<2 * NI>(XI, qx, J);
+            count_le_back_multi<2 * NI>(TA.hi, qx, J, Jb);
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+                if (abk[i].x < abk[i].y) {
+                    const int g = tid + i * nt;
+                    const int u = uitem(g < NU_WDD ? g : g - NU_WDD);
+                    apply_runs(Runs{Jb[2 * i], J[2 * i], Jb[2 * i + 1], J[2 * i + 1]}, abk[i].x, abk[i].y,
+                               swn[uring(u)], XI, TA.hi, TA.iw, ((lane & 1) ? SU.s.X : sacc)[(u < U_WD) ? 0 : 1]);
+                }
+            sweep_spot_donor(tid, XI, TA, phase_index(sph, SU.s.scp, m), sab, sbw, snorm[0], sdq, snorm[1], sacc + 2);
+            __syncthreads();  // B4
+            long long r[6] = {0, 0, 0, 0, 0, 0};
+            block_scan<6>(sacc, spart, tid, r, SU.s.X);
+            PAIR_STAMP(12, tid == 0);
+            fw = double(r[0]) * FX_INV;
+            fd = double(r[1]) * FX_INV;
+            eb = double(r[2]) * FX_INV;
+            R3 = double(r[3]);
+            R4 = double(r[4]);
+            R5 = double(r[5]);
+        }
+        const double sg = sgeo[G_S], cg = sgeo[G_C];
+        const double bden = sgeo[G_BDEN], fis = sgeo[G_FIS];
+        const double2 scp2 = sincospi_ool(2.0 * phc);
+        const double e0 = sg * scp2.y, e1 = -sg * scp2.x;
+        double D = 0.0;
+        if (!dir) D = (e0 * R3 + e1 * R4 + cg * R5) * (FX_INV * snorm[3]);
+        else if (own) D = direct_donor(sdq, e0, e1, cg);
+        double beam = 0.0;
+        if (bden > 0.0) beam = (fis + (1.0 - fis) * fmax(sgeo[G_NB0] * e0 + sgeo[G_NB1] * e1 + sgeo[G_NB2] * cg, 0.0)) / bden;
+        const double sbs = beam * (1.0 - eb), srs = D / snorm[2];
+        if (own) {
+            const double f = sgeo[G_WDF] * (1.0 - fw) + sgeo[G_DF] * (1.0 - fd) + sgeo[G_SF] * sbs + sgeo[G_RSF] * srs;
+            const double rr = (sy[tid] - f) / sye[tid];
+            chi = isnan(f) ? INFINITY : rr * rr;
+        }
+    }
+    chi = wave_sum(chi);
+    if (lane == 0) red[1][wv] = chi;
+    __syncthreads();
+    if (tid == 0) {
+        double tot = 0.0;
+        for (int i = 0; i < nw; ++i) tot += red[1][i];
+        L.lle[pair] = -0.5 * tot;
+    }
+    PAIR_STAMP(13, tid == 0);
+    finish_walker(L, pair, tid, acc1, sq, sacc1, sflag);
+    PAIR_STAMP(15, tid == 0);
+}
+
 // -------------------------------------------------------------- k_gp_dcp
 // GP trees: the changepoint distance of pairs whose walker tripped the
 // cache rule (k_setup marked them G_GP_OK = 2): dist_cp = (dphi + phi4 -
@@ -3169,7 +3560,7 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
         const size_t P48 = size_t(npairs) * LFG_NGEO;
         if (sp->in) {
             X.jk = ws.jk + size_t(h) * W;
-            X.accflag = ws.accflag;
+            X.accflag = ws.accflag + size_t(hn) * ws.accstride;  // the partner half's acceptances
             X.geoC = ws.geoC + 2 * h * P48;
             X.statusC = ws.statusC + 2 * h * size_t(npairs);
             X.bstatusC = ws.bstatusC + 2 * h * size_t(npairs);
@@ -3202,7 +3593,21 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
             X.nspecblk = (2 * ((X.nspec + ELEM_BLOCK - 1) / ELEM_BLOCK) + 7) / 8 * 8;  // keeps the pair -> XCD map
         }
     }
-    int rc = run_front(S, ws, st, ev, true, &X, !(sp && sp->in));
+    // k_pair: the element solve and the likelihood of a pair in one
+    // workgroup (one-tile eclipses, S = 1, no GP); the speculative lanes must
+    // fit wave 7's spare lanes
+    static const bool pair_env = [] {
+        const char* e = getenv("LFG_PAIR");
+        return e && e[0] == '1';
+    }();
+    int spl = 0, nbc = 0;
+    if (X.nspec > 0 && npairs >= 2) {
+        nbc = (npairs + 1) / 2;
+        spl = (X.nspec + (npairs - nbc) - 1) / (npairs - nbc);
+    }
+    const bool pair_path = pair_env && !T->gp && T->nsub == 1 && T->max_n <= LIKE_TILE && T->ndim <= LIKE_THREADS &&
+                           (X.nspec == 0 || (npairs >= 2 && spl <= 64 - PAIR_SPEC_LANE0));
+    int rc = run_front(S, ws, st, ev, !pair_path, &X, !(sp && sp->in));
     if (rc) return rc;
     double* lle = lnlike_e ? lnlike_e : ws.lle;
     LikeArgs L{ws.geo, ws.status, ws.ab, ws.donor, ws.wts, T->E, T->off, T->max_n, T->x, T->y, T->ye,
@@ -3211,8 +3616,34 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
                T->ndim, acc ? acc->half : 0, acc ? acc->seed : 0ull, acc ? acc->step : 0ull,
                acc ? acc->naccept : nullptr};
     L.bstatus = ws.bstatus;
-    L.accflag = (sp && acc) ? ws.accflag : nullptr;  // sharded: k_accept_regen records them
+    // sharded: k_accept_regen records them
+    L.accflag = (sp && acc) ? ws.accflag + size_t(prop->half) * ws.accstride : nullptr;
     L.combine = T->E == 1;  // E > 1: k_combine_walkers after the likelihood kernels
+    if (pair_path) {
+        PairArgs A{L, X, nullptr, nullptr, spl, nbc};
+        if (sp && sp->out && acc && T->E == 1) {
+            // this launch accepts moves of half h while its speculative lanes
+            // read half h's rows: they read the snapshot of them instead (taken
+            // by the launch before, or here), and the launch snapshots half 1 - h
+            const int h = prop->half, hn = 1 - h, ns = prop->ns;
+            const size_t rows = size_t(ns) * T->ndim;
+            double* snap_h = ws.snap + size_t(h) * ws.accstride * T->ndim;
+            if (!sp->in && hipMemcpyAsync(snap_h, prop->pos + size_t(h) * rows, rows * sizeof(double),
+                                          hipMemcpyDeviceToDevice, st) != hipSuccess)
+                return LFG_E_LAUNCH;
+            A.X.S[0].ppos = A.X.S[1].ppos = snap_h;
+            A.snap_src = prop->pos + size_t(hn) * rows;
+            A.snap_dst = ws.snap + size_t(hn) * ws.accstride * T->ndim;
+        }
+        hipLaunchKernelGGL(k_pair, dim3(npairs), dim3(LIKE_THREADS), 0, st, A);
+        if ((rc = launch_ok())) return rc;
+        if (T->E > 1) {
+            hipLaunchKernelGGL(k_combine_walkers, dim3((W + 3) / 4), dim3(256), 0, st, L);
+            if ((rc = launch_ok())) return rc;
+        }
+        mark(3);
+        return LFG_OK;
+    }
     if (T->gp) {
         L.res = ws.res;
         L.gpx = ws.gpx;
@@ -3375,7 +3806,8 @@ int lfg_stretch_accept_regen_spec(double* pos, double* lnp, int W, int half, dou
     if (!wsp || ws_bytes < ws.total) return LFG_E_WORKSPACE;
     const int ns = W / 2;
     hipLaunchKernelGGL(k_accept_regen, dim3((ns + 63) / 64), dim3(64), 0, static_cast<hipStream_t>(stream), pos,
-                       lnp, W, T->ndim, half, a, lnp_new, seed, step, naccept, ws.accflag);
+                       lnp, W, T->ndim, half, a, lnp_new, seed, step, naccept,
+                       ws.accflag + size_t(half) * ws.accstride);
     return launch_ok();
 }
 
@@ -3503,6 +3935,14 @@ int lfg_debug_like_waves(unsigned long long* host)
 }
 #endif
 
+#ifdef LFG_PROFILE_PAIR
+// diagnostic build only: k_pair's phase stamps of the last launch, host [20][4096]
+int lfg_debug_pair(unsigned long long* host)
+{
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pair_t), sizeof(g_pair_t)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 #ifdef LFG_PROFILE_ELEM
 // diagnostic build only: k_elements' per-wave stamps of the last launch, host [4][32768]
 int lfg_debug_elem_waves(unsigned long long* host)
@@ -3519,7 +3959,15 @@ int lfg_debug_setup_cycles(unsigned long long* host)
 }
 #endif
 
-const char* lfg_version(void) { return "lfg 0.3.0 gfx950 fp64"; }
+// the hash of the sources and flags this library was built from
+// (lfit_python_amd._native.source_hash, passed by build()); the tag string
+// lets build() read it back from the file without loading it
+#ifndef LFG_SRC_HASH
+#define LFG_SRC_HASH "unhashed"
+#endif
+__attribute__((used)) const char lfg_src_hash_tag[] = "lfg-src-hash:" LFG_SRC_HASH;
+
+const char* lfg_version(void) { return "lfg 0.4.0 gfx950 fp64 layout=pair src=" LFG_SRC_HASH; }
 
 #ifdef LFG_COUNT_ITERS
 // diagnostic builds only: read and clear the iteration counters of k_elements

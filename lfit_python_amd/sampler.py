@@ -124,8 +124,15 @@ class EnsembleSampler:
         # so the production run after reset() never replays burn-in draws
         # (the reference hands the burn-in RNG state on, mcmc_utils.py:135-183)
         self.rng_step = 0
-        self._chunks = []  # stored chain: device (chain [n, W, ndim], lnprob [n, W]) per run
+        # stored chain: (chain [n, W, ndim], lnprob [n, W]) per stored run.  A run
+        # fills a device chunk (the steps stay free of host syncs); when it ends
+        # the chunk moves to host memory, as emcee keeps its chain in
+        # RAM, so device memory holds one run's chunk at a time however long
+        # the chain grows (offload = False keeps every chunk on the device)
+        self._chunks = []
         self._cat = None
+        self._last = None  # the most recent run's chunk (None: it stored nothing)
+        self.offload = True
         self.timer = None  # optional callable(walkers) -> lnp used instead of self.ev
         # one process, HIP moves, an evaluator with the fused entry: proposal,
         # ln_prob and acceptance in one launch sequence (lfg_stretch_step_half);
@@ -361,13 +368,24 @@ class EnsembleSampler:
             self.set_state(p0, lnprob0)
         thin = max(1, int(thin))
         if not store:
+            self._last = None
             return None, thin
         n = -(-int(iterations) // thin)  # steps i with i % thin == 0 (emcee 2.x stores those)
         buf = (torch.empty((n, self.W, self.ndim), dtype=torch.float64, device=self.dev),
                torch.empty((n, self.W), dtype=torch.float64, device=self.dev))
         self._chunks.append(buf)
+        self._last = buf
         self._cat = None
         return buf, thin
+
+    def _end(self, buf):
+        """end of a stored run: its device chunk moves to host memory (offload)"""
+        if buf is None or not self.offload or self.dev.type != "cuda":
+            return
+        host = tuple(t.cpu() for t in buf)
+        self._chunks = [host if c is buf else c for c in self._chunks]
+        self._last = host
+        self._cat = None
 
     def _store(self, buf, i, thin):
         if buf is not None and i % thin == 0:
@@ -388,6 +406,8 @@ class EnsembleSampler:
         for i in range(int(iterations)):
             self.step()
             self._store(buf, i, thin)
+            if i == int(iterations) - 1:
+                self._end(buf)
             yield _host(self.pos), _host(self.lnp), self.random_state
 
     def run_mcmc(self, pos0, N, rstate0=None, lnprob0=None, storechain=True, store=None, thin=1, **kwargs):
@@ -399,45 +419,50 @@ class EnsembleSampler:
         for i in range(int(N)):
             self.step()
             self._store(buf, i, thin)
+        self._end(buf)
         return _host(self.pos), _host(self.lnp), self.random_state
 
     def _concat(self):
+        """the stored chain as one (chain, lnprob) pair, wherever the chunks
+        live (host after offload); not cached in place of the chunks"""
         import torch
         if self._cat is None:
             if not self._chunks:
-                self._cat = (torch.empty((0, self.W, self.ndim), dtype=torch.float64, device=self.dev),
-                             torch.empty((0, self.W), dtype=torch.float64, device=self.dev))
+                self._cat = (torch.empty((0, self.W, self.ndim), dtype=torch.float64),
+                             torch.empty((0, self.W), dtype=torch.float64))
             elif len(self._chunks) == 1:
                 self._cat = self._chunks[0]
             else:
-                self._cat = (torch.cat([c for c, _ in self._chunks]), torch.cat([l for _, l in self._chunks]))
-                self._chunks = [self._cat]
+                self._cat = (torch.cat([c.cpu() for c, _ in self._chunks]),
+                             torch.cat([l.cpu() for _, l in self._chunks]))
         return self._cat
 
     @property
     def chain_dev(self):
-        """the stored chain on the device, step-major [nsteps, W, ndim]"""
-        return self._concat()[0]
+        """the stored chain on the device, step-major [nsteps, W, ndim] (an
+        upload of the host chunks when they were offloaded)"""
+        return self._concat()[0].to(self.dev)
 
     @property
     def lnprob_dev(self):
         """the stored ln_prob on the device, [nsteps, W]"""
-        return self._concat()[1]
+        return self._concat()[1].to(self.dev)
 
     def last_run(self):
-        """(chain [n, W, ndim], lnprob [n, W]) device views of the most recent
-        stored sample()/run_mcmc() call (bulk chain_prod.txt writes)"""
-        return self._chunks[-1] if self._chunks else self._concat()
+        """(chain [n, W, ndim], lnprob [n, W]) of the most recent
+        sample()/run_mcmc() call, None if that call stored nothing (bulk
+        chain_prod.txt writes; host tensors once the run was offloaded)"""
+        return self._last
 
     @property
     def chain(self):
         """emcee's chain: host array (nwalkers, nsteps, ndim)"""
-        return _host(self.chain_dev.permute(1, 0, 2).contiguous())
+        return _host(self._concat()[0].permute(1, 0, 2))
 
     @property
     def lnprobability(self):
         """emcee's lnprobability: host array (nwalkers, nsteps)"""
-        return _host(self.lnprob_dev.t().contiguous())
+        return _host(self._concat()[1].t())
 
     @property
     def flatchain(self):
@@ -467,6 +492,7 @@ class EnsembleSampler:
         self.naccept.zero_()
         self._chunks = []
         self._cat = None
+        self._last = None
 
     @property
     def random_state(self):

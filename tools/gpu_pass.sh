@@ -35,8 +35,8 @@ for s in $steps; do
     xch)   args+=("${tag}_xch:200:python3 bench.py --exchange-path --no-cpu > $O/${tag}_c2_xch.json") ;;
     p5)    args+=("${tag}_p5:300:rocprofv3 --kernel-trace --stats -d $O/${tag}_prof5 -o run --output-format csv -- python3 bench.py --config 5 --steps 6 --warmup 2 --no-cpu") ;;
     pgp)   args+=("${tag}_pgp:200:rocprofv3 --kernel-trace --stats -d $O/${tag}_profgp -o run --output-format csv -- python3 bench.py --config gp --steps 30 --warmup 3 --no-cpu") ;;
-    tl2)   args+=("${tag}_tl2:200:LFG_LIB=$E/liblfg_ELEMPROF.so python3 tools/elem_timeline.py --config 2") ;;
-    like2) args+=("${tag}_like2:200:LFG_LIB=$E/liblfg_LIKEPROF.so python3 tools/like_profile.py 512 300 1") ;;
+    tl2)   args+=("${tag}_tl2:200:LFG_DIAGNOSTIC=1 LFG_LIB=$E/liblfg_ELEMPROF.so python3 tools/elem_timeline.py --config 2") ;;
+    like2) args+=("${tag}_like2:200:LFG_DIAGNOSTIC=1 LFG_LIB=$E/liblfg_LIKEPROF.so python3 tools/like_profile.py 512 300 1") ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -1,0 +1,65 @@
+"""Diagnostic: phase stamps of k_pair (build with -DLFG_PROFILE_PAIR:
+tools/build_exp.sh PAIRPROF -DLFG_PROFILE_PAIR; load with LFG_DIAGNOSTIC=1
+LFG_LIB=build/exp/liblfg_PAIRPROF.so).  Runs config-2 chain steps as bench.py
+does and prints, for the last launch, each phase's end relative to the
+block's start (us, 100 MHz s_memrealtime): the eight waves' element-phase
+ends (wave 7: the last chunk + the speculative setup lanes), the barriers,
+the sweep + scan, chi^2 and the finish."""
+import ctypes
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from lfit_python_amd import _native, batch, sampler, synthetic  # noqa: E402
+from lfit_python_amd.lfit import flux_batch  # noqa: E402
+
+dev = torch.device("cuda", 0)
+W = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+L = _native.lib()
+
+
+def flux_fn(pars, x, w, nsub):
+    f, st = flux_batch(np.asarray(pars)[None, :], x, w, nsub=nsub, device=dev)
+    return f[0].cpu().numpy()
+
+
+model = synthetic.config_single(npts=300, flux_fn=flux_fn)
+tree = batch.compile_tree(model)
+ev = batch.LnProbEvaluator(tree, device=dev, max_walkers=W)
+p0 = np.array(model.dynasty_par_vals)
+init = sampler.initialise_walkers(p0, sampler.comp_scatter(model.dynasty_par_names, 0.1), W,
+                                  lambda p: ev(torch.as_tensor(p, device=dev)).cpu().numpy(), seed=20261015)
+S = sampler.EnsembleSampler(W, tree.ndim, ev, seed=20261015)
+S.set_state(init)
+for _ in range(10):
+    S.step()
+torch.cuda.synchronize()
+t = np.zeros((20, 4096), dtype=np.uint64)
+assert L.lfg_debug_pair(ctypes.c_void_p(t.ctypes.data)) == 0
+nb = W // 2
+t = t[:, :nb].astype(np.float64)
+t0 = t[0]
+span = (t[15].max() - t0.min()) / 100.0
+print("blocks %d, launch span %.2f us (first start -> last finish)" % (nb, span))
+print("block start spread: %s us" % np.percentile((t0 - t0.min()) / 100.0, [0, 50, 90, 100]).round(2))
+rows = [("wave %d elements" % k, 1 + k) for k in range(8)] + [
+    ("B1 (phase barrier)", 9), ("B2 (items, norms)", 10), ("B3 (cells)", 11), ("sweep + scan", 12),
+    ("chi^2", 13), ("finish", 15)]
+for name, k in rows:
+    d = (t[k] - t0) / 100.0
+    print("%-22s median %7.2f  p90 %7.2f  max %7.2f us" % (name, np.median(d), np.percentile(d, 90), d.max()))
+kind = t[17].astype(int)
+for k, nm in ((0, "setup"), (1, "prior"), (2, "stream")):
+    m = kind == k
+    if m.any():
+        pre = (t[16][m] - t0[m]) / 100.0
+        spec = (t[8][m] - t[16][m]) / 100.0
+        fin_k = (t[15][m] - t0[m]) / 100.0
+        print("spec kind %-6s blocks %3d: wave 7 pre-spec median %6.2f | spec part median %6.2f p90 %6.2f max %6.2f"
+              " | block finish median %6.2f max %6.2f" % (nm, m.sum(), np.median(pre), np.median(spec),
+                                                        np.percentile(spec, 90), spec.max(), np.median(fin_k), fin_k.max()))
+fin = (t[15] - t0.min()) / 100.0
+print("block finish times from launch start: %s us" % np.percentile(fin, [0, 10, 50, 90, 100]).round(2))
