@@ -20,6 +20,8 @@
 #include <cmath>
 #include <vector>
 
+#include "lfg.h"
+#include "lfg_cpu.h"
 #include "lfg_device.hpp"
 #include "lfg_tables.hpp"
 
@@ -598,6 +600,70 @@ int lfc_lnprob_batch_gp(const double* walkers, int W, int ndim, int E, const int
         delete T;
     }
     return used;
+}
+
+}  // extern "C"
+
+// per parameter set: setup, elements, then f(pair, tables) -> its outputs
+template <typename F>
+static int per_set(const double* pars, int W, int P, int* status, int nthreads, F f)
+{
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel num_threads(nthreads)
+    {
+        std::vector<double> buf;
+        Tables* T = new Tables;
+#pragma omp for schedule(dynamic, 1)
+        for (int i = 0; i < W; ++i) {
+            Pair G{};
+            double rp;
+            const int st = setup_pair(pars + size_t(i) * P, P, G, rp);
+            if (status) status[i] = st;
+            if (st == ST_OK) elements(G, *T);
+            f(i, st, G, *T, buf);
+        }
+        delete T;
+    }
+    return LFG_OK;
+}
+
+extern "C" {
+
+// ---- the lfg_cpu_* twins of include/lfg.h's entry points (lfg_cpu.h):
+// host pointers, the same argument meaning and status codes
+int lfg_cpu_flux(const double* pars, int W, int P, const double* x, const double* w, int N, int nsub, double* flux,
+                 int* status, int nthreads)
+{
+    if (W <= 0 || N < 0 || nsub < 1 || (P != 14 && P != 18) || !pars || !flux || (N > 0 && !x)) return LFG_E_ARGS;
+    return per_set(pars, W, P, status, nthreads,
+                   [&](int i, int st, const Pair& G, const Tables& T, std::vector<double>& buf) {
+                       double* f = flux + size_t(i) * N;
+                       if (st != ST_OK) { std::fill(f, f + N, NAN); return; }
+                       chisq(G, T, x, w, nullptr, nullptr, N, nsub, buf, f);
+                   });
+}
+
+int lfg_cpu_lnlike(const double* pars, int W, int P, const double* x, const double* w, int N, int nsub,
+                   const double* y, const double* ye, double* lnlike, int* status, int nthreads)
+{
+    if (W <= 0 || N < 0 || nsub < 1 || (P != 14 && P != 18) || !pars || !lnlike || (N > 0 && (!x || !y || !ye)))
+        return LFG_E_ARGS;
+    return per_set(pars, W, P, status, nthreads,
+                   [&](int i, int st, const Pair& G, const Tables& T, std::vector<double>& buf) {
+                       lnlike[i] = (st != ST_OK) ? -INFINITY : -0.5 * chisq(G, T, x, w, y, ye, N, nsub, buf);
+                   });
+}
+
+int lfg_cpu_lnprob(const double* walkers, int W, const lfg_tree* T, double* lnp, int nthreads)
+{
+    if (W <= 0 || !T || T->E <= 0 || T->ndim <= 0 || !walkers || !lnp) return LFG_E_ARGS;
+    lfc_lnprob_batch_gp(walkers, W, T->ndim, T->E, T->gather, T->npars, T->consts, T->off, T->x, T->y, T->ye, T->w,
+                        T->nsub, T->prior_type, T->prior_p1, T->prior_p2, T->prior_norm, T->roche_priors,
+                        T->gp ? T->gp_gather : nullptr, T->gp ? T->gp_base : nullptr, T->gp ? T->gp_ecl : nullptr, lnp,
+                        nthreads);
+    if (T->fixed_invalid)
+        for (int i = 0; i < W; ++i) lnp[i] = -INFINITY;
+    return LFG_OK;
 }
 
 }  // extern "C"

@@ -124,6 +124,22 @@ int lfg_flux(const double* pars, int W, int P, const double* x,
              int* status, void* ws, size_t ws_bytes, void* stream);
 
 /*
+ * Fused single-eclipse ln_like, no tree: SimpleEclipse.chisq / ln_like
+ * (CVModel.py:157-191) of W parameter sets against one light curve,
+ * ln_like = -0.5 sum_p ((y_p - flux_p) / ye_p)^2, a NaN flux -> chi^2 = +inf
+ * (CVModel.py:163-171); no flux array is materialised and no prior is
+ * applied (lfg_lnprob adds the priors through a tree).
+ *   pars, x, w, N, nsub, status: as lfg_flux
+ *   y, ye   [dev] N data points and errors
+ *   lnlike  [dev] W (-inf where status != LFG_ST_OK)
+ * Workspace: lfg_workspace_size(W, 1).
+ */
+int lfg_lnlike(const double* pars, int W, int P, const double* x,
+               const double* w, int N, int nsub, const double* y,
+               const double* ye, double* lnlike, int* status, void* ws,
+               size_t ws_bytes, void* stream);
+
+/*
  * Batched emcee log-probability of a whole walker ensemble through a compiled
  * tree: mcmcfit.ln_prob (mcmcfit.py:37-41) -> Node.ln_prob (model.py:476-498)
  * = ln_prior (model.py:426-474 + Roche priors) + sum_e -0.5 chi^2_e

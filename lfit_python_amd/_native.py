@@ -67,7 +67,7 @@ class LfgTree(ctypes.Structure):
     ]
 
 
-EXPORTS = ("lfg_workspace_size", "lfg_workspace_size_tree", "lfg_flux", "lfg_lnprob", "lfg_lnprior", "lfg_lnprob_timed",
+EXPORTS = ("lfg_workspace_size", "lfg_workspace_size_tree", "lfg_flux", "lfg_lnlike", "lfg_lnprob", "lfg_lnprior", "lfg_lnprob_timed",
            "lfg_stretch_lnprob_accept", "lfg_stretch_step_half", "lfg_stretch_step_half_spec",
            "lfg_stretch_step_shard", "lfg_stretch_step_shard_spec", "lfg_stretch_accept_regen_spec",
            "lfg_stretch_accept_regen",
@@ -168,6 +168,8 @@ def lib():
         L.lfg_workspace_size_tree.argtypes = [ip, ctypes.POINTER(LfgTree)]
         L.lfg_flux.restype = ip
         L.lfg_flux.argtypes = [vp, ip, ip, vp, vp, ip, ip, vp, vp, vp, vp, sz, vp]
+        L.lfg_lnlike.restype = ip
+        L.lfg_lnlike.argtypes = [vp, ip, ip, vp, vp, ip, ip, vp, vp, vp, vp, vp, sz, vp]
         L.lfg_lnprob.restype = ip
         L.lfg_lnprob.argtypes = [vp, ip, ctypes.POINTER(LfgTree), vp, vp, vp, sz, vp]
         L.lfg_lnprior.restype = ip

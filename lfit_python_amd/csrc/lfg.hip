@@ -2445,10 +2445,6 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
 // the speculative lanes of other blocks read partner rows of the same half:
 // those lanes read the snapshot (SetupArgs.ppos) that the launch before took
 // of that half, and this launch snapshots the other half for the next one.
-constexpr int PAIR_SPEC_LANE0 = 32;  // wave 7 lanes of the speculative setup
-#ifndef PAIR_XWAVE
-#define PAIR_XWAVE 1  // the wave that also takes the last chunk (7: wave 7, before the speculative lanes)
-#endif
 typedef const __attribute__((address_space(4))) double* CGeo;
 
 struct PairArgs {
@@ -2456,14 +2452,13 @@ struct PairArgs {
     ElemSpec X;                // candidate selection (X.jk) and speculative lanes (X.nspec, X.S)
     const double* snap_src;    // nullable: rows [ns][ndim] of the other half of pos, copied to snap_dst
     double* snap_dst;
-    int spl;                   // speculative lanes per block (<= 64 - PAIR_SPEC_LANE0)
+    int spl;                   // speculative lanes per block (<= 64: wave 0's job 0)
     int nbc;                   // blocks [0, nbc) carry candidate 0's lanes, the rest candidate 1's
 };
 
-// chunk pairs of waves 0-6 (k_elements' 64-item chunks; chunk 14 is wave 7's):
-// the round-3 per-chunk wave durations (profiles/r03/elem_timeline_c2_w.txt)
-// paired long with short, 20.8-21.8 us each
-__constant__ int kPairChunks[7][2] = {{12, 1}, {6, 0}, {11, 2}, {10, 3}, {4, 8}, {5, 9}, {13, 7}};
+// the chunks of k_pair's element jobs 1..15, longest first (spot, outer
+// disc, donor, inner disc, WD: the Newton steps per region)
+__constant__ int kJobChunk[15] = {11, 12, 10, 9, 8, 13, 14, 7, 6, 5, 4, 3, 2, 1, 0};
 
 #ifdef LFG_PROFILE_PAIR  // diagnostic build only: s_memrealtime (100 MHz) stamps of each block's phases
 __device__ unsigned long long g_pair_t[20][4096];
@@ -2592,39 +2587,59 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
         sflag[1] = 0;
     }
 
-    // ---- element phase
+    __shared__ int sjob;
+    if (tid == 0) sjob = 8;
+    __syncthreads();  // B0: sjob
+
+    // ---- element phase: 16 jobs.  Job 0: this block's speculative setup
+    // lanes of the next half; jobs 1..15: the 15 item chunks, longest first
+    // (kJobChunk).  Wave w takes job w, then grabs the next free job from
+    // sjob, at most twice (8 waves x 3 >= 16): the waves finish together
+    // whatever the pair's Newton counts (a static two-chunk split waited
+    // ~8 us at the phase barrier on its slowest wave)
+    if (wv == 0) {
+        if (lane < A.spl && X.nspec > 0) {
+            // candidate uniform per block: X.S[c] stays in scalar registers
+            const int c = pair < A.nbc ? 0 : 1;
+            const int t = (pair - c * A.nbc) * A.spl + lane;
+            if (t < X.nspec) setup_any(X.S[__builtin_amdgcn_readfirstlane(c)], t);
+#ifdef LFG_PROFILE_PAIR
+            if (lane == 0 && blockIdx.x < 4096) {
+                const int np = X.S[0].W * X.S[0].E;
+                g_pair_t[17][blockIdx.x] = t >= X.nspec ? 9 : (t < np ? 0 : (t < np + X.S[0].W ? 1 : 2));
+            }
+#endif
+        }
+    }
     if (st == ST_OK) {
         const ElemOut O{SU.ab, sab, sdq, swt, sbw};
-#define G Gc
-        if (wv < 7) {
-            // two straight calls, not a loop: a loop's invariant constants
-            // (the transcendental polynomials) would be hoisted and spilled
-            element_item(kPairChunks[wv][0] * 64 + lane, G, O);
-            element_item(kPairChunks[wv][1] * 64 + lane, G, O);
-        }
-        // the last chunk (4 donor tiles, the 21 ring-weight lanes): after
-        // the lightest pair of chunks (wave PAIR_XWAVE), or wave 7's own
-        // before its speculative lanes
-        if (wv == PAIR_XWAVE) {
-            if (lane < 4) element_item(14 * 64 + lane, G, O);
-            else if (lane < 4 + NDISC_R + 1) ring_weight_lane(lane - 4, G, swt);
-        }
-#undef G
+        // chunk c: items v = 64 c + lane (c < 13: WD, disc, spot; 13: donor;
+        // 14: the last 36 donor tiles and the 21 ring-weight lanes)
+        auto chunk = [&](int j) {
+            const int c = kJobChunk[j - 1];
+            int v = -1, rb = -1;
+            if (c < 13) v = (c * 64 + lane < U_WD + U_DISC + U_BS) ? c * 64 + lane : -1;
+            else if (c == 13) v = U_WD + U_DISC + U_BS + lane;
+            else if (lane < 36) v = U_WD + U_DISC + U_BS + 64 + lane;
+            else if (lane < 36 + NDISC_R + 1) rb = lane - 36;
+            if (v >= 0) element_item(v, Gc, O);
+            else if (rb >= 0) ring_weight_lane(rb, Gc, swt);
+        };
+        auto grab = [&]() {
+            int j = 0;
+            if (lane == 0) j = atomicAdd(&sjob, 1);
+            return __builtin_amdgcn_readfirstlane(__shfl(j, 0, 64));
+        };
+        // straight-line calls, not a loop: a loop's invariant constants (the
+        // transcendental polynomials) were hoisted and spilled to scratch
+        if (wv > 0) chunk(wv);
+        int j = grab();
+        if (j < 16) chunk(j);
+        j = grab();
+        if (j < 16) chunk(j);
     }
-    static_assert(14 * 64 + 4 == NUNIQ, "wave 7 holds the last chunk");
-    PAIR_STAMP(16, wv == 7 && lane == 0);
-    if (wv == 7 && lane >= PAIR_SPEC_LANE0 && lane < PAIR_SPEC_LANE0 + A.spl && X.nspec > 0) {
-        // speculative setup lanes of the next half (candidate uniform per block)
-        const int c = pair < A.nbc ? 0 : 1;
-        const int t = (pair - c * A.nbc) * A.spl + (lane - PAIR_SPEC_LANE0);
-        if (t < X.nspec) setup_any(X.S[__builtin_amdgcn_readfirstlane(c)], t);
-#ifdef LFG_PROFILE_PAIR
-        if (lane == PAIR_SPEC_LANE0 && blockIdx.x < 4096) {
-            const int np = X.S[0].W * X.S[0].E;
-            g_pair_t[17][blockIdx.x] = t >= X.nspec ? 9 : (t < np ? 0 : (t < np + X.S[0].W ? 1 : 2));
-        }
-#endif
-    }
+    static_assert(13 * 64 >= U_WD + U_DISC + U_BS && 12 * 64 < U_WD + U_DISC + U_BS, "13 chunks of WD/disc/spot");
+    static_assert(U_DON == 64 + 36 && 36 + NDISC_R + 1 <= 64, "the donor and ring-weight chunks");
     PAIR_STAMP(1 + wv, lane == 0);
     __syncthreads();  // B1: the tables, swt, sflag reset, windows
     PAIR_STAMP(9, tid == 0);
@@ -3498,6 +3513,43 @@ int lfg_flux(const double* pars, int W, int P, const double* x, const double* w,
     return LFG_OK;
 }
 
+// k_pair serves trees whose eclipses fit one tile with S = 1 and no GP
+// (LFG_PAIR=1 in the environment; k_elements + k_lnlike otherwise)
+static bool pair_ok(int gp, int nsub, int max_n, int ndim)
+{
+    static const bool env = [] {
+        const char* e = getenv("LFG_PAIR");
+        return e && e[0] == '1';
+    }();
+    return env && !gp && nsub == 1 && max_n <= LIKE_TILE && ndim <= LIKE_THREADS;
+}
+
+int lfg_lnlike(const double* pars, int W, int P, const double* x, const double* w, int N, int nsub, const double* y,
+               const double* ye, double* lnlike, int* status, void* wsp, size_t ws_bytes, void* stream)
+{
+    if (W <= 0 || N < 0 || nsub < 1 || (P != 14 && P != 18) || !pars || !lnlike || (N > 0 && (!x || !y || !ye)))
+        return LFG_E_ARGS;
+    Ws ws = carve(wsp, W, 1);
+    if (!wsp || ws_bytes < ws.total) return LFG_E_WORKSPACE;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    SetupArgs S{pars, W, P, 1, P, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
+                ws.geo, ws.status, ws.prior, ws.bstatus, 0, nullptr, nullptr};
+    const bool pair = pair_ok(0, nsub, N, 0);
+    int rc = run_front(S, ws, st, nullptr, !pair);
+    if (rc) return rc;
+    LikeArgs L{ws.geo, ws.status, ws.ab, ws.donor, ws.wts, 1, nullptr, N, x, y, ye, w,
+               nsub, nullptr, nullptr, lnlike, W, nullptr, nullptr, nullptr, false, nullptr,
+               nullptr, nullptr, nullptr, 0, 0, 0ull, 0ull, nullptr};
+    L.bstatus = ws.bstatus;
+    if (pair) hipLaunchKernelGGL(k_pair, dim3(W), dim3(LIKE_THREADS), 0, st, PairArgs{L, ElemSpec{}, nullptr, nullptr, 0, 0});
+    else if (nsub > 1) hipLaunchKernelGGL((k_lnlike<1, true>), dim3(W), dim3(LIKE_THREADS), 0, st, L);
+    else hipLaunchKernelGGL((k_lnlike<1, false>), dim3(W), dim3(LIKE_THREADS), 0, st, L);
+    if ((rc = launch_ok())) return rc;
+    if (status && hipMemcpyAsync(status, ws.status, sizeof(int) * W, hipMemcpyDeviceToDevice, st) != hipSuccess)
+        return LFG_E_LAUNCH;
+    return LFG_OK;
+}
+
 struct Accept {  // fused stretch-move acceptance of lfg_stretch_lnprob_accept
     double* pos;
     double* lnp;
@@ -3596,17 +3648,12 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
     // k_pair: the element solve and the likelihood of a pair in one
     // workgroup (one-tile eclipses, S = 1, no GP); the speculative lanes must
     // fit wave 7's spare lanes
-    static const bool pair_env = [] {
-        const char* e = getenv("LFG_PAIR");
-        return e && e[0] == '1';
-    }();
     int spl = 0, nbc = 0;
     if (X.nspec > 0 && npairs >= 2) {
         nbc = (npairs + 1) / 2;
         spl = (X.nspec + (npairs - nbc) - 1) / (npairs - nbc);
     }
-    const bool pair_path = pair_env && !T->gp && T->nsub == 1 && T->max_n <= LIKE_TILE && T->ndim <= LIKE_THREADS &&
-                           (X.nspec == 0 || (npairs >= 2 && spl <= 64 - PAIR_SPEC_LANE0));
+    const bool pair_path = pair_ok(T->gp, T->nsub, T->max_n, T->ndim) && (X.nspec == 0 || (npairs >= 2 && spl <= 64));
     int rc = run_front(S, ws, st, ev, !pair_path, &X, !(sp && sp->in));
     if (rc) return rc;
     double* lle = lnlike_e ? lnlike_e : ws.lle;

@@ -116,6 +116,42 @@ class CV:
 # lfit.CV is wdFlux*ywd + dFlux*yd + sFlux*ys + rsFlux*yrs of these at
 # inc = roche.findi(q, dphi) and phase x - phi0 (testCV.py:65; MODEL_SPEC 5.6).
 
+
+def lnlike_batch(pars, x, y, ye, width=None, nsub=1, device=None):
+    """Batched SimpleEclipse.ln_like (CVModel.py:157-191) of one light curve,
+    through lfg_lnlike: -0.5 chi^2 of W parameter sets, fused (no flux array),
+    -inf where the model is invalid (chi^2 = inf, CVModel.py:163-171).
+    Returns torch tensors on the device: ln_like [W], status [W] int32."""
+    import torch
+    _native.require_gpu()
+    L = _native.lib()
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    P_t = torch.as_tensor(pars, dtype=torch.float64, device=dev)
+    if P_t.ndim == 1:
+        P_t = P_t[None, :]
+    P_t = P_t.contiguous()
+    W, P = P_t.shape
+    if P not in (14, 18):
+        raise ValueError("lfit.CV takes 14 or 18 parameters, got %d" % P)
+    x_np = np.ascontiguousarray(np.asarray(x, dtype=np.float64).reshape(-1))
+    if width is None:
+        width = _default_width(x_np)
+    w_np = np.array(np.broadcast_to(np.asarray(width, dtype=np.float64), x_np.shape))
+    t = {k: torch.as_tensor(np.ascontiguousarray(v, dtype=np.float64).reshape(-1), device=dev)
+         for k, v in (("x", x_np), ("w", w_np), ("y", y), ("ye", ye))}
+    N = t["x"].shape[0]
+    if t["y"].shape[0] != N or t["ye"].shape[0] != N:
+        raise ValueError("x, y and ye must have the same length")
+    out = torch.empty(W, dtype=torch.float64, device=dev)
+    status = torch.empty(W, dtype=torch.int32, device=dev)
+    ws = _native.Workspace.get(L.lfg_workspace_size(W, 1), dev)
+    vp = lambda a: ctypes.c_void_p(a.data_ptr())
+    with torch.cuda.device(dev):
+        rc = L.lfg_lnlike(vp(P_t), W, P, vp(t["x"]), vp(t["w"]), N, int(nsub), vp(t["y"]), vp(t["ye"]), vp(out),
+                          vp(status), vp(ws), ws.numel(), _native.stream_ptr(dev))
+    _native.check(rc, "lfg_lnlike")
+    return out, status
+
 def disc_grid(npts):
     """PyDisc's npts -> (rings, azimuths): 1000 -> 20 x 50 (MODEL_SPEC 5.2,
     5.6); other sizes keep the 2.5 azimuths-per-ring aspect, so the element

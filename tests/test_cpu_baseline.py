@@ -66,3 +66,33 @@ def test_port_gp_tree_matches_reference(oracle, port):
     fin = np.isfinite(got)
     np.testing.assert_allclose(got[fin], d["ln_prob"][fin], rtol=1e-9)
     np.testing.assert_allclose(got[fin], ref[fin], rtol=1e-9)
+
+
+def test_cpu_twins_match_oracle_and_batch(oracle, port):
+    """The lfg_cpu_* twins (cpu_baseline/lfg_cpu.h): lfg_cpu_lnlike and
+    lfg_cpu_flux of one eclipse against the oracle's flux and chi^2
+    (SimpleEclipse.chisq, CVModel.py:157-178), lfg_cpu_lnprob against the
+    batch form bench.py times, with an invalid parameter set among them."""
+    from tests.helpers import random_pars, phase_grid
+    pars = random_pars(12, complex_bs=True, seed=5)
+    pars[3, 4] = -1.0  # q < 0: LFG_ST_BAD_Q
+    x, w = phase_grid(300)
+    rng = np.random.default_rng(3)
+    _, f0 = oracle.flux(pars[0], x, w)
+    y = f0 + 0.004 * rng.standard_normal(x.size)
+    ye = np.full(x.size, 0.004)
+    ll, st = port.lnlike(pars, x, w, y, ye, nthreads=4)
+    fl, st2 = port.flux(pars, x, w, nthreads=4)
+    assert st[3] == 1 and st2[3] == 1 and np.isneginf(ll[3]) and np.isnan(fl[3]).all()
+    ok = st == 0
+    assert ok.sum() >= 8
+    for i in np.flatnonzero(ok):
+        _, fo = oracle.flux(pars[i], x, w)
+        np.testing.assert_allclose(fl[i], fo, rtol=1e-9, atol=1e-12)
+        chi = np.sum(((y - fo) / ye) ** 2)
+        assert abs(ll[i] - (-0.5 * chi)) <= 1e-9 * max(1.0, 0.5 * chi)
+    m = synthetic.config_single(300, flux_fn=_flux(oracle))
+    t = batch.compile_tree(m)
+    p0 = np.array(m.dynasty_par_vals)
+    walk = p0 * (1.0 + 0.01 * rng.standard_normal((16, p0.size)))
+    np.testing.assert_array_equal(port.lnprob(walk, t, nthreads=4), port.lnprob_batch(walk, t, nthreads=4)[0])

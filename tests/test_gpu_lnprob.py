@@ -551,3 +551,43 @@ def test_lnprior_tiny_log_uniform_products():
     got = ev.ln_prior(torch.as_tensor(walkers, device="cuda")).cpu().numpy()
     ref = np.array([sum(p.ln_prob(v) for p, v in zip(pri, row)) for row in walkers])
     np.testing.assert_allclose(got, ref, rtol=1e-13, atol=1e-11)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nsub", [1, 3])
+def test_lfg_lnlike_matches_tree_and_cpu_twin(oracle, nsub, tmp_path):
+    """lfg_lnlike (one eclipse, fused chi^2, no tree) against lfg_lnprob's
+    per-eclipse ln_like on the same one-eclipse tree, and against its CPU
+    twin lfg_cpu_lnlike (cpu_baseline/lfg_cpu.h), both through ctypes."""
+    import torch
+    from cpu_baseline import cpu
+    from lfit_python_amd import batch, synthetic
+    from lfit_python_amd.lfit import lnlike_batch
+    dev = torch.device("cuda", 0)
+    m = synthetic.config_single(300, flux_fn=lambda p, x, w, ns: oracle.flux(p, x, w, nsub=ns)[1], nsub=nsub)
+    t = batch.compile_tree(m, nsub=nsub)
+    ev = batch.LnProbEvaluator(t, device=dev)
+    rng = np.random.default_rng(41)
+    p0 = np.array(m.dynasty_par_vals)
+    walk = p0 * (1.0 + 0.02 * rng.standard_normal((96, p0.size)))
+    lle = torch.empty((96, 1), dtype=torch.float64, device=dev)
+    lnp = ev(torch.as_tensor(walk, device=dev), lnlike_e=lle).cpu().numpy()
+    leaf = m.leaves()[0]
+    # each walker's CV vector, as the tree routes it (cv_parlist)
+    pars = np.empty((96, 18))
+    for i in range(96):
+        m.dynasty_par_vals = walk[i]
+        pars[i] = leaf.cv_parlist
+    lc = leaf.lc
+    got, st = lnlike_batch(pars, lc.x, lc.y, lc.ye, width=lc.w, nsub=nsub, device=dev)
+    got = got.cpu().numpy()
+    ref = lle.cpu().numpy()[:, 0]
+    fin = np.isfinite(lnp)   # the tree skips walkers its priors reject
+    assert fin.sum() >= 48
+    np.testing.assert_allclose(got[fin], ref[fin], rtol=1e-12, atol=1e-9)
+    port = cpu.CpuPort(cpu.build(out=str(tmp_path / "liblfg_cpu.so")))
+    twin, st2 = port.lnlike(pars, lc.x, lc.w, lc.y, lc.ye, nsub=nsub, nthreads=4)
+    np.testing.assert_array_equal(st2, st.cpu().numpy())
+    ok = st2 == 0
+    np.testing.assert_allclose(got[ok], twin[ok], rtol=1e-10, atol=1e-8)
+    assert np.all(np.isneginf(got[~ok]))
