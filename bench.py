@@ -32,13 +32,25 @@ records a start/stop event pair around that kernel only.  (A timing event is
 a queue barrier: events around all kernels cost ~20 % of the step, so they
 stay out of the timed region.)
 
-Roofline (MODEL_SPEC.md section 11): the path is FP64-VALU bound.  Achieved
-= walker evals/s per GPU x E x the counted algorithmic FLOPs per
-walker-eclipse evaluation (F_setup + 900 roots x F_geom + N S (1500 x 3 +
-400 x 6 + 40)), against the 78.6 TFLOP/s FP64 vector peak.  The HBM
-fraction uses SURVEY.md 8(d)'s bytes (8 ndim + 8 per walker, 32 N per
-eclipse per launch); the element tables the kernels hand each other are
-reported apart as materialised bytes.
+Roofline (MODEL_SPEC.md section 11; the path is FP64-VALU or latency bound,
+neither HBM- nor MFMA-bound):
+  roofline.achieved / frac   the DOMINANT kernel (k_pair, or k_elements on
+      the two-kernel layout, chosen by the warmup's events): its counted FP64
+      work per launch (profiles/r03/flops_<config>.json per pair x the pairs
+      of a launch) / its average launch time over the timed region (HIP events
+      on its stream) / 78.6 TFLOP/s;
+  roofline.traffic           HBM bytes per launch of that kernel from the
+      committed PMC passes (profiles/*/pmc_traffic_<config>.json), when they
+      were taken on the same workload and kernel layout;
+  roofline.whole_step        every kernel of the step on the same counts x
+      evals/s per GPU;
+  roofline.direct_form_equivalent   SURVEY 8(d)'s direct element x point
+      count (a rate of equivalent work, not a utilisation);
+  roofline.hbm               SURVEY 8(d)'s algorithmic bytes per half-step
+      (8 ndim + 8 per walker, 32 N per eclipse per launch) over the step time,
+      the element tables kernels hand each other apart (none on k_pair).
+Multi-rank lines carry "ranks": the world size, the RCCL communicator's own
+count (ncclCommCount), each rank's step time and exchange time.
 """
 import argparse
 import ctypes
@@ -59,8 +71,10 @@ FP64_PEAK_TFLOPS = 78.6
 PMC_DIR = os.path.join(ROOT, "profiles", "r03")   # pmc_traffic_<config>.json (tools/pmc_traffic.py)
 
 NEV = 4  # LFG_NEV (include/lfg.h)
-# (name as rocprofv3 prints it, start event, end event)
-KERNELS = [("k_setup", 0, 1), ("k_elements", 1, 2), ("k_lnlike", 2, 3)]
+# (name as rocprofv3 prints it, start event, end event) per kernel layout
+# (lfg_layout): k_elements + k_lnlike, or k_pair (both in one workgroup per pair)
+KERNELS_TWO = [("k_setup", 0, 1), ("k_elements", 1, 2), ("k_lnlike", 2, 3)]
+KERNELS_PAIR = [("k_setup", 0, 1), ("k_pair", 2, 3)]
 
 # Counted FP64 work per (walker, eclipse) pair of the algorithm the kernels
 # execute (MODEL_SPEC.md section 11; tools/flop_count.py + tools/like_count.py
@@ -82,6 +96,7 @@ MATERIALISED_PER_PAIR = {
     "k_setup": 18 * 8 + GEO_SETUP * 8 + 4 + 3 * 8 + GEO_BSPOT * 8 + 4,
     "k_elements": GEO_READ * 8 + 8 + NELU * 16 + U_DON * DON_STRIDE * 8 + WT_N * 8,
     "k_lnlike": GEO_READ * 8 + 4 + NELU * 16 + U_DON * DON_STRIDE * 8 + WT_N * 8 + 8,
+    "k_pair": GEO_READ * 8 + 4 + 8,   # the tables stay in the workgroup's LDS
 }
 
 CONFIGS = {
@@ -214,6 +229,7 @@ def flops_per_pair(config, npts, nsub):
         direct = (direct - d["F_acc_total"]) + d["F_acc_total"] * r
         note = "scaled from %s's %d x %d points x sub-samples" % (os.path.basename(path), d["npts"], d["nsub"])
     executed = float(pk["k_elements"] + pk["k_lnlike"])   # the spec path: no k_setup launch per step
+    pk["k_pair"] = executed                                # k_elements' and k_lnlike's work in one kernel
     return {"per_kernel": pk, "executed": executed, "direct": direct, "note": note,
             "source": os.path.relpath(path, ROOT)}
 
@@ -221,7 +237,7 @@ def flops_per_pair(config, npts, nsub):
 # kernels inside each event span of the timed region (the GP pair of kernels
 # runs between k_lnlike's events)
 SPAN = {"k_setup": ("k_setup",), "k_elements": ("k_elements",),
-        "k_lnlike": ("k_lnlike", "k_gp_dcp", "k_gp_like")}
+        "k_lnlike": ("k_lnlike", "k_gp_dcp", "k_gp_like"), "k_pair": ("k_pair", "k_combine_walkers")}
 
 
 def pmc_row(kernel, config, npts, nsub, pairs):
@@ -249,6 +265,26 @@ def pmc_row(kernel, config, npts, nsub, pairs):
         return None, None
     scale = pairs / float(meta.get("pairs_per_launch", pairs))
     return {k: v * scale for k, v in out.items()}, os.path.relpath(path, ROOT)
+
+
+def rank_block(dist, world, backend, own_ms, xch_ms, cnt, dev):
+    """The line's "ranks" object (every rank calls it: one all_gather of each
+    rank's own ms per step and exchange ms): world size, backend, the RCCL
+    communicator's own rank count and user rank (cnt = ncclCommCount,
+    ncclCommUserRank of rank 0's communicator, or None), per-rank times"""
+    import torch
+    mine = torch.tensor([own_ms, xch_ms if xch_ms is not None else float("nan")], dtype=torch.float64, device=dev)
+    allr = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(allr, mine)
+    per = torch.stack(allr).cpu().numpy()
+    return {"world_size": world, "backend": backend,
+            "rccl_comm_count": cnt[0] if cnt else None, "rccl_user_rank": cnt[1] if cnt else None,
+            "ms_per_step_per_rank": [float(v) for v in per[:, 0]],
+            "ms_per_step_min": float(per[:, 0].min()), "ms_per_step_max": float(per[:, 0].max()),
+            "exchange_ms_per_half_step": [None if np.isnan(v) else float(v) for v in per[:, 1]],
+            "note": "ms_per_step_per_rank: each rank's timed steps before the closing barrier; exchange: events "
+                    "around the all_gather on the sampled calls (rccl_comm_count: ncclCommCount of the direct RCCL "
+                    "communicator, null when the exchange ran through torch.distributed)"}
 
 
 def run(args):
@@ -309,6 +345,8 @@ def run(args):
     if args.emu:
         S.emulate_rank(*args.emu)
     S.set_state(init)
+    layout = L.lfg_layout(ctypes.byref(ev.ctree))
+    KERNELS = KERNELS_PAIR if layout == 1 else KERNELS_TWO
 
     # HIP events around kernels of lfg_lnprob calls (include/lfg.h LFG_NEV)
     events = []
@@ -351,6 +389,24 @@ def run(args):
 
     timed_half.takes_spec = timed_shard.takes_spec = True
 
+    # the per-half-step ln_prob exchange, timed by HIP events on the stream it
+    # is enqueued on, on the calls whose shard kernels are sampled too
+    xch_events = []
+    xch_on = [False]
+    plain_gather = S._gather
+
+    def timed_gather(out, mine):
+        if not xch_on[0] or (ncall[0] - 1) % every[0]:
+            return plain_gather(out, mine)
+        # the exchange is enqueued on torch's current stream (comm.py), so
+        # torch's events see it
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        plain_gather(out, mine)
+        e1.record()
+        xch_events.append((e0, e1))
+    S._gather = timed_gather
+
     def set_timing(on):
         if world == 1 and not args.shard_path:
             S.half_timer = timed_half if on else None
@@ -379,7 +435,7 @@ def run(args):
         S.step()
     torch.cuda.synchronize()
     set_timing(False)
-    dom = 2  # k_lnlike unless calibrated
+    dom = len(KERNELS) - 1  # the likelihood kernel unless calibrated
     calib = {}
     if events:
         cal_ms, _ = kernel_ms(KERNELS)
@@ -394,6 +450,7 @@ def run(args):
     pool.extend(make_evs() for _ in range((calls + every[0] - 1) // every[0]))
     set_timing(True)
 
+    xch_on[0] = True
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -401,15 +458,26 @@ def run(args):
     for _ in range(args.steps):
         S.step()
     torch.cuda.synchronize()
+    own_elapsed = time.perf_counter() - t0   # this rank's own steps, before it waits for the others
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     set_timing(False)
+    xch_on[0] = False
+    S._gather = plain_gather
+    xch_ms = None
+    if xch_events:
+        xch_ms = sum(e0.elapsed_time(e1) for e0, e1 in xch_events) / len(xch_events)
+    ranks = None
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        # every rank's own step time and exchange time, and what RCCL says the
+        # communicator holds: the line proves how many ranks exchanged
+        ranks = rank_block(dist, world, backend, own_elapsed / args.steps * 1e3, xch_ms,
+                           S._rccl.count() if S._rccl else None, dev)
 
     # the dominant kernel's device time over the timed region
     shard = events[0][1] if events else W // 2   # walkers per launch
@@ -445,7 +513,9 @@ def run(args):
     avg_dom = float(dom_ms[0])
     E = tree.E
     npts = int(np.max(np.diff(tree.offsets)))
-    value = W * args.steps / elapsed
+    # emulation: one rank of N evaluates W / N walkers per step (the rest of the
+    # ensemble is held, not evaluated): the line counts what was evaluated
+    value = (W // args.emu[1] if args.emu else W) * args.steps / elapsed
     acc = float(np.mean(S.acceptance_fraction))
 
     # ---- FP64 roofline on the counted work of the executed algorithm (MODEL_SPEC 11)
@@ -545,7 +615,10 @@ def run(args):
                                                                   "(DESIGN.md 3): an intermediate, not 8(d) work"}},
             },
             "acceptance_fraction": acc,
-            **({"emulation": emu} if emu else {}),
+            "kernel_layout": "k_pair" if layout == 1 else "k_elements + k_lnlike",
+            **({"ranks": ranks} if ranks else {}),
+            **({"exchange_ms_per_half_step": xch_ms} if (xch_ms is not None and not ranks) else {}),
+            **({"emulation": emu, "emulated_rank": True} if emu else {}),
             **cpu,
         }
         print(json.dumps(line), file=json_out, flush=True)

@@ -390,6 +390,12 @@ int lfg_event_elapsed_ms(void* start, void* stop, float* ms);
 
 const char* lfg_version(void);
 
+/* The kernels a tree's ln_prob runs on: 1 = k_pair (element solve and
+ * likelihood of a walker-eclipse pair in one workgroup: one-tile eclipses,
+ * nsub = 1, no GP, LFG_PAIR=1 in the environment), 0 = k_elements +
+ * k_lnlike; LFG_E_ARGS for a null or empty tree.  For measurement tools. */
+int lfg_layout(const lfg_tree* tree);
+
 #ifdef __cplusplus
 }
 #endif

@@ -74,7 +74,7 @@ EXPORTS = ("lfg_workspace_size", "lfg_workspace_size_tree", "lfg_flux", "lfg_lnl
            "lfg_elements", "lfg_roche", "lfg_stretch_propose", "lfg_stretch_accept",
            "lfg_stretch_propose_dev", "lfg_stretch_accept_dev", "lfg_event_create", "lfg_event_destroy",
            "lfg_event_elapsed_ms", "lfg_wdphases", "lfg_gp_lnlike", "lfg_component_workspace_size",
-           "lfg_component", "lfg_version")
+           "lfg_component", "lfg_version", "lfg_layout")
 
 
 FLAGS = ["--offload-arch=%s" % ARCH, "-O3", "-std=c++17", "-fPIC", "-shared"]
@@ -226,6 +226,8 @@ def lib():
         L.lfg_component.argtypes = [ip, vp, ip, vp, vp, ip, ip, ip, vp, vp, ip, vp, vp, vp, sz, vp]
         L.lfg_version.restype = ctypes.c_char_p
         L.lfg_version.argtypes = []
+        L.lfg_layout.restype = ip
+        L.lfg_layout.argtypes = [ctypes.POINTER(LfgTree)]
         _lib = L
         return L
 

@@ -44,6 +44,8 @@ def _load_rccl():
     lib.ncclAllGather.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
                                   ctypes.c_void_p, ctypes.c_void_p]
     lib.ncclCommDestroy.argtypes = [ctypes.c_void_p]
+    lib.ncclCommCount.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
+    lib.ncclCommUserRank.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
     lib.ncclGetErrorString.restype = ctypes.c_char_p
     return lib
 
@@ -85,6 +87,14 @@ class RcclAllGather:
                                            mine.numel(), NCCL_FLOAT64, self.comm,
                                            ctypes.c_void_p(torch.cuda.current_stream(mine.device).cuda_stream)),
                     "ncclAllGather")
+
+    def count(self):
+        """(ranks in the communicator, this rank's index) as RCCL reports them
+        (ncclCommCount, ncclCommUserRank): bench.py puts them on its line"""
+        n, r = ctypes.c_int(), ctypes.c_int()
+        self._check(self.lib.ncclCommCount(self.comm, ctypes.byref(n)), "ncclCommCount")
+        self._check(self.lib.ncclCommUserRank(self.comm, ctypes.byref(r)), "ncclCommUserRank")
+        return n.value, r.value
 
     def close(self):
         if self.comm:

@@ -3524,6 +3524,12 @@ static bool pair_ok(int gp, int nsub, int max_n, int ndim)
     return env && !gp && nsub == 1 && max_n <= LIKE_TILE && ndim <= LIKE_THREADS;
 }
 
+int lfg_layout(const lfg_tree* T)
+{
+    if (!T || T->E <= 0) return LFG_E_ARGS;
+    return pair_ok(T->gp, T->nsub, T->max_n, T->ndim) ? 1 : 0;
+}
+
 int lfg_lnlike(const double* pars, int W, int P, const double* x, const double* w, int N, int nsub, const double* y,
                const double* ye, double* lnlike, int* status, void* wsp, size_t ws_bytes, void* stream)
 {
