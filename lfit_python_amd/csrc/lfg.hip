@@ -2466,8 +2466,15 @@ __device__ unsigned long long g_pair_t[20][4096];
     do {                                                                           \
         if ((cond) && blockIdx.x < 4096) g_pair_t[slot][blockIdx.x] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
+// per wave (lane 0) inside the sweep: 0 counts done, 1 WD/disc applied, 2 spot/donor applied, 3 after B4
+__device__ unsigned long long g_pair_w[4][8][4096];
+#define PAIR_WSTAMP(k)                                                                                  \
+    do {                                                                                                \
+        if (lane == 0 && blockIdx.x < 4096) g_pair_w[k][wv][blockIdx.x] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
 #else
 #define PAIR_STAMP(slot, cond)
+#define PAIR_WSTAMP(k)
 #endif
 
 __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
@@ -2739,6 +2746,7 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
             }
             count_lt_multi<2 * NI>(XI, qx, J);
             count_le_back_multi<2 * NI>(TA.hi, qx, J, Jb);
+            PAIR_WSTAMP(0);
 #pragma unroll
             for (int i = 0; i < NI; ++i)
                 if (abk[i].x < abk[i].y) {
@@ -2747,8 +2755,11 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
                     apply_runs(Runs{Jb[2 * i], J[2 * i], Jb[2 * i + 1], J[2 * i + 1]}, abk[i].x, abk[i].y,
                                swn[uring(u)], XI, TA.hi, TA.iw, ((lane & 1) ? SU.s.X : sacc)[(u < U_WD) ? 0 : 1]);
                 }
+            PAIR_WSTAMP(1);
             sweep_spot_donor(tid, XI, TA, phase_index(sph, SU.s.scp, m), sab, sbw, snorm[0], sdq, snorm[1], sacc + 2);
+            PAIR_WSTAMP(2);
             __syncthreads();  // B4
+            PAIR_WSTAMP(3);
             long long r[6] = {0, 0, 0, 0, 0, 0};
             block_scan<6>(sacc, spart, tid, r, SU.s.X);
             PAIR_STAMP(12, tid == 0);
@@ -3993,6 +4004,11 @@ int lfg_debug_like_waves(unsigned long long* host)
 int lfg_debug_pair(unsigned long long* host)
 {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pair_t), sizeof(g_pair_t)) == hipSuccess ? 0 : -1;
+}
+// and its per-wave sweep stamps, host [4][8][4096]
+int lfg_debug_pair_waves(unsigned long long* host)
+{
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pair_w), sizeof(g_pair_w)) == hipSuccess ? 0 : -1;
 }
 #endif
 

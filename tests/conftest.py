@@ -33,3 +33,19 @@ def pytest_collection_modifyitems(config, items):
 def oracle():
     from oracle.oracle import Oracle
     return Oracle()
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _native_library_is_this_tree(request):
+    """Before any GPU test: the loaded liblfg_hip.so carries the source hash
+    of this tree (a stale or foreign library fails the session loudly)."""
+    if not any("gpu" in item.keywords for item in request.session.items):
+        return
+    try:
+        import torch
+        if not torch.cuda.is_available():
+            return
+    except Exception:
+        return
+    from lfit_python_amd import _native
+    _native.verify()

@@ -115,6 +115,40 @@ def test_element_tables(oracle, pars):
     np.testing.assert_allclose(don[0], odon, rtol=1e-9, atol=1e-14)
 
 
+def _grazing_sets():
+    """parameter sets whose eclipse chords graze the WD and the disc: small
+    dphi (inclination near the lowest that eclipses the WD centre) and a
+    large disc, where the tangency equation's slope g' is small and the
+    Newton stop rule (|dth| <= 1e-6, ~|dth|^2 g''/2g' after the step) is
+    weakest"""
+    out = []
+    for q, dphi, rdisc in ((0.1037, 0.006, 0.45), (0.1037, 0.012, 0.6), (0.3, 0.008, 0.5), (0.05, 0.004, 0.4)):
+        p = np.array(TRUTH18, dtype=float)
+        p[4], p[5], p[6] = q, dphi, rdisc
+        out.append(p)
+    return out
+
+
+@pytest.mark.parametrize("k", range(4))
+def test_element_tables_grazing(oracle, k):
+    """near-grazing contacts against the oracle's nested solver: every
+    interval both find within PHASE_ATOL; an element one solver finds
+    eclipsed and the other not must be a vanishing chord (< 1e-6 phase)"""
+    pars = _grazing_sets()[k]
+    st, a, b, wg, don, geo = _elements_gpu(pars)
+    ost, oa, ob, ow, odon, ogeo = oracle.elements(pars)
+    assert st[0] == ost == 0
+    g, o = a[0] < b[0], oa < ob
+    both = g & o
+    assert both.sum() > 50
+    assert np.max(np.abs(a[0][both] - oa[both])) < PHASE_ATOL
+    assert np.max(np.abs(b[0][both] - ob[both])) < PHASE_ATOL
+    only = g ^ o
+    if only.any():
+        width = np.where(g, b[0] - a[0], ob - oa)[only]
+        assert np.max(width) < 1e-6, width
+
+
 @pytest.mark.parametrize("complex_bs", [True, False])
 @pytest.mark.parametrize("nsub", [1, 5])
 def test_flux_matches_oracle(oracle, complex_bs, nsub):

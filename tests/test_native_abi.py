@@ -108,3 +108,49 @@ def test_rccl_unique_id_round_trip_keeps_nul_bytes():
     assert comm.uid_bytes(uid) == raw
     with pytest.raises(ValueError):
         comm.uid_from(raw[:100])
+
+
+def test_stale_library_is_rebuilt(tmp_path, monkeypatch):
+    """build() decides by the compiled-in source hash, not file times: a
+    library whose hash is not the tree's is rebuilt, the tree's is kept."""
+    import shutil
+    lib = tmp_path / "liblfg_hip.so"
+    shutil.copy(_native.LIB_PATH, lib)
+    h0 = _native.file_hash(str(lib))
+    want = _native.source_hash()
+    data = lib.read_bytes().replace(h0.encode(), want.encode())   # "the tree's" library
+    lib.write_bytes(data.replace(want.encode(), b"0123456789abcdef"))   # a stale one
+    assert _native.file_hash(str(lib)) == "0123456789abcdef"
+    calls = []
+    monkeypatch.setattr(_native, "LIB_PATH", str(lib))
+    monkeypatch.setattr(_native.subprocess, "run", lambda cmd, check: (calls.append(cmd), shutil.copy(
+        _native.LIB_PATH + ".orig", cmd[cmd.index("-o") + 1]))[0])
+    (tmp_path / "liblfg_hip.so.orig").write_bytes(data)
+    _native.build()
+    assert len(calls) == 1 and ('-DLFG_SRC_HASH="%s"' % want) in calls[0]
+    assert _native.file_hash(str(lib)) == want
+    _native.build()                      # now current: nothing rebuilt
+    assert len(calls) == 1
+
+
+def test_foreign_library_refused(tmp_path):
+    """LFG_LIB without LFG_DIAGNOSTIC=1 is refused at import; with it, a
+    library carrying another source hash fails verify() (what smoke() and the
+    GPU test session run before any kernel)."""
+    import shutil
+    import sys
+    foreign = tmp_path / "liblfg_foreign.so"
+    h0 = _native.file_hash(_native.LIB_PATH)
+    data = open(_native.LIB_PATH, "rb").read().replace(h0.encode(), b"fedcba9876543210")  # tag and lfg_version
+    foreign.write_bytes(data)
+    env = dict(os.environ, LFG_LIB=str(foreign))
+    env.pop("LFG_DIAGNOSTIC", None)
+    code = "import lfit_python_amd._native"
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True)
+    assert r.returncode != 0 and "LFG_DIAGNOSTIC" in r.stderr
+    env["LFG_DIAGNOSTIC"] = "1"
+    code = ("import lfit_python_amd._native as n\n"
+            "try:\n    n.verify()\nexcept RuntimeError as e:\n    print('refused', e)\n")
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True)
+    assert "refused" in r.stdout and "fedcba9876543210" in r.stdout, r.stdout + r.stderr
+    shutil.rmtree(tmp_path, ignore_errors=True)

@@ -63,3 +63,12 @@ for k, nm in ((0, "setup"), (1, "prior"), (2, "stream")):
                                                         np.percentile(spec, 90), spec.max(), np.median(fin_k), fin_k.max()))
 fin = (t[15] - t0.min()) / 100.0
 print("block finish times from launch start: %s us" % np.percentile(fin, [0, 10, 50, 90, 100]).round(2))
+wv = np.zeros((4, 8, 4096), dtype=np.uint64)
+if L.lfg_debug_pair_waves(ctypes.c_void_p(wv.ctypes.data)) == 0:
+    wv = wv[:, :, :nb].astype(np.float64)
+    b3 = t[11]
+    print("sweep per wave from B3 (us): median over blocks of [earliest wave, latest wave]")
+    for k, nm in enumerate(("counts", "WD/disc applied", "spot/donor applied", "after B4")):
+        d = (wv[k] - b3[None, :]) / 100.0
+        print("  %-20s earliest %6.2f  latest %6.2f" % (nm, np.median(d.min(0)), np.median(d.max(0))))
+    print("  %-20s %6.2f" % ("scan done (thread 0)", np.median((t[12] - b3) / 100.0)))
