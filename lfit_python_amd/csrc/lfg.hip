@@ -649,8 +649,37 @@ __device__ __forceinline__ void ring_weight_lane(int rb, GPtr G, double* __restr
     if (rb == 0) wtd[NDISC_R] = TWO_PI * (Pt - P);
 }
 
+// results of an item go to a sink: wd_disc(u, a, b), spot(j, a, b, w),
+// donor(uu, vx, vy, vz, centre, half-width)
+template <typename GPtr, typename Sink>
+__device__ __forceinline__ void element_item_to(int v, GPtr G, Sink& K);
+
+// the sink of k_elements (and k_pair's point-major fallback): the tables
+struct MemSink {
+    const ElemOut& O;
+    __device__ __forceinline__ void wd_disc(int u, double a, double b) { O.abw[uslot(u)] = make_double2(a, b); }
+    __device__ __forceinline__ void spot(int j, double a, double b, double w)
+    {
+        O.abs[j] = make_double2(a, b);
+        O.wbs[j] = w;
+    }
+    __device__ __forceinline__ void donor(int uu, double vx, double vy, double vz, double cen, double hw)
+    {
+        double* D = O.don + uu * DON_STRIDE;
+        D[0] = vx;
+        D[1] = vy;
+        D[2] = vz;
+        D[3] = cen;
+        D[4] = hw;
+    }
+};
+
 template <typename GPtr>
-__device__ __forceinline__ void element_item(int v, GPtr G, const ElemOut& O);
+__device__ __forceinline__ void element_item(int v, GPtr G, const ElemOut& O)
+{
+    MemSink K{O};
+    element_item_to(v, G, K);
+}
 
 // one k_elements lane's item v of pair `pair` (v >= NUNIQ: the disc ring
 // weights of the last chunk's spare lanes)
@@ -683,8 +712,8 @@ __device__ __forceinline__ void element_lane(int v, int pair, int npairs, const 
 
 // item v (v < NUNIQ) of a pair: item order WD, disc, spot, donor; k_elements
 // deals the chunks of 64 items out in its own dispatch order (kOrder)
-template <typename GPtr>
-__device__ __forceinline__ void element_item(int v, GPtr G, const ElemOut& O)
+template <typename GPtr, typename Sink>
+__device__ __forceinline__ void element_item_to(int v, GPtr G, Sink& K)
 {
     constexpr int V_BS = U_WD + U_DISC;
     const int u = (v < V_BS) ? v : (v < V_BS + U_BS ? U_MAIN + (v - V_BS) : v - U_BS);
@@ -719,12 +748,7 @@ __device__ __forceinline__ void element_item(int v, GPtr G, const ElemOut& O)
         // rho cos(alpha) = vx, rho sin(alpha) = vy  ->  |theta + alpha| < acos(kappa)
         const double srho = s * sqrt(vx * vx + vy * vy);
         const double kap = (srho > 0.0) ? -c * vz / srho : (c * vz > 0.0 ? -2.0 : 2.0);
-        double* D = O.don + uu * DON_STRIDE;
-        D[0] = vx;
-        D[1] = vy;
-        D[2] = vz;
-        D[3] = -atan2(vy, vx) * (1.0 / TWO_PI);
-        D[4] = acos(fmin(fmax(kap, -1.0), 1.0)) * (1.0 / TWO_PI);
+        K.donor(uu, vx, vy, vz, -atan2(vy, vx) * (1.0 / TWO_PI), acos(fmin(fmax(kap, -1.0), 1.0)) * (1.0 / TWO_PI));
         return;
     }
 
@@ -749,7 +773,6 @@ __device__ __forceinline__ void element_item(int v, GPtr G, const ElemOut& O)
     } else {  // bright-spot strip (MODEL_SPEC 5.3): no mirror partner
         const int j = u - U_MAIN;
         const double uk = (j + 0.5) * (G[G_UMAX] / NBS);
-        O.wbs[j] = bs_weight(j, G);
         const double off = G[G_L] * (uk - G[G_UPK]);
         Px = fma(off, G[G_CAZ], G[G_BSX]);
         Py = fma(off, G[G_SAZ], G[G_BSY]);
@@ -789,8 +812,8 @@ __device__ __forceinline__ void element_item(int v, GPtr G, const ElemOut& O)
 #else
     element_interval_fast(R, Px, Py, Pz, s, c, G[G_RCAL], G[G_REFF], a, b);
 #endif
-    if (u >= U_MAIN) O.abs[u - U_MAIN] = make_double2(a, b);
-    else O.abw[uslot(u)] = make_double2(a, b);
+    if (u >= U_MAIN) K.spot(u - U_MAIN, a, b, bs_weight(u - U_MAIN, G));
+    else K.wd_disc(u, a, b);
 }
 
 #ifdef LFG_PROFILE_ELEM  // diagnostic build only: per-wave start / end (s_memrealtime, 100 MHz), HW_ID, kind
@@ -2429,18 +2452,25 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
 // ------------------------------------------------------------------ k_pair
 // k_elements and k_lnlike<1, false> of one (walker, eclipse) pair in ONE
 // workgroup, for trees whose eclipses fit one tile (max_n <= LIKE_TILE, S =
-// 1, no GP): the pair's element intervals, spot and donor tables go from the
-// solver lanes to the block's LDS and never through HBM, and the half-step
+// 1, no GP): the element intervals never leave the workgroup, the half-step
 // is one launch instead of two (no kernel boundary behind a 10 MB table
-// write-back, no prologue re-fetch of the tables).
-//  * element phase: waves 0-6 solve two 64-item chunks of k_elements' item
-//    numbering each (paired long with short, PAIR_CHUNKS), wave 7 the last
-//    chunk (4 donor tiles and the 21 ring-weight lanes) and, on lanes 32..,
-//    this block's share of the speculative setup lanes of the next half
-//    (setup_any, as k_elements' leading blocks run them); every lane's
-//    results are in LDS at the phase barrier
-//  * likelihood phase: k_lnlike's single-tile sweep, scan, chi^2 and fused
-//    acceptance, its per-thread items read from LDS
+// write-back, no re-fetch of the tables), and the interval sweep runs inside
+// the element phase: a lane that has solved an element adds its runs to the
+// LDS difference arrays at once, while other waves are still solving.
+//  * prologue: every thread forms its point's window and phase (and its
+//    predecessor's, for the sortedness flags and the phase-index cells, so
+//    no barrier is needed for them), the disc ring weights (21 lanes);
+//  * element phase: 16 jobs, wave w takes job w and grabs the next free one
+//    from an LDS counter twice more.  Job 0: this block's share of the
+//    speculative setup lanes of the next half (setup_any, as k_elements'
+//    leading blocks run them); jobs 1..15: the 15 chunks of 64 items, longest
+//    first.  Each solved item is swept (element and mirror for WD/disc, the
+//    four mirrored donor tiles) with k_lnlike's run / point-mode rules.  The
+//    spot and donor sums are accumulated unnormalised (int64 fixed point at
+//    2^-54 / 2^-58, exact) with their totals, and normalised per point;
+//  * after the phase barrier: the block scan, each point's flux, chi^2, the
+//    fused acceptance.  Unsorted or invalid windows: the tables go to LDS and
+//    the point-major pass runs instead (as k_lnlike's).
 // With the fused acceptance the block writes its walker's row of pos while
 // the speculative lanes of other blocks read partner rows of the same half:
 // those lanes read the snapshot (SetupArgs.ppos) that the launch before took
@@ -2460,13 +2490,17 @@ struct PairArgs {
 // disc, donor, inner disc, WD: the Newton steps per region)
 __constant__ int kJobChunk[15] = {11, 12, 10, 9, 8, 13, 14, 7, 6, 5, 4, 3, 2, 1, 0};
 
+// fixed-point scales of k_pair's unnormalised spot and donor sums, as
+// factors into to_fx's 2^61: spot weights <= 1 (100 of them: 2^54), donor
+// vectors (their |v| sums stay far below 2^5: 2^58)
+constexpr double PAIR_SPOT_S = 1.0 / 128.0, PAIR_DON_S = 1.0 / 8.0;
+
 #ifdef LFG_PROFILE_PAIR  // diagnostic build only: s_memrealtime (100 MHz) stamps of each block's phases
 __device__ unsigned long long g_pair_t[20][4096];
 #define PAIR_STAMP(slot, cond)                                                     \
     do {                                                                           \
         if ((cond) && blockIdx.x < 4096) g_pair_t[slot][blockIdx.x] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
-// per wave (lane 0) inside the sweep: 0 counts done, 1 WD/disc applied, 2 spot/donor applied, 3 after B4
 __device__ unsigned long long g_pair_w[4][8][4096];
 #define PAIR_WSTAMP(k)                                                                                  \
     do {                                                                                                \
@@ -2477,25 +2511,158 @@ __device__ unsigned long long g_pair_w[4][8][4096];
 #define PAIR_WSTAMP(k)
 #endif
 
+// k_pair's sweep of one solved item (the element phase's sink): element runs
+// over the tile's windows (WD, disc, spot) and the donor tiles' visibility
+// arcs over the point phases, into the LDS difference arrays; or, for a tile
+// that goes point-major, the tables
+struct PairSink {
+    bool dir;
+    int lane;
+    PhaseIndex XW, XP;      // windows (lo, cells) and point phases (sph, scp)
+    const double* hi;
+    const double* iw;
+    unsigned long long (*acc)[LIKE_TILE + 1];   // sacc
+    unsigned long long (*acc2)[LIKE_TILE + 1];  // second WD/disc copies (odd lanes)
+    unsigned long long* tot;                    // [2] spot weight and donor quadrature sums
+    const double* swt;      // disc ring weights, disc total
+    double ul, itwd, s, c;  // ulimb, 1 / (2 pi (F(1) - F(0))), sin / cos i
+    double2* ab;            // point-major: the WD/disc intervals, spot intervals and weights, donor tiles
+    double2* sab;
+    double* sbw;
+    double* sdq;
+
+    __device__ __forceinline__ void wd_disc(int u, double a, double b)
+    {
+        if (dir) {
+            ab[uslot(u)] = make_double2(a, b);
+            return;
+        }
+        if (!(a < b)) return;
+        const int ir = uring(u);
+        const double wn = (u < U_WD) ? wd_ring_weight(ir, ul) * itwd : swt[ir - NWD_RINGS] * (1.0 / swt[NDISC_R]);
+        double q[4] = {a, b, -b, -a};  // the element and its mirror [-b, -a]
+        int J[4], Jb[4];
+        count_lt_multi<4>(XW, q, J);
+        count_le_back_multi<4>(hi, q, J, Jb);
+        unsigned long long* A = ((lane & 1) ? acc2 : acc)[(u < U_WD) ? 0 : 1];
+        apply_runs(Runs{Jb[0], J[0], Jb[1], J[1]}, a, b, wn, XW, hi, iw, A);
+        apply_runs(Runs{Jb[2], J[2], Jb[3], J[3]}, -b, -a, wn, XW, hi, iw, A);
+    }
+    __device__ __forceinline__ void spot(int j, double a, double b, double w)
+    {
+        sab[j] = make_double2(a, b);
+        sbw[j] = w;
+        atomicAdd(tot, static_cast<unsigned long long>(to_fx(w * PAIR_SPOT_S)));
+        if (!dir && a < b) apply_runs(element_runs(a, b, XW, hi), a, b, w * PAIR_SPOT_S, XW, hi, iw, acc[2]);
+    }
+    __device__ __forceinline__ void donor(int uu, double vx0, double vy0, double vz0, double cen0, double hw0)
+    {
+        double* D = sdq + uu * DON_STRIDE;
+        D[0] = vx0;
+        D[1] = vy0;
+        D[2] = vz0;
+        D[3] = cen0;
+        D[4] = hw0;
+        long long tn = 0;
+#pragma unroll 1
+        for (int mr = 0; mr < 4; ++mr) {  // the tile's mirror images, as k_lnlike's donor lanes form them
+            const double vx = vx0, vy = (mr & 1) ? -vy0 : vy0, vz = (mr & 2) ? -vz0 : vz0;
+            const double cen = (mr & 1) ? -cen0 : cen0;
+            const double hw = (mr & 2) ? 0.5 - hw0 : hw0;
+            tn += to_fx(fmax(-s * vy + c * vz, 0.0) * PAIR_DON_S);
+            if (dir || !(hw > 0.0)) continue;
+            const long long qx = to_fx(vx * PAIR_DON_S), qy = to_fx(vy * PAIR_DON_S), qz = to_fx(vz * PAIR_DON_S);
+            // visible for phases in (cen - hw, cen + hw) mod 1
+            double x1 = -INFINITY, x2 = INFINITY, y1 = 0.0, y2 = 0.0;
+            bool two = false;
+            if (hw < 0.5) {
+                const double lo = cen - hw, hi2 = cen + hw;
+                if (lo < -0.5) { x2 = hi2; y1 = lo + 1.0; y2 = INFINITY; two = true; }
+                else if (hi2 > 0.5) { x1 = lo; y1 = -INFINITY; y2 = hi2 - 1.0; two = true; }
+                else { x1 = lo; x2 = hi2; }
+            }
+            for (int i = 0; i < (two ? 2 : 1); ++i) {
+                const int P = count_below<true>(XP, i ? y1 : x1), Q = count_below<false>(XP, i ? y2 : x2);
+                if (P < Q) {
+                    fx_add(acc[3], P, qx);
+                    fx_add(acc[4], P, qy);
+                    fx_add(acc[5], P, qz);
+                    if (Q < XP.m) {
+                        fx_add(acc[3], Q, -qx);
+                        fx_add(acc[4], Q, -qy);
+                        fx_add(acc[5], Q, -qz);
+                    }
+                }
+            }
+        }
+        atomicAdd(tot + 1, static_cast<unsigned long long>(tn));
+    }
+};
+
+// point-major WD and disc eclipse fractions of one window (k_pair's
+// unsorted-tile pass: direct_wd_disc with the ring weights formed here)
+__device__ __forceinline__ double2 pair_direct_wd_disc(const double2* __restrict__ AB, double ul,
+                                                       const double* __restrict__ swt, double phc, double wk,
+                                                       double twd, double td)
+{
+    double ewd = 0.0, ed = 0.0;
+    const double lo = phc - wk, hi = phc + wk;
+    auto cover = [&](double2 ab) {
+        return (wk > 0.0) ? fmax(fmin(ab.y, hi) - fmax(ab.x, lo), 0.0) : ((phc > ab.x && phc < ab.y) ? 1.0 : 0.0);
+    };
+    for (int ring = 0; ring < NWD_RINGS + NDISC_R; ++ring) {  // each unique item and its mirror
+        const int u0 = ring < NWD_RINGS ? 2 * ring * ring : U_WD + (ring - NWD_RINGS) * (NDISC_AZ / 2);
+        const int u1 = ring < NWD_RINGS ? 2 * (ring + 1) * (ring + 1) : u0 + NDISC_AZ / 2;
+        double acc = 0.0;
+        for (int u = u0; u < u1; ++u) {
+            const double2 ab = AB[uslot(u)];
+            acc += cover(ab) + cover(mirror_ab(ab));
+        }
+        const double wr = ring < NWD_RINGS ? wd_ring_weight(ring, ul) : swt[ring - NWD_RINGS];
+        if (ring < NWD_RINGS) ewd = fma(wr, acc, ewd); else ed = fma(wr, acc, ed);
+    }
+    const double nrm = (wk > 0.0) ? 1.0 / (2.0 * wk) : 1.0;
+    return make_double2(ewd * nrm * (1.0 / twd), ed * nrm * (1.0 / td));
+}
+
+// window p of a pair's tile: phase, lo, hi (k_lnlike's put_window arithmetic)
+__device__ __forceinline__ void pair_window(const LikeArgs& L, int o0, int p, double phi0, double& ph, double& lo,
+                                            double& hi, double& hw)
+{
+    ph = wrap_phase(L.x[o0 + p] - phi0);
+    hw = L.w ? L.w[o0 + p] : 0.0;
+    lo = ph - hw;
+    hi = ph + hw;
+}
+
+// the cells of phase index (v sorted, v[0] = v0, v[m-1] = v1) that point p
+// fills, as build_cells does, from p's own value and its predecessor's
+__device__ __forceinline__ void pair_cells(int* cell, int p, int m, double vprev, double vown, double v0, double v1)
+{
+    const double span = v1 - v0, ginv = span > 0.0 ? LIKE_NC / span : 0.0;
+    auto ci = [&](double x) {
+        const double u = (x - v0) * ginv;
+        return u < 0.0 ? -1 : (u >= double(LIKE_NC) ? LIKE_NC : int(u));
+    };
+    const int g0 = p ? ci(vprev) : -1, g1 = ci(vown);
+    for (int g = g0 + 1; g <= g1; ++g) cell[g] = p;
+    if (p == m - 1)
+        for (int g = g1 + 1; g <= LIKE_NC; ++g) cell[g] = m;
+}
+
 __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
 {
     const LikeArgs& L = A.L;
     const ElemSpec& X = A.X;
-    __shared__ double sgeo[LFG_NGEO];
-    __shared__ double swr[NWD_RINGS + NDISC_R];
-    __shared__ double swn[NWD_RINGS + NDISC_R];
-    __shared__ double swt[NDISC_R + 1];           // disc ring weights and the disc total (ring-weight lanes)
+    __shared__ double swt[NDISC_R + 1];           // disc ring weights and the disc total (prologue)
     __shared__ double sbw[NBS];
     __shared__ double2 sab[NBS];
     __shared__ double sdq[U_DON * DON_STRIDE];
     __shared__ double sacc1[3];
-    __shared__ double snorm[4];
     __shared__ TileBufs TA;
     __shared__ double sph[LIKE_TILE];
-    // the WD/disc intervals live here from the element phase until every
-    // thread has its sweep items in registers; then the second difference
-    // arrays and the point-phase cells (unless the tile goes point-major,
-    // which reads the intervals in its pass)
+    // the second WD/disc difference arrays and the point-phase cells; or,
+    // for a tile that goes point-major, the WD/disc intervals
     __shared__ union PairU_ {
         struct {
             unsigned long long X[2][LIKE_TILE + 1];
@@ -2504,9 +2671,12 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
         double2 ab[NU_WDD];
     } SU;
     __shared__ unsigned long long sacc[6][LIKE_TILE + 1];
+    __shared__ unsigned long long stot[2];
     __shared__ long long spart[6][LIKE_THREADS / 64];
-    __shared__ double red[3][LIKE_THREADS / 64];
-    __shared__ int sflag[2];
+    __shared__ double red[LIKE_THREADS / 64];
+    __shared__ int sflagw[LIKE_THREADS / 64];
+    __shared__ int sflag[1];
+    __shared__ int sjob;
     __shared__ double sq[ACC_LDS];
     __shared__ double sy[LIKE_TILE], sye[LIKE_TILE];
 
@@ -2566,7 +2736,6 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
     if (tid == LFG_NGEO + 3) const_cast<int*>(L.status)[pair] = stp;
     const bool prej = L.prior && prior_rejects(lpr, G);
     const int st = (stp == ST_OK && prej) ? -1 : stp;  // -1: prior-rejected, straight to the -inf finish
-    if (tid < LFG_NGEO) sgeo[tid] = G[tid];
     // the other half's rows for the next launch's speculative lanes
     if (A.snap_dst && e == 0)
         for (int d = tid; d < L.ndim; d += nt) A.snap_dst[size_t(w) * L.ndim + d] = A.snap_src[size_t(w) * L.ndim + d];
@@ -2578,26 +2747,53 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
         sacc1[1] = zf;
         sacc1[2] = L.lnp_ens[L.half * npairs + pair];
     }
-    // this thread's point (one tile: m = n points) into LDS; its window is
-    // formed after the element phase (nothing held in registers through it)
+    // this thread's point (one tile: m = n points): window and phase into LDS,
+    // its sortedness against the predecessor, and the cells it fills of the
+    // two phase indices (windows' lo, point phases), formed from its own and
+    // its predecessor's windows, so that no barrier separates them
     const bool own = tid < n;
+    const int m = n;
+    int fl = 0;
     if (own) {
-        sph[tid] = L.x[o0 + tid];
-        TA.iw[tid] = L.w ? L.w[o0 + tid] : 0.0;
+        const double phi0 = Gc[G_PHI0];
+        double ph, lo, hi, hw;
+        pair_window(L, o0, tid, phi0, ph, lo, hi, hw);
+        TA.lo[tid] = lo;
+        TA.hi[tid] = hi;
+        TA.iw[tid] = 1.0 / (2.0 * hw);
+        sph[tid] = ph;
         sy[tid] = L.y[o0 + tid];
         sye[tid] = L.ye[o0 + tid];
+        double php = 0.0, lop = 0.0, hip = 0.0, hwp, ph0, lo0, hi0, hw0, ph1, lo1, hi1, hw1;
+        if (tid) pair_window(L, o0, tid - 1, phi0, php, lop, hip, hwp);
+        pair_window(L, o0, 0, phi0, ph0, lo0, hi0, hw0);
+        pair_window(L, o0, m - 1, phi0, ph1, lo1, hi1, hw1);
+        fl = (hw >= 0.0) ? 0 : 4;  // negative or NaN widths: point-major
+        if (tid && (lo < lop || hi < hip || ph < php)) fl = 4;
+        pair_cells(TA.cell, tid, m, lop, lo, lo0, lo1);
+        pair_cells(SU.s.scp, tid, m, php, ph, ph0, ph1);
+    }
+    {
+        const int wf = wave_or4(fl);
+        if (lane == 0) sflagw[wv] = wf;
     }
     for (int i = 0; i < 6; ++i) sacc[i][tid] = 0ull;
+    SU.s.X[0][tid] = 0ull;
+    SU.s.X[1][tid] = 0ull;
     if (tid == 0) {
         for (int i = 0; i < 6; ++i) sacc[i][nt] = 0ull;
-        sflag[0] = 0;
-        sflag[1] = 0;
+        SU.s.X[0][nt] = 0ull;
+        SU.s.X[1][nt] = 0ull;
+        stot[0] = stot[1] = 0ull;
+        sjob = 8;
     }
+    // the disc ring weights (MODEL_SPEC 5.2): wave 7's lanes 0..NDISC_R
+    if (st == ST_OK && wv == 7 && lane <= NDISC_R) ring_weight_lane(lane, Gc, swt);
+    __syncthreads();  // B0: windows, cells, flags, zeroed sums, ring weights, sjob
+    PAIR_STAMP(16, tid == 0);
 
-    __shared__ int sjob;
-    if (tid == 0) sjob = 8;
-    __syncthreads();  // B0: sjob
-
+    bool dir = false;
+    for (int k = 0; k < nw; ++k) dir = dir || sflagw[k] != 0;
     // ---- element phase: 16 jobs.  Job 0: this block's speculative setup
     // lanes of the next half; jobs 1..15: the 15 item chunks, longest first
     // (kJobChunk).  Wave w takes job w, then grabs the next free job from
@@ -2618,19 +2814,18 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
 #endif
         }
     }
-    if (st == ST_OK) {
-        const ElemOut O{SU.ab, sab, sdq, swt, sbw};
-        // chunk c: items v = 64 c + lane (c < 13: WD, disc, spot; 13: donor;
-        // 14: the last 36 donor tiles and the 21 ring-weight lanes)
+    if (st == ST_OK && m > 0) {
+        const double ul = Gc[G_ULIMB];
+        PairSink K{dir, lane, phase_index(TA.lo, TA.cell, m), phase_index(sph, SU.s.scp, m), TA.hi, TA.iw, sacc,
+                   SU.s.X, stot, swt, ul, 1.0 / (TWO_PI * ((1.0 - ul) * 0.5 + ul / 3.0)), Gc[G_S], Gc[G_C],
+                   SU.ab, sab, sbw, sdq};
+        // chunk c: items v = 64 c + lane (c < 13: WD, disc, spot; 13, 14: donor)
         auto chunk = [&](int j) {
             const int c = kJobChunk[j - 1];
-            int v = -1, rb = -1;
+            int v = -1;
             if (c < 13) v = (c * 64 + lane < U_WD + U_DISC + U_BS) ? c * 64 + lane : -1;
-            else if (c == 13) v = U_WD + U_DISC + U_BS + lane;
-            else if (lane < 36) v = U_WD + U_DISC + U_BS + 64 + lane;
-            else if (lane < 36 + NDISC_R + 1) rb = lane - 36;
-            if (v >= 0) element_item(v, Gc, O);
-            else if (rb >= 0) ring_weight_lane(rb, Gc, swt);
+            else if (c == 13 || lane < U_DON - 64) v = U_WD + U_DISC + U_BS + (c - 13) * 64 + lane;
+            if (v >= 0) element_item_to(v, Gc, K);
         };
         auto grab = [&]() {
             int j = 0;
@@ -2646,9 +2841,9 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
         if (j < 16) chunk(j);
     }
     static_assert(13 * 64 >= U_WD + U_DISC + U_BS && 12 * 64 < U_WD + U_DISC + U_BS, "13 chunks of WD/disc/spot");
-    static_assert(U_DON == 64 + 36 && 36 + NDISC_R + 1 <= 64, "the donor and ring-weight chunks");
+    static_assert(U_DON > 64 && U_DON <= 128, "two donor chunks");
     PAIR_STAMP(1 + wv, lane == 0);
-    __syncthreads();  // B1: the tables, swt, sflag reset, windows
+    __syncthreads();  // B1: the sums (or the tables)
     PAIR_STAMP(9, tid == 0);
 
     if (st != ST_OK) {
@@ -2656,142 +2851,55 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
         finish_walker(L, pair, tid, acc1, sq, sacc1, sflag);
         return;
     }
-    // ---- likelihood phase (k_lnlike<1, false>, one tile)
-    const double wk = own ? TA.iw[tid] : 0.0;
-    const double phc = wrap_phase(own ? sph[tid] - sgeo[G_PHI0] : 0.0);
-    int flA = put_window(TA, tid, own, phc, wk);
-    if (own) sph[tid] = phc;
-    __syncthreads();  // B1b: the windows
-    flA |= check_sorted(TA, tid, own);
-    const int flB = (flA & 7) | ((own && tid && sph[tid] < sph[tid - 1]) ? 4 : 0);
-    {
-        const int wfA = wave_or4(flA), wfB = wave_or4(flB);
-        if (lane == 0 && wfA) atomicOr(&sflag[0], wfA);
-        if (lane == 0 && wfB) atomicOr(&sflag[1], wfB);
-    }
-    const int m = n;
-    if (m > 0) build_cells(TA.lo, m, TA.cell, tid);
-    const double s = sgeo[G_S], c = sgeo[G_C], ul = sgeo[G_ULIMB];
-    const double td = swt[NDISC_R];
-    constexpr int NI = (NWD + NDISC + nt - 1) / nt;
-    double2 abk[NI];
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-        const int g = tid + i * nt;
-        abk[i] = (g < NWD + NDISC) ? sweep_ab(SU.ab, g) : make_double2(1.0, -1.0);
-    }
-    double tb = 0.0, dn = 0.0, vs = 0.0, wring = 0.0;
-    if (tid < NBS) {
-        tb = sbw[tid];
-    } else if (tid >= nt - NDONOR) {
-        // donor normalisation at quadrature (theta = pi/2): e = (0, -s, c)
-        const int t = tid - (nt - NDONOR), mr = t & 3;
-        const double* dq = sdq + (t >> 2) * DON_STRIDE;
-        const double vy = (mr & 1) ? -dq[1] : dq[1], vz = (mr & 2) ? -dq[2] : dq[2];
-        dn = fmax(-s * vy + c * vz, 0.0);
-        vs = fabs(dq[0]) + fabs(dq[1]) + fabs(dq[2]);
-    }
-    if (tid >= NBS && tid < NBS + NWD_RINGS) wring = wd_ring_weight(tid - NBS, ul);
-    else if (tid >= NBS + NWD_RINGS && tid < NBS + NWD_RINGS + NDISC_R) wring = swt[tid - NBS - NWD_RINGS];
-    if (tid >= NBS && tid < NBS + NWD_RINGS + NDISC_R) swr[tid - NBS] = wring;
-    tb = wave_sum(tb);
-    dn = wave_sum(dn);
-    vs = wave_sum(vs);
-    if (lane == 0) { red[0][wv] = tb; red[1][wv] = dn; red[2][wv] = vs; }
-    __syncthreads();  // B2: every read of SU.ab (unless point-major), the flags, the partials
-    PAIR_STAMP(10, tid == 0);
-    if (wv == 0) {
-        double p0 = 0.0, p1 = 0.0, p2 = 0.0;
-        if (lane < nw) { p0 = red[0][lane]; p1 = red[1][lane]; p2 = red[2][lane]; }
-        p0 = wave_sum(p0);
-        p1 = wave_sum(p1);
-        p2 = wave_sum(p2);
-        if (lane == 0) {
-            snorm[0] = 1.0 / p0;
-            snorm[1] = 1.0 / p2;
-            snorm[2] = p1;
-            snorm[3] = p2;
-        }
-    }
-    const double twd = TWO_PI * ((1.0 - ul) * 0.5 + ul / 3.0);  // 2 pi [F(1) - F(0)]
-    if (tid >= NBS && tid < NBS + NWD_RINGS + NDISC_R)
-        swn[tid - NBS] = wring * ((tid - NBS < NWD_RINGS) ? 1.0 / twd : 1.0 / td);
-    const bool dir = (sflag[0] & 7) != 0 || sflag[1] != 0;
-    if (!dir) {
-        SU.s.X[0][tid] = 0ull;
-        SU.s.X[1][tid] = 0ull;
-        if (tid == 0) { SU.s.X[0][nt] = 0ull; SU.s.X[1][nt] = 0ull; }
-        if (m > 0) build_cells(sph, m, SU.s.scp, tid);
-    }
-    __syncthreads();  // B3
-    PAIR_STAMP(11, tid == 0);
+    // ---- each point's flux and chi^2
     double chi = 0.0;
-    if (n > 0) {
+    if (m > 0) {
+        const double s = Gc[G_S], c = Gc[G_C], ul = Gc[G_ULIMB];
+        const double twd = TWO_PI * ((1.0 - ul) * 0.5 + ul / 3.0);  // 2 pi [F(1) - F(0)]
+        const double wspot = double(static_cast<long long>(stot[0])) * (FX_INV / PAIR_SPOT_S);
+        const double dn = double(static_cast<long long>(stot[1])) * (FX_INV / PAIR_DON_S);
+        const double phc = own ? sph[tid] : 0.0;
         double fw = 0.0, fd = 0.0, eb = 0.0, R3 = 0.0, R4 = 0.0, R5 = 0.0;
         if (dir) {
             if (own) {
-                const double2 f2 = direct_wd_disc(SU.ab, swr, phc, wk, twd, td);
+                const double wk = L.w ? L.w[o0 + tid] : 0.0;
+                const double2 f2 = pair_direct_wd_disc(SU.ab, ul, swt, phc, wk, twd, swt[NDISC_R]);
                 fw = f2.x;
                 fd = f2.y;
-                eb = direct_spot(sab, sbw, phc, wk, snorm[0]);
+                eb = direct_spot(sab, sbw, phc, wk, 1.0 / wspot);
             }
         } else {
-            const PhaseIndex XI = phase_index(TA.lo, TA.cell, m);
-            double qx[2 * NI];
-            int J[2 * NI], Jb[2 * NI];
-#pragma unroll
-            for (int i = 0; i < NI; ++i) {
-                qx[2 * i] = abk[i].x;
-                qx[2 * i + 1] = abk[i].y;
-            }
-            count_lt_multi<2 * NI>(XI, qx, J);
-            count_le_back_multi<2 * NI>(TA.hi, qx, J, Jb);
-            PAIR_WSTAMP(0);
-#pragma unroll
-            for (int i = 0; i < NI; ++i)
-                if (abk[i].x < abk[i].y) {
-                    const int g = tid + i * nt;
-                    const int u = uitem(g < NU_WDD ? g : g - NU_WDD);
-                    apply_runs(Runs{Jb[2 * i], J[2 * i], Jb[2 * i + 1], J[2 * i + 1]}, abk[i].x, abk[i].y,
-                               swn[uring(u)], XI, TA.hi, TA.iw, ((lane & 1) ? SU.s.X : sacc)[(u < U_WD) ? 0 : 1]);
-                }
-            PAIR_WSTAMP(1);
-            sweep_spot_donor(tid, XI, TA, phase_index(sph, SU.s.scp, m), sab, sbw, snorm[0], sdq, snorm[1], sacc + 2);
-            PAIR_WSTAMP(2);
-            __syncthreads();  // B4
-            PAIR_WSTAMP(3);
             long long r[6] = {0, 0, 0, 0, 0, 0};
             block_scan<6>(sacc, spart, tid, r, SU.s.X);
             PAIR_STAMP(12, tid == 0);
             fw = double(r[0]) * FX_INV;
             fd = double(r[1]) * FX_INV;
-            eb = double(r[2]) * FX_INV;
+            eb = double(r[2]) * (FX_INV / PAIR_SPOT_S) / wspot;
             R3 = double(r[3]);
             R4 = double(r[4]);
             R5 = double(r[5]);
         }
-        const double sg = sgeo[G_S], cg = sgeo[G_C];
-        const double bden = sgeo[G_BDEN], fis = sgeo[G_FIS];
         const double2 scp2 = sincospi_ool(2.0 * phc);
-        const double e0 = sg * scp2.y, e1 = -sg * scp2.x;
+        const double e0 = s * scp2.y, e1 = -s * scp2.x;
         double D = 0.0;
-        if (!dir) D = (e0 * R3 + e1 * R4 + cg * R5) * (FX_INV * snorm[3]);
-        else if (own) D = direct_donor(sdq, e0, e1, cg);
+        if (!dir) D = (e0 * R3 + e1 * R4 + c * R5) * (FX_INV / PAIR_DON_S);
+        else if (own) D = direct_donor(sdq, e0, e1, c);
         double beam = 0.0;
-        if (bden > 0.0) beam = (fis + (1.0 - fis) * fmax(sgeo[G_NB0] * e0 + sgeo[G_NB1] * e1 + sgeo[G_NB2] * cg, 0.0)) / bden;
-        const double sbs = beam * (1.0 - eb), srs = D / snorm[2];
+        const double bden = Gc[G_BDEN], fis = Gc[G_FIS];
+        if (bden > 0.0) beam = (fis + (1.0 - fis) * fmax(Gc[G_NB0] * e0 + Gc[G_NB1] * e1 + Gc[G_NB2] * c, 0.0)) / bden;
+        const double sbs = beam * (1.0 - eb), srs = D / dn;
         if (own) {
-            const double f = sgeo[G_WDF] * (1.0 - fw) + sgeo[G_DF] * (1.0 - fd) + sgeo[G_SF] * sbs + sgeo[G_RSF] * srs;
+            const double f = Gc[G_WDF] * (1.0 - fw) + Gc[G_DF] * (1.0 - fd) + Gc[G_SF] * sbs + Gc[G_RSF] * srs;
             const double rr = (sy[tid] - f) / sye[tid];
             chi = isnan(f) ? INFINITY : rr * rr;
         }
     }
     chi = wave_sum(chi);
-    if (lane == 0) red[1][wv] = chi;
+    if (lane == 0) red[wv] = chi;
     __syncthreads();
     if (tid == 0) {
         double tot = 0.0;
-        for (int i = 0; i < nw; ++i) tot += red[1][i];
+        for (int i = 0; i < nw; ++i) tot += red[i];
         L.lle[pair] = -0.5 * tot;
     }
     PAIR_STAMP(13, tid == 0);

@@ -45,10 +45,12 @@ t0 = t[0]
 span = (t[15].max() - t0.min()) / 100.0
 print("blocks %d, launch span %.2f us (first start -> last finish)" % (nb, span))
 print("block start spread: %s us" % np.percentile((t0 - t0.min()) / 100.0, [0, 50, 90, 100]).round(2))
-rows = [("wave %d elements" % k, 1 + k) for k in range(8)] + [
-    ("B1 (phase barrier)", 9), ("B2 (items, norms)", 10), ("B3 (cells)", 11), ("sweep + scan", 12),
+rows = [("B0 (prologue)", 16)] + [("wave %d elements" % k, 1 + k) for k in range(8)] + [
+    ("B1 (phase barrier)", 9), ("B2 (items, norms)", 10), ("B3 (cells)", 11), ("scan", 12),
     ("chi^2", 13), ("finish", 15)]
 for name, k in rows:
+    if not t[k].any():
+        continue
     d = (t[k] - t0) / 100.0
     print("%-22s median %7.2f  p90 %7.2f  max %7.2f us" % (name, np.median(d), np.percentile(d, 90), d.max()))
 kind = t[17].astype(int)
@@ -56,15 +58,15 @@ for k, nm in ((0, "setup"), (1, "prior"), (2, "stream")):
     m = kind == k
     if m.any():
         pre = (t[16][m] - t0[m]) / 100.0
-        spec = (t[8][m] - t[16][m]) / 100.0
+        spec = (t[1][m] - t[16][m]) / 100.0   # wave 0: its job 0 (the speculative lanes) and the chunks it grabbed
         fin_k = (t[15][m] - t0[m]) / 100.0
-        print("spec kind %-6s blocks %3d: wave 7 pre-spec median %6.2f | spec part median %6.2f p90 %6.2f max %6.2f"
+        print("spec kind %-6s blocks %3d: B0 median %6.2f | wave 0 after B0 median %6.2f p90 %6.2f max %6.2f"
               " | block finish median %6.2f max %6.2f" % (nm, m.sum(), np.median(pre), np.median(spec),
                                                         np.percentile(spec, 90), spec.max(), np.median(fin_k), fin_k.max()))
 fin = (t[15] - t0.min()) / 100.0
 print("block finish times from launch start: %s us" % np.percentile(fin, [0, 10, 50, 90, 100]).round(2))
 wv = np.zeros((4, 8, 4096), dtype=np.uint64)
-if L.lfg_debug_pair_waves(ctypes.c_void_p(wv.ctypes.data)) == 0:
+if L.lfg_debug_pair_waves(ctypes.c_void_p(wv.ctypes.data)) == 0 and wv.any():
     wv = wv[:, :, :nb].astype(np.float64)
     b3 = t[11]
     print("sweep per wave from B3 (us): median over blocks of [earliest wave, latest wave]")
