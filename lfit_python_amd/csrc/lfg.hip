@@ -2476,6 +2476,7 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
 // those lanes read the snapshot (SetupArgs.ppos) that the launch before took
 // of that half, and this launch snapshots the other half for the next one.
 typedef const __attribute__((address_space(4))) double* CGeo;
+constexpr int DCP_LANES = 16, DCP_NTHETA = 10;  // k_gp_dcp / k_pair<true>: limb points of wdphases
 
 struct PairArgs {
     LikeArgs L;
@@ -2650,6 +2651,11 @@ __device__ __forceinline__ void pair_cells(int* cell, int p, int m, double vprev
         for (int g = g1 + 1; g <= LIKE_NC; ++g) cell[g] = m;
 }
 
+// GP (GP trees, MODE 2 of k_lnlike): instead of chi^2 the residuals, each
+// point's e^{-lam dx} and changepoint block go to the workspace for
+// k_gp_like, and a walker that tripped the changepoint cache rule has its
+// distance solved here (k_gp_dcp's ten limb points, on wave 0's lanes 32..)
+template <bool GP>
 __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
 {
     const LikeArgs& L = A.L;
@@ -2763,7 +2769,11 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
         TA.iw[tid] = 1.0 / (2.0 * hw);
         sph[tid] = ph;
         sy[tid] = L.y[o0 + tid];
-        sye[tid] = L.ye[o0 + tid];
+        if (!GP) sye[tid] = L.ye[o0 + tid];
+        if (GP) {  // the Kalman filter's transition factor of this point (k_gp_like)
+            const double xp = L.x[o0 + tid], dx = xp - (tid ? L.x[o0 + tid - 1] : xp);
+            L.gpx[size_t(pair) * L.N + tid] = exp(-(Gc[G_GP_LAM] * dx));
+        }
         double php = 0.0, lop = 0.0, hip = 0.0, hwp, ph0, lo0, hi0, hw0, ph1, lo1, hi1, hw1;
         if (tid) pair_window(L, o0, tid - 1, phi0, php, lop, hip, hwp);
         pair_window(L, o0, 0, phi0, ph0, lo0, hi0, hw0);
@@ -2814,6 +2824,46 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
 #endif
         }
     }
+    __shared__ double sdcp;
+    if (GP) {
+        // the changepoint distance: the cache's, or (cache rule tripped,
+        // G_GP_OK = 2) dist_cp = (dphi + phi4 - phi3) / 2 from ten limb
+        // points' egress phases (CVModel.py:561-570; k_gp_dcp's solve)
+        const bool pend = st == ST_OK && Gc[G_GP_OK] == 2.0;
+        if (pend && wv == 0 && lane >= 32 && lane < 32 + DCP_LANES) {
+            const int k = lane - 32;
+            bool ok = Gc[G_GP_RWD] > 0.0;
+            double b = NAN;
+            if (ok && k < DCP_NTHETA) {
+                const Roche R{Gc[G_Q], Gc[G_CA], Gc[G_CB], Gc[G_MU], Gc[G_XL1], Gc[G_PL1], Gc[G_RS], Gc[G_RS2]};
+                const double s = Gc[G_S], c = Gc[G_C], r1 = Gc[G_GP_RWD];
+                double dphi_c;
+                if (findphi_fast(R, Gc[G_INC], dphi_c) == ST_OK) {
+                    double sth, cth, sp, cp, a;
+                    sincos(PI * dphi_c, &sth, &cth);
+                    sincos(TWO_PI * k / DCP_NTHETA, &sp, &cp);
+                    if (!element_interval(R, r1 * (cp * sth - sp * c * cth), r1 * (cp * cth + sp * c * sth),
+                                          r1 * (sp * s), s, c, eggleton(R.q), a, b))
+                        b = NAN;
+                }
+            }
+            double lo = isnan(b) ? INFINITY : b, hi = isnan(b) ? -INFINITY : b;
+            for (int off = DCP_LANES / 2; off > 0; off >>= 1) {
+                lo = fmin(lo, __shfl_xor(lo, off, DCP_LANES));
+                hi = fmax(hi, __shfl_xor(hi, off, DCP_LANES));
+            }
+            if (k == 0) {
+                ok = ok && lo <= hi;  // no eclipsed limb point: wdphases fails
+                const double d = ok ? (Gc[G_GP_DPHI] + (hi - lo)) / 2.0 : NAN;
+                double* Gd = const_cast<double*>(L.geo) + size_t(pair) * LFG_NGEO;  // the standard slot
+                Gd[G_GP_DCP] = d;
+                Gd[G_GP_OK] = ok ? 1.0 : 0.0;
+                sdcp = d;
+            }
+        } else if (!pend && tid == 0) {
+            sdcp = Gc[G_GP_DCP];
+        }
+    }
     if (st == ST_OK && m > 0) {
         const double ul = Gc[G_ULIMB];
         PairSink K{dir, lane, phase_index(TA.lo, TA.cell, m), phase_index(sph, SU.s.scp, m), TA.hi, TA.iw, sacc,
@@ -2847,11 +2897,12 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
     PAIR_STAMP(9, tid == 0);
 
     if (st != ST_OK) {
+        if (GP) return;  // k_gp_like sees the status (or the prior) and finishes the pair
         if (tid == 0) L.lle[pair] = -INFINITY;
         finish_walker(L, pair, tid, acc1, sq, sacc1, sflag);
         return;
     }
-    // ---- each point's flux and chi^2
+    // ---- each point's flux and chi^2 (GP: residual, changepoint block)
     double chi = 0.0;
     if (m > 0) {
         const double s = Gc[G_S], c = Gc[G_C], ul = Gc[G_ULIMB];
@@ -2890,10 +2941,17 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
         const double sbs = beam * (1.0 - eb), srs = D / dn;
         if (own) {
             const double f = Gc[G_WDF] * (1.0 - fw) + Gc[G_DF] * (1.0 - fd) + Gc[G_SF] * sbs + Gc[G_RSF] * srs;
-            const double rr = (sy[tid] - f) / sye[tid];
-            chi = isnan(f) ? INFINITY : rr * rr;
+            if (GP) {
+                const size_t q = size_t(pair) * L.N + tid;
+                L.res[q] = sy[tid] - f;
+                L.gpb[q] = gp_block(L.x[o0 + tid], L.gp_ecl[2 * e], L.gp_ecl[2 * e + 1], sdcp, Gc[G_PHI0]);
+            } else {
+                const double rr = (sy[tid] - f) / sye[tid];
+                chi = isnan(f) ? INFINITY : rr * rr;
+            }
         }
     }
+    if (GP) return;  // k_gp_like forms ln_like from the residuals
     chi = wave_sum(chi);
     if (lane == 0) red[wv] = chi;
     __syncthreads();
@@ -2915,7 +2973,6 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
 // (the nested eclipse solver), min / max by shuffles; other pairs return at
 // once.  Runs after k_elements (the pair's record is in the standard slot)
 // and before k_lnlike<2>, which reads G_GP_DCP.
-constexpr int DCP_LANES = 16, DCP_NTHETA = 10;
 __global__ __launch_bounds__(64) void k_gp_dcp(double* __restrict__ geo, const int* __restrict__ status, int npairs)
 {
     const int pair = int(blockIdx.x) * (64 / DCP_LANES) + int(threadIdx.x) / DCP_LANES;
@@ -3640,7 +3697,8 @@ static bool pair_ok(int gp, int nsub, int max_n, int ndim)
         const char* e = getenv("LFG_PAIR");
         return e && e[0] == '1';
     }();
-    return env && !gp && nsub == 1 && max_n <= LIKE_TILE && ndim <= LIKE_THREADS;
+    (void)gp;
+    return env && nsub == 1 && max_n <= LIKE_TILE && ndim <= LIKE_THREADS;
 }
 
 int lfg_layout(const lfg_tree* T)
@@ -3666,7 +3724,7 @@ int lfg_lnlike(const double* pars, int W, int P, const double* x, const double* 
                nsub, nullptr, nullptr, lnlike, W, nullptr, nullptr, nullptr, false, nullptr,
                nullptr, nullptr, nullptr, 0, 0, 0ull, 0ull, nullptr};
     L.bstatus = ws.bstatus;
-    if (pair) hipLaunchKernelGGL(k_pair, dim3(W), dim3(LIKE_THREADS), 0, st, PairArgs{L, ElemSpec{}, nullptr, nullptr, 0, 0});
+    if (pair) hipLaunchKernelGGL(k_pair<false>, dim3(W), dim3(LIKE_THREADS), 0, st, PairArgs{L, ElemSpec{}, nullptr, nullptr, 0, 0});
     else if (nsub > 1) hipLaunchKernelGGL((k_lnlike<1, true>), dim3(W), dim3(LIKE_THREADS), 0, st, L);
     else hipLaunchKernelGGL((k_lnlike<1, false>), dim3(W), dim3(LIKE_THREADS), 0, st, L);
     if ((rc = launch_ok())) return rc;
@@ -3807,7 +3865,17 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
             A.snap_src = prop->pos + size_t(hn) * rows;
             A.snap_dst = ws.snap + size_t(hn) * ws.accstride * T->ndim;
         }
-        hipLaunchKernelGGL(k_pair, dim3(npairs), dim3(LIKE_THREADS), 0, st, A);
+        if (T->gp) {
+            L.res = ws.res;
+            L.gpx = ws.gpx;
+            L.gpb = ws.gpb;
+            A.L = L;
+            hipLaunchKernelGGL(k_pair<true>, dim3(npairs), dim3(LIKE_THREADS), 0, st, A);
+            if ((rc = launch_ok())) return rc;
+            hipLaunchKernelGGL(k_gp_like, dim3(T->E * ((W + GP_PAIRS - 1) / GP_PAIRS)), dim3(GP_BLOCK), 0, st, L);
+        } else {
+            hipLaunchKernelGGL(k_pair<false>, dim3(npairs), dim3(LIKE_THREADS), 0, st, A);
+        }
         if ((rc = launch_ok())) return rc;
         if (T->E > 1) {
             hipLaunchKernelGGL(k_combine_walkers, dim3((W + 3) / 4), dim3(256), 0, st, L);
