@@ -2023,7 +2023,7 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
     c = G[G_C];
     ul = G[G_ULIMB];
     td = Wt[WT_TD];
-    if (tid < n) {
+    if (!SUB && tid < n) {  // (S > 1: at the first tile, after the table build it would be held through)
         px = L.x[o0 + tid];
         pw = L.w ? L.w[o0 + tid] : 0.0;
     }
@@ -2282,13 +2282,13 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
         const int m = min(LIKE_TILE, n - t0);
         LIKE_STAMP(0);
         const bool own = tid < m;
-        if (t0 > 0 && own) {
+        if ((t0 > 0 || SUB) && own) {
             // the point index re-formed from a fresh (volatile) read of the
             // offset: o0 + tid would otherwise be held, spilled, over the tiles
             const int p = (offs ? *reinterpret_cast<const volatile int*>(L.off + e) : 0) + t0 + tid;
             px = L.x[p];
             pw = L.w ? L.w[p] : 0.0;
-            if (CHI) {
+            if (CHI && t0 > 0) {
                 sy[tid] = L.y[p];
                 if (!GP) sye[tid] = L.ye[p];
             }
@@ -2345,11 +2345,17 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
             if (wdd) {
                 if constexpr (TAB) {
                     // re-read per tile (L2): held over the tiles they would not
-                    // leave the sub-bin queries their registers
+                    // leave the sub-bin queries their registers.  The pointer is
+                    // laundered through an empty asm so that the compiler cannot
+                    // reuse the prologue's loads of the same (restrict) table:
+                    // it kept those values live through the table build, 48 B
+                    // of scratch per lane
+                    const double2* ABt = AB;
+                    asm volatile("" : "+s"(ABt));
 #pragma unroll
                     for (int i = 0; i < NI; ++i) {
                         const int g = tid + i * nt;
-                        abk[i] = (g < NWD + NDISC) ? sweep_ab(AB, g) : make_double2(1.0, -1.0);
+                        abk[i] = (g < NWD + NDISC) ? sweep_ab(ABt, g) : make_double2(1.0, -1.0);
                     }
                 }
                 const PhaseIndex X = phase_index(TA.lo, TA.cell, m);

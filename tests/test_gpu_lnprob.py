@@ -591,3 +591,35 @@ def test_lfg_lnlike_matches_tree_and_cpu_twin(oracle, nsub, tmp_path):
     ok = st2 == 0
     np.testing.assert_allclose(got[ok], twin[ok], rtol=1e-10, atol=1e-8)
     assert np.all(np.isneginf(got[~ok]))
+
+
+def test_chunked_production_keeps_device_memory_flat(tmp_path):
+    """mcmc_utils.run_mcmc_save in chunks (as mcmcfit does): each run's
+    stored chunk moves to host memory when the run ends, so device memory
+    after every chunk is the same however many chunks were written (ADVICE
+    r03: the chunks used to stay on the device until reset()); last_run()
+    is the most recent run's chunk, and None after a run that stored nothing."""
+    import torch
+    from lfit_python_amd import batch, mcmc_utils, sampler, synthetic
+    m = synthetic.config_single(300, flux_fn=_flux_fn)
+    t = batch.compile_tree(m)
+    ev = batch.LnProbEvaluator(t)
+    p0 = np.array(m.dynasty_par_vals)
+    W = 64
+    init = sampler.initialise_walkers(p0, sampler.comp_scatter(m.dynasty_par_names, 0.1), W,
+                                      lambda p: ev(torch.as_tensor(p, device="cuda")).cpu().numpy())
+    S = sampler.EnsembleSampler(W, t.ndim, ev, seed=5)
+    pos, lnp, st = S.run_mcmc(init, 2, storechain=False)
+    assert S.last_run() is None
+    used = []
+    for k in range(6):
+        S.run_mcmc(None, 10, storechain=True)
+        torch.cuda.synchronize()
+        used.append(torch.cuda.memory_allocated())
+        ch, lp = S.last_run()
+        assert ch.shape == (10, W, t.ndim) and ch.device.type == "cpu"
+    assert max(used) == min(used), used
+    assert S.chain.shape == (W, 60, t.ndim)
+    np.testing.assert_array_equal(S.chain[:, -10:], np.asarray(ch).transpose(1, 0, 2))
+    S.run_mcmc(None, 3, storechain=False)
+    assert S.last_run() is None
