@@ -2489,8 +2489,8 @@ struct PairArgs {
     ElemSpec X;                // candidate selection (X.jk) and speculative lanes (X.nspec, X.S)
     const double* snap_src;    // nullable: rows [ns][ndim] of the other half of pos, copied to snap_dst
     double* snap_dst;
-    int spl;                   // speculative lanes per block (<= 64: wave 0's job 0)
-    int nbc;                   // blocks [0, nbc) carry candidate 0's lanes, the rest candidate 1's
+    int spl;                   // speculative lanes per block that has them (64: wave 0's job 0)
+    int nbc;                   // blocks [0, nbc) carry candidate 0's lanes, [nbc, 2 nbc) candidate 1's
 };
 
 // the chunks of k_pair's element jobs 1..15, longest first (spot, outer
@@ -2632,12 +2632,12 @@ __device__ __forceinline__ double2 pair_direct_wd_disc(const double2* __restrict
     return make_double2(ewd * nrm * (1.0 / twd), ed * nrm * (1.0 / td));
 }
 
-// window p of a pair's tile: phase, lo, hi (k_lnlike's put_window arithmetic)
-__device__ __forceinline__ void pair_window(const LikeArgs& L, int o0, int p, double phi0, double& ph, double& lo,
-                                            double& hi, double& hw)
+// a point's window: phase, lo, hi (k_lnlike's put_window arithmetic)
+__device__ __forceinline__ void pair_window(double x, double w, double phi0, double& ph, double& lo, double& hi,
+                                            double& hw)
 {
-    ph = wrap_phase(L.x[o0 + p] - phi0);
-    hw = L.w ? L.w[o0 + p] : 0.0;
+    ph = wrap_phase(x - phi0);
+    hw = w;
     lo = ph - hw;
     hi = ph + hw;
 }
@@ -2698,9 +2698,11 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
     PAIR_STAMP(0, tid == 0);
 #ifdef LFG_PROFILE_PAIR
     if (tid == 0 && blockIdx.x < 4096) {
-        unsigned hw;
+        unsigned hw, xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
         g_pair_t[14][blockIdx.x] = hw;
+        g_pair_t[18][blockIdx.x] = xcc;
     }
 #endif
     const int E = L.E;
@@ -2710,80 +2712,85 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
     const int o0 = offs ? L.off[e] : 0;
     const int n = offs ? L.off[e + 1] - o0 : L.N;
 
-    // ---- prologue: the pair's candidate (speculative setup) or standard slots
+    // the point loads the windows need, issued first: they overlap the
+    // candidate chain below (own point, predecessor, first and last)
+    const bool own = tid < n;
+    const int m = n;
+    const int pl = own ? tid : 0;
+    const double* xe = L.x + o0;
+    double xw_own = 0.0, xw_prv = 0.0, xw_0 = 0.0, xw_1 = 0.0;
+    double ww_own = 0.0, ww_prv = 0.0, ww_0 = 0.0, ww_1 = 0.0;
+    if (n > 0) {
+        xw_own = xe[pl];
+        xw_prv = xe[pl > 0 ? pl - 1 : 0];
+        xw_0 = xe[0];
+        xw_1 = xe[n - 1];
+    }
+    if (L.w && n > 0) {
+        const double* we = L.w + o0;
+        ww_own = we[pl];
+        ww_prv = we[pl > 0 ? pl - 1 : 0];
+        ww_0 = we[0];
+        ww_1 = we[n - 1];
+    }
+    // ---- prologue: the pair's candidate (speculative setup) or standard
+    // slots.  Only what the phase barrier B0 waits for is done here (the
+    // barrier waits for every wave's outstanding memory operations): both
+    // candidates' per-pair words are loaded alongside the selection chain
+    // (jk -> accflag), and the copies into the standard slots, the snapshot
+    // and the acceptance's prefetch follow B0 (wave 7's first task)
     const double* G;
-    int st0, bst;
-    double lpr = 0.0, zf = 0.0;
-    const double* qsrc = L.qprop ? L.qprop + size_t(w) * L.ndim : nullptr;
+    int st0, bst, cand = 0;
+    double lpr = 0.0, zf = 0.0, rpr, phi0;
     if (X.jk) {
-        const int cand = __builtin_amdgcn_readfirstlane(X.accflag[X.jk[w]]);
-        const size_t cp = size_t(cand) * npairs + pair, cw = size_t(cand) * nwk + w;
-        G = X.geoC + cp * LFG_NGEO;
-        st0 = X.statusC[cp];
-        bst = X.bstatusC[cp];
-        lpr = X.priorC[cw];
-        zf = X.zfC[cw];
-        qsrc = X.qC + cw * X.ndim;
-        // the selected candidate into the standard slots (API readers, k_combine_walkers)
-        double* Gd = const_cast<double*>(L.geo) + size_t(pair) * LFG_NGEO;
-        if (tid < LFG_NGEO) Gd[tid] = G[tid];
-        if (tid == LFG_NGEO) X.bstatus[pair] = bst;
-        if (e == 0) {
-            for (int d = tid; d < X.ndim; d += nt) X.q[size_t(w) * X.ndim + d] = qsrc[d];
-            if (tid == LFG_NGEO + 1) X.prior[w] = lpr;
-            if (tid == LFG_NGEO + 2) X.zf[w] = zf;
-        }
+        const size_t c0 = size_t(pair), c1 = size_t(npairs) + pair;
+        const int sa0 = X.statusC[c0], sa1 = X.statusC[c1], sb0 = X.bstatusC[c0], sb1 = X.bstatusC[c1];
+        const double lp0 = X.priorC[w], lp1 = X.priorC[size_t(nwk) + w];
+        const double* G0 = X.geoC + c0 * LFG_NGEO;
+        const double* G1 = X.geoC + c1 * LFG_NGEO;
+        const double rp0 = G0[G_RPRIOR] + G0[G_RPRIOR_BS], rp1 = G1[G_RPRIOR] + G1[G_RPRIOR_BS];
+        const double ph0 = G0[G_PHI0], ph1 = G1[G_PHI0];
+        cand = __builtin_amdgcn_readfirstlane(X.accflag[X.jk[w]]);
+        PAIR_STAMP(10, tid == 0 && cand >= 0);
+        G = cand ? G1 : G0;
+        st0 = cand ? sa1 : sa0;
+        bst = cand ? sb1 : sb0;
+        lpr = cand ? lp1 : lp0;
+        rpr = cand ? rp1 : rp0;
+        phi0 = cand ? ph1 : ph0;
     } else {
         G = L.geo + size_t(pair) * LFG_NGEO;
         st0 = L.status[pair];
         bst = L.bstatus[pair];
         if (L.prior) lpr = L.prior[w];
-        if (L.zfac) zf = L.zfac[w];
+        rpr = G[G_RPRIOR] + G[G_RPRIOR_BS];
+        phi0 = G[G_PHI0];
     }
     // the record through the constant address space: its reads are scalar
     // loads into SGPRs, as in k_elements (the launch writes no record it
     // reads: the standard slot it copies into is not G when X.jk is set)
     const CGeo Gc = (CGeo)(G);
     const int stp = (st0 != ST_OK) ? st0 : bst;  // MODEL_SPEC 6 order: setup failures first
-    if (tid == LFG_NGEO + 3) const_cast<int*>(L.status)[pair] = stp;
-    const bool prej = L.prior && prior_rejects(lpr, G);
+    const bool prej = L.prior && !(lpr + rpr > -INFINITY);  // prior_rejects
     const int st = (stp == ST_OK && prej) ? -1 : stp;  // -1: prior-rejected, straight to the -inf finish
-    // the other half's rows for the next launch's speculative lanes
-    if (A.snap_dst && e == 0)
-        for (int d = tid; d < L.ndim; d += nt) A.snap_dst[size_t(w) * L.ndim + d] = A.snap_src[size_t(w) * L.ndim + d];
     const bool acc1 = L.pos && E == 1;
-    if (acc1 && tid < L.ndim && tid < ACC_LDS) sq[tid] = qsrc[tid];
-    if (acc1 && tid == nt - 1) {
-        const uint4 r = draw(L.seed, L.step, L.half, 1, pair);
-        sacc1[0] = log(u53(r.x, r.y));
-        sacc1[1] = zf;
-        sacc1[2] = L.lnp_ens[L.half * npairs + pair];
-    }
     // this thread's point (one tile: m = n points): window and phase into LDS,
     // its sortedness against the predecessor, and the cells it fills of the
     // two phase indices (windows' lo, point phases), formed from its own and
     // its predecessor's windows, so that no barrier separates them
-    const bool own = tid < n;
-    const int m = n;
     int fl = 0;
     if (own) {
-        const double phi0 = Gc[G_PHI0];
         double ph, lo, hi, hw;
-        pair_window(L, o0, tid, phi0, ph, lo, hi, hw);
+        pair_window(xw_own, ww_own, phi0, ph, lo, hi, hw);
+        PAIR_STAMP(11, tid == 0 && ph != 12345.0);
         TA.lo[tid] = lo;
         TA.hi[tid] = hi;
         TA.iw[tid] = 1.0 / (2.0 * hw);
         sph[tid] = ph;
-        sy[tid] = L.y[o0 + tid];
-        if (!GP) sye[tid] = L.ye[o0 + tid];
-        if (GP) {  // the Kalman filter's transition factor of this point (k_gp_like)
-            const double xp = L.x[o0 + tid], dx = xp - (tid ? L.x[o0 + tid - 1] : xp);
-            L.gpx[size_t(pair) * L.N + tid] = exp(-(Gc[G_GP_LAM] * dx));
-        }
         double php = 0.0, lop = 0.0, hip = 0.0, hwp, ph0, lo0, hi0, hw0, ph1, lo1, hi1, hw1;
-        if (tid) pair_window(L, o0, tid - 1, phi0, php, lop, hip, hwp);
-        pair_window(L, o0, 0, phi0, ph0, lo0, hi0, hw0);
-        pair_window(L, o0, m - 1, phi0, ph1, lo1, hi1, hw1);
+        if (tid) pair_window(xw_prv, ww_prv, phi0, php, lop, hip, hwp);
+        pair_window(xw_0, ww_0, phi0, ph0, lo0, hi0, hw0);
+        pair_window(xw_1, ww_1, phi0, ph1, lo1, hi1, hw1);
         fl = (hw >= 0.0) ? 0 : 4;  // negative or NaN widths: point-major
         if (tid && (lo < lop || hi < hip || ph < php)) fl = 4;
         pair_cells(TA.cell, tid, m, lop, lo, lo0, lo1);
@@ -2801,8 +2808,9 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
         SU.s.X[0][nt] = 0ull;
         SU.s.X[1][nt] = 0ull;
         stot[0] = stot[1] = 0ull;
-        sjob = 8;
+        sjob = (X.nspec > 0 && pair < 2 * A.nbc) ? 8 : 9;
     }
+    PAIR_STAMP(19, tid == 0);
     // the disc ring weights (MODEL_SPEC 5.2): wave 7's lanes 0..NDISC_R
     if (st == ST_OK && wv == 7 && lane <= NDISC_R) ring_weight_lane(lane, Gc, swt);
     __syncthreads();  // B0: windows, cells, flags, zeroed sums, ring weights, sjob
@@ -2810,14 +2818,60 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
 
     bool dir = false;
     for (int k = 0; k < nw; ++k) dir = dir || sflagw[k] != 0;
+    // this thread's data point (read after the phase barrier), the GP
+    // filter's transition factor of the point (k_gp_like)
+    if (own) {
+        sy[tid] = L.y[o0 + tid];
+        if (!GP) sye[tid] = L.ye[o0 + tid];
+        if (GP) {
+            const double xp = L.x[o0 + tid], dx = xp - (tid ? L.x[o0 + tid - 1] : xp);
+            L.gpx[size_t(pair) * L.N + tid] = exp(-(Gc[G_GP_LAM] * dx));
+        }
+    }
+    if (wv == 7) {
+        // housekeeping off the prologue's critical path: the selected candidate
+        // into the standard slots (API readers, k_combine_walkers, k_gp_like),
+        // the pair status, the snapshot of the other half's rows for the next
+        // launch's speculative lanes, the fused acceptance's prefetch
+        const int l = lane;
+        if (X.jk) {
+            const size_t cw = size_t(cand) * nwk + w;
+            double* Gd = const_cast<double*>(L.geo) + size_t(pair) * LFG_NGEO;
+            if (l < LFG_NGEO) Gd[l] = G[l];
+            if (l == 48) X.bstatus[pair] = bst;
+            if (e == 0) {
+                const double* qc = X.qC + cw * X.ndim;
+                for (int d = l; d < X.ndim; d += 64) X.q[size_t(w) * X.ndim + d] = qc[d];
+                if (l == 49) X.prior[w] = lpr;
+                if (l == 50) X.zf[w] = X.zfC[cw];
+            }
+        }
+        if (l == 51) const_cast<int*>(L.status)[pair] = stp;
+        if (A.snap_dst && e == 0)
+            for (int d = l; d < L.ndim; d += 64) A.snap_dst[size_t(w) * L.ndim + d] = A.snap_src[size_t(w) * L.ndim + d];
+        if (acc1) {
+            const double* qsrc = X.jk ? X.qC + (size_t(cand) * nwk + w) * X.ndim : L.qprop + size_t(w) * L.ndim;
+            for (int d = l; d < L.ndim && d < ACC_LDS; d += 64) sq[d] = qsrc[d];
+            if (l == 63) {
+                const uint4 r = draw(L.seed, L.step, L.half, 1, pair);
+                sacc1[0] = log(u53(r.x, r.y));
+                sacc1[1] = X.jk ? X.zfC[size_t(cand) * nwk + w] : L.zfac[w];
+                sacc1[2] = L.lnp_ens[L.half * npairs + pair];
+            }
+        }
+    }
     // ---- element phase: 16 jobs.  Job 0: this block's speculative setup
     // lanes of the next half; jobs 1..15: the 15 item chunks, longest first
     // (kJobChunk).  Wave w takes job w, then grabs the next free job from
     // sjob, at most twice (8 waves x 3 >= 16): the waves finish together
     // whatever the pair's Newton counts (a static two-chunk split waited
     // ~8 us at the phase barrier on its slowest wave)
-    if (wv == 0) {
-        if (lane < A.spl && X.nspec > 0) {
+    // the speculative lanes fill whole waves: wave 0 of the first 2 nbc blocks
+    // (a few lanes in every block's wave 0 cost each of them the lanes' whole
+    // instruction stream: SIMD issue slots of ~10x the work)
+    const bool specblk = X.nspec > 0 && pair < 2 * A.nbc;
+    if (wv == 0 && specblk) {
+        if (lane < A.spl) {
             // candidate uniform per block: X.S[c] stays in scalar registers
             const int c = pair < A.nbc ? 0 : 1;
             const int t = (pair - c * A.nbc) * A.spl + lane;
@@ -2890,7 +2944,9 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
         };
         // straight-line calls, not a loop: a loop's invariant constants (the
         // transcendental polynomials) were hoisted and spilled to scratch
-        if (wv > 0) chunk(wv);
+        // (a block without speculative lanes starts wave w on job w + 1)
+        if (!specblk) chunk(wv + 1);
+        else if (wv > 0) chunk(wv);
         int j = grab();
         if (j < 16) chunk(j);
         j = grab();
@@ -3730,7 +3786,7 @@ int lfg_lnlike(const double* pars, int W, int P, const double* x, const double* 
                nsub, nullptr, nullptr, lnlike, W, nullptr, nullptr, nullptr, false, nullptr,
                nullptr, nullptr, nullptr, 0, 0, 0ull, 0ull, nullptr};
     L.bstatus = ws.bstatus;
-    if (pair) hipLaunchKernelGGL(k_pair<false>, dim3(W), dim3(LIKE_THREADS), 0, st, PairArgs{L, ElemSpec{}, nullptr, nullptr, 0, 0});
+    if (pair) hipLaunchKernelGGL(k_pair<false>, dim3(W), dim3(LIKE_THREADS), 0, st, PairArgs{L, ElemSpec{}, nullptr, nullptr, 64, 0});
     else if (nsub > 1) hipLaunchKernelGGL((k_lnlike<1, true>), dim3(W), dim3(LIKE_THREADS), 0, st, L);
     else hipLaunchKernelGGL((k_lnlike<1, false>), dim3(W), dim3(LIKE_THREADS), 0, st, L);
     if ((rc = launch_ok())) return rc;
@@ -3837,12 +3893,9 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
     // k_pair: the element solve and the likelihood of a pair in one
     // workgroup (one-tile eclipses, S = 1, no GP); the speculative lanes must
     // fit wave 7's spare lanes
-    int spl = 0, nbc = 0;
-    if (X.nspec > 0 && npairs >= 2) {
-        nbc = (npairs + 1) / 2;
-        spl = (X.nspec + (npairs - nbc) - 1) / (npairs - nbc);
-    }
-    const bool pair_path = pair_ok(T->gp, T->nsub, T->max_n, T->ndim) && (X.nspec == 0 || (npairs >= 2 && spl <= 64));
+    // the speculative lanes: whole waves (wave 0 of blocks [0, 2 nbc)), nbc per candidate
+    const int spl = 64, nbc = (X.nspec + 63) / 64;
+    const bool pair_path = pair_ok(T->gp, T->nsub, T->max_n, T->ndim) && (X.nspec == 0 || 2 * nbc <= npairs);
     int rc = run_front(S, ws, st, ev, !pair_path, &X, !(sp && sp->in));
     if (rc) return rc;
     double* lle = lnlike_e ? lnlike_e : ws.lle;

@@ -45,7 +45,7 @@ t0 = t[0]
 span = (t[15].max() - t0.min()) / 100.0
 print("blocks %d, launch span %.2f us (first start -> last finish)" % (nb, span))
 print("block start spread: %s us" % np.percentile((t0 - t0.min()) / 100.0, [0, 50, 90, 100]).round(2))
-rows = [("B0 (prologue)", 16)] + [("wave %d elements" % k, 1 + k) for k in range(8)] + [
+rows = [("candidate known", 10), ("own window (phi0)", 11), ("prologue before B0", 19), ("B0 (prologue)", 16)] + [("wave %d elements" % k, 1 + k) for k in range(8)] + [
     ("B1 (phase barrier)", 9), ("B2 (items, norms)", 10), ("B3 (cells)", 11), ("scan", 12),
     ("chi^2", 13), ("finish", 15)]
 for name, k in rows:
@@ -74,3 +74,5 @@ if L.lfg_debug_pair_waves(ctypes.c_void_p(wv.ctypes.data)) == 0 and wv.any():
         d = (wv[k] - b3[None, :]) / 100.0
         print("  %-20s earliest %6.2f  latest %6.2f" % (nm, np.median(d.min(0)), np.median(d.max(0))))
     print("  %-20s %6.2f" % ("scan done (thread 0)", np.median((t[12] - b3) / 100.0)))
+if len(sys.argv) > 2:  # raw stamps for offline analysis
+    np.save(sys.argv[2], t)
