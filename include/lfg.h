@@ -391,10 +391,17 @@ int lfg_event_elapsed_ms(void* start, void* stop, float* ms);
 const char* lfg_version(void);
 
 /* The kernels a tree's ln_prob runs on: 1 = k_pair (element solve and
- * likelihood of a walker-eclipse pair in one workgroup: one-tile eclipses,
- * nsub = 1, no GP, LFG_PAIR=1 in the environment), 0 = k_elements +
- * k_lnlike; LFG_E_ARGS for a null or empty tree.  For measurement tools. */
+ * likelihood of a walker-eclipse pair in one workgroup: eclipses of at most
+ * 512 points, nsub = 1), 0 = k_elements + k_lnlike (every other tree);
+ * LFG_E_ARGS for a null or empty tree.  For measurement tools. */
 int lfg_layout(const lfg_tree* tree);
+
+/* Process-wide layout switch (tests, A/B measurement): 0 = k_elements +
+ * k_lnlike for every tree, 1 = k_pair where lfg_layout allows it (the
+ * default), -1 = back to the environment's choice (LFG_PAIR=0 selects 0).
+ * Returns the previous setting (0 or 1), LFG_E_ARGS for another value.  Not
+ * synchronised with launches in flight on other host threads. */
+int lfg_set_layout(int mode);
 
 #ifdef __cplusplus
 }

@@ -74,7 +74,7 @@ EXPORTS = ("lfg_workspace_size", "lfg_workspace_size_tree", "lfg_flux", "lfg_lnl
            "lfg_elements", "lfg_roche", "lfg_stretch_propose", "lfg_stretch_accept",
            "lfg_stretch_propose_dev", "lfg_stretch_accept_dev", "lfg_event_create", "lfg_event_destroy",
            "lfg_event_elapsed_ms", "lfg_wdphases", "lfg_gp_lnlike", "lfg_component_workspace_size",
-           "lfg_component", "lfg_version", "lfg_layout")
+           "lfg_component", "lfg_version", "lfg_layout", "lfg_set_layout")
 
 
 FLAGS = ["--offload-arch=%s" % ARCH, "-O3", "-std=c++17", "-fPIC", "-shared"]
@@ -228,6 +228,9 @@ def lib():
         L.lfg_version.argtypes = []
         L.lfg_layout.restype = ip
         L.lfg_layout.argtypes = [ctypes.POINTER(LfgTree)]
+        if hasattr(L, "lfg_set_layout"):  # (older experiment builds lack it)
+            L.lfg_set_layout.restype = ip
+            L.lfg_set_layout.argtypes = [ip]
         _lib = L
         return L
 

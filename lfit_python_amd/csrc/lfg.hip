@@ -15,6 +15,7 @@
 // Replaces, per walker, mcmcfit.ln_prob (mcmcfit.py:37-41) -> Node.ln_prob
 // (model.py:476-498) -> lfit.CV.calcFlux (CVModel.py:138).
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -657,6 +658,7 @@ __device__ __forceinline__ void element_item_to(int v, GPtr G, Sink& K);
 // the sink of k_elements (and k_pair's point-major fallback): the tables
 struct MemSink {
     const ElemOut& O;
+    __device__ __forceinline__ void mark() {}
     __device__ __forceinline__ void wd_disc(int u, double a, double b) { O.abw[uslot(u)] = make_double2(a, b); }
     __device__ __forceinline__ void spot(int j, double a, double b, double w)
     {
@@ -748,7 +750,9 @@ __device__ __forceinline__ void element_item_to(int v, GPtr G, Sink& K)
         // rho cos(alpha) = vx, rho sin(alpha) = vy  ->  |theta + alpha| < acos(kappa)
         const double srho = s * sqrt(vx * vx + vy * vy);
         const double kap = (srho > 0.0) ? -c * vz / srho : (c * vz > 0.0 ? -2.0 : 2.0);
-        K.donor(uu, vx, vy, vz, -atan2(vy, vx) * (1.0 / TWO_PI), acos(fmin(fmax(kap, -1.0), 1.0)) * (1.0 / TWO_PI));
+        const double cen = -atan2(vy, vx) * (1.0 / TWO_PI), hw = acos(fmin(fmax(kap, -1.0), 1.0)) * (1.0 / TWO_PI);
+        K.mark();
+        K.donor(uu, vx, vy, vz, cen, hw);
         return;
     }
 
@@ -812,6 +816,7 @@ __device__ __forceinline__ void element_item_to(int v, GPtr G, Sink& K)
 #else
     element_interval_fast(R, Px, Py, Pz, s, c, G[G_RCAL], G[G_REFF], a, b);
 #endif
+    K.mark();
     if (u >= U_MAIN) K.spot(u - U_MAIN, a, b, bs_weight(u - U_MAIN, G));
     else K.wd_disc(u, a, b);
 }
@@ -839,7 +844,6 @@ __global__ __launch_bounds__(ELEM_BLOCK) __attribute__((amdgpu_waves_per_eu(ELEM
 #ifdef LFG_PROFILE_ELEM
     const unsigned long long pt0 = __builtin_amdgcn_s_memrealtime();
 #endif
-#ifndef LFG_NO_SPEC_LANES  // (experiment: the element path alone, with LFG_SPEC=0)
     if (int(blockIdx.x) < X.nspecblk) {  // speculative setup lanes of the next half
         // candidate c's lanes fill blocks [c * nb, (c + 1) * nb): c is uniform
         // in a block, so X.S[c] is selected in scalar registers (a lane-varying
@@ -853,7 +857,6 @@ __global__ __launch_bounds__(ELEM_BLOCK) __attribute__((amdgpu_waves_per_eu(ELEM
 #endif
         return;
     }
-#endif
     const unsigned bid = blockIdx.x - unsigned(X.nspecblk);
     // blocks cover the NUNIQ unique items of every pair in chunks of
     // blockDim.x (the spot items fill the last chunk); block b takes pair
@@ -1296,6 +1299,71 @@ __device__ __forceinline__ void apply_runs(const Runs& R, double a, double b, do
     }
 }
 
+// apply_runs for NI intervals of one lane with every LDS read issued before
+// the first atomic: a read waits for all the lane's earlier LDS operations
+// (one in-order counter), so reads between atomics waited for each atomic's
+// round trip.  The first K windows of each partial run are read up front
+// (windows that tile the phase axis give one at each end); longer partial
+// runs finish one window at a time after the atomics.  The same entries as
+// apply_runs: identical integer sums.
+template <int NI>
+__device__ __forceinline__ void apply_runs_batched(const Runs (&R)[NI], const double (&a)[NI], const double (&b)[NI],
+                                                   double wn, const PhaseIndex& X, const double* __restrict__ hi,
+                                                   const double* __restrict__ iw, unsigned long long* acc)
+{
+    constexpr int K = 2;
+    const int last = X.m - 1;
+    int ps[NI][2], pn[NI][2];
+    long long q[NI][2][K];
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+        const bool whole = R[k].P2 < R[k].P3;
+        const int e0 = whole ? R[k].P2 : R[k].P4, s1 = whole ? R[k].P3 : R[k].P4;
+        ps[k][0] = R[k].P1;
+        pn[k][0] = e0 - R[k].P1;
+        ps[k][1] = s1;
+        pn[k][1] = R[k].P4 - s1;
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                const int p = min(ps[k][e] + i, last);
+                const double ov = fmin(b[k], hi[p]) - fmax(a[k], X.v[p]);
+                q[k][e][i] = (i < pn[k][e] && ov > 0.0) ? to_fx(wn * ov * iw[p]) : 0;
+            }
+    }
+    const long long qw = to_fx(wn);
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+        if (R[k].P2 < R[k].P3) {
+            fx_add(acc, R[k].P2, qw);
+            if (R[k].P3 < X.m) fx_add(acc, R[k].P3, -qw);
+        }
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                const int p = ps[k][e] + i;
+                if (q[k][e][i] != 0) {
+                    fx_add(acc, p, q[k][e][i]);
+                    if (p + 1 < X.m) fx_add(acc, p + 1, -q[k][e][i]);
+                }
+            }
+    }
+#pragma unroll
+    for (int k = 0; k < NI; ++k)
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+            for (int p = ps[k][e] + K; p < ps[k][e] + pn[k][e]; ++p) {
+                const double ov = fmin(b[k], hi[p]) - fmax(a[k], X.v[p]);
+                if (ov > 0.0) {
+                    const long long qq = to_fx(wn * ov * iw[p]);
+                    fx_add(acc, p, qq);
+                    if (p + 1 < X.m) fx_add(acc, p + 1, -qq);
+                }
+            }
+}
+
 // ring of unique WD/disc item u: WD ring r holds 2 r^2 <= u < 2 (r + 1)^2,
 // disc rings follow (NDISC_AZ / 2 items each)
 __device__ __forceinline__ int uring(int u)
@@ -1321,6 +1389,15 @@ __device__ __forceinline__ long long wave_scan_incl(long long v, int lane)
     v += dpp64<0x142, 0xa>(v);
     v += dpp64<0x143, 0xc>(v);
     return v;
+}
+
+// the wave's total of v (all 64 lanes active), in every lane
+__device__ __forceinline__ long long wave_total(long long v)
+{
+    v = wave_scan_incl(v, 0);
+    const int lo = __builtin_amdgcn_readlane(static_cast<int>(v), 63);
+    const int hi = __builtin_amdgcn_readlane(static_cast<int>(v >> 32), 63);
+    return (static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo);
 }
 
 // inclusive prefix of NA difference arrays at index tid (one entry per thread)
@@ -2491,6 +2568,12 @@ struct PairArgs {
     double* snap_dst;
     int spl;                   // speculative lanes per block that has them (64: wave 0's job 0)
     int nbc;                   // blocks [0, nbc) carry candidate 0's lanes, [nbc, 2 nbc) candidate 1's
+    // with X.jk: walker w's partner j in the other half, drawn here as the
+    // speculative lanes drew it (make_prop: draw(seed, step, half, 0, lo + w),
+    // j = umulhi(r.z, ns)) instead of read back from X.jk, one dependent
+    // global load less before the candidate is known
+    unsigned long long jseed, jstep;
+    int jhalf, jlo, jns;
 };
 
 // the chunks of k_pair's element jobs 1..15, longest first (spot, outer
@@ -2509,6 +2592,7 @@ __device__ unsigned long long g_pair_t[20][4096];
         if ((cond) && blockIdx.x < 4096) g_pair_t[slot][blockIdx.x] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 __device__ unsigned long long g_pair_w[4][8][4096];
+__device__ unsigned long long g_pair_j[3][16][4096];  // per chunk: job start, sink entry, end
 #define PAIR_WSTAMP(k)                                                                                  \
     do {                                                                                                \
         if (lane == 0 && blockIdx.x < 4096) g_pair_w[k][wv][blockIdx.x] = __builtin_amdgcn_s_memrealtime(); \
@@ -2537,7 +2621,18 @@ struct PairSink {
     double2* sab;
     double* sbw;
     double* sdq;
+    unsigned long long* mk;  // diagnostic builds: where mark() stamps the sink's entry
+    // lane-local sums flushed once per wave (flush): the spot weight and donor
+    // quadrature totals, and the donor arcs that open at the tile's first point
+    // (all 64 lanes of a wave added these to the same LDS word: 64-way conflicts)
+    long long tspot, tdon, bx, by, bz;
 
+    __device__ __forceinline__ void mark()
+    {
+#ifdef LFG_PROFILE_PAIR
+        if (mk) *mk = __builtin_amdgcn_s_memrealtime();
+#endif
+    }
     __device__ __forceinline__ void wd_disc(int u, double a, double b)
     {
         if (dir) {
@@ -2552,15 +2647,20 @@ struct PairSink {
         count_lt_multi<4>(XW, q, J);
         count_le_back_multi<4>(hi, q, J, Jb);
         unsigned long long* A = ((lane & 1) ? acc2 : acc)[(u < U_WD) ? 0 : 1];
-        apply_runs(Runs{Jb[0], J[0], Jb[1], J[1]}, a, b, wn, XW, hi, iw, A);
-        apply_runs(Runs{Jb[2], J[2], Jb[3], J[3]}, -b, -a, wn, XW, hi, iw, A);
+        const Runs RR[2] = {Runs{Jb[0], J[0], Jb[1], J[1]}, Runs{Jb[2], J[2], Jb[3], J[3]}};
+        const double aa[2] = {a, -b}, bb[2] = {b, -a};
+        apply_runs_batched<2>(RR, aa, bb, wn, XW, hi, iw, A);
     }
     __device__ __forceinline__ void spot(int j, double a, double b, double w)
     {
         sab[j] = make_double2(a, b);
         sbw[j] = w;
-        atomicAdd(tot, static_cast<unsigned long long>(to_fx(w * PAIR_SPOT_S)));
-        if (!dir && a < b) apply_runs(element_runs(a, b, XW, hi), a, b, w * PAIR_SPOT_S, XW, hi, iw, acc[2]);
+        tspot += to_fx(w * PAIR_SPOT_S);
+        if (!dir && a < b) {
+            const Runs RR[1] = {element_runs(a, b, XW, hi)};
+            const double aa[1] = {a}, bb[1] = {b};
+            apply_runs_batched<1>(RR, aa, bb, w * PAIR_SPOT_S, XW, hi, iw, acc[2]);
+        }
     }
     __device__ __forceinline__ void donor(int uu, double vx0, double vy0, double vz0, double cen0, double hw0)
     {
@@ -2571,14 +2671,16 @@ struct PairSink {
         D[3] = cen0;
         D[4] = hw0;
         long long tn = 0;
-#pragma unroll 1
+        // the arcs' point ranges first (LDS reads), then their entries
+        int PA[4][2], QA[4][2];
+#pragma unroll
         for (int mr = 0; mr < 4; ++mr) {  // the tile's mirror images, as k_lnlike's donor lanes form them
-            const double vx = vx0, vy = (mr & 1) ? -vy0 : vy0, vz = (mr & 2) ? -vz0 : vz0;
+            const double vy = (mr & 1) ? -vy0 : vy0, vz = (mr & 2) ? -vz0 : vz0;
             const double cen = (mr & 1) ? -cen0 : cen0;
             const double hw = (mr & 2) ? 0.5 - hw0 : hw0;
             tn += to_fx(fmax(-s * vy + c * vz, 0.0) * PAIR_DON_S);
+            PA[mr][0] = QA[mr][0] = PA[mr][1] = QA[mr][1] = 0;
             if (dir || !(hw > 0.0)) continue;
-            const long long qx = to_fx(vx * PAIR_DON_S), qy = to_fx(vy * PAIR_DON_S), qz = to_fx(vz * PAIR_DON_S);
             // visible for phases in (cen - hw, cen + hw) mod 1
             double x1 = -INFINITY, x2 = INFINITY, y1 = 0.0, y2 = 0.0;
             bool two = false;
@@ -2588,12 +2690,30 @@ struct PairSink {
                 else if (hi2 > 0.5) { x1 = lo; y1 = -INFINITY; y2 = hi2 - 1.0; two = true; }
                 else { x1 = lo; x2 = hi2; }
             }
-            for (int i = 0; i < (two ? 2 : 1); ++i) {
-                const int P = count_below<true>(XP, i ? y1 : x1), Q = count_below<false>(XP, i ? y2 : x2);
+            PA[mr][0] = count_below<true>(XP, x1);
+            QA[mr][0] = count_below<false>(XP, x2);
+            if (two) {
+                PA[mr][1] = count_below<true>(XP, y1);
+                QA[mr][1] = count_below<false>(XP, y2);
+            }
+        }
+        const long long qx = to_fx(vx0 * PAIR_DON_S), qy0 = to_fx(vy0 * PAIR_DON_S), qz0 = to_fx(vz0 * PAIR_DON_S);
+#pragma unroll
+        for (int mr = 0; mr < 4; ++mr) {
+            const long long qy = (mr & 1) ? -qy0 : qy0, qz = (mr & 2) ? -qz0 : qz0;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int P = PA[mr][i], Q = QA[mr][i];
                 if (P < Q) {
-                    fx_add(acc[3], P, qx);
-                    fx_add(acc[4], P, qy);
-                    fx_add(acc[5], P, qz);
+                    if (P == 0) {
+                        bx += qx;
+                        by += qy;
+                        bz += qz;
+                    } else {
+                        fx_add(acc[3], P, qx);
+                        fx_add(acc[4], P, qy);
+                        fx_add(acc[5], P, qz);
+                    }
                     if (Q < XP.m) {
                         fx_add(acc[3], Q, -qx);
                         fx_add(acc[4], Q, -qy);
@@ -2602,7 +2722,21 @@ struct PairSink {
                 }
             }
         }
-        atomicAdd(tot + 1, static_cast<unsigned long long>(tn));
+        tdon += tn;
+    }
+    // the lane-local sums into LDS: every lane of the wave calls it, after its
+    // last item (the integer sums are exact in any order)
+    __device__ __forceinline__ void flush()
+    {
+        const long long t0 = wave_total(tspot), t1 = wave_total(tdon);
+        const long long x = wave_total(bx), y = wave_total(by), z = wave_total(bz);
+        if (lane == 0) {
+            if (t0) atomicAdd(tot, static_cast<unsigned long long>(t0));
+            if (t1) atomicAdd(tot + 1, static_cast<unsigned long long>(t1));
+            if (x) fx_add(acc[3], 0, x);
+            if (y) fx_add(acc[4], 0, y);
+            if (z) fx_add(acc[5], 0, z);
+        }
     }
 };
 
@@ -2750,7 +2884,8 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
         const double* G1 = X.geoC + c1 * LFG_NGEO;
         const double rp0 = G0[G_RPRIOR] + G0[G_RPRIOR_BS], rp1 = G1[G_RPRIOR] + G1[G_RPRIOR_BS];
         const double ph0 = G0[G_PHI0], ph1 = G1[G_PHI0];
-        cand = __builtin_amdgcn_readfirstlane(X.accflag[X.jk[w]]);
+        const int jw = int(__umulhi(draw(A.jseed, A.jstep, A.jhalf, 0, A.jlo + w).z, unsigned(A.jns)));
+        cand = __builtin_amdgcn_readfirstlane(X.accflag[__builtin_amdgcn_readfirstlane(jw)]);
         PAIR_STAMP(10, tid == 0 && cand >= 0);
         G = cand ? G1 : G0;
         st0 = cand ? sa1 : sa0;
@@ -2929,13 +3064,24 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
         PairSink K{dir, lane, phase_index(TA.lo, TA.cell, m), phase_index(sph, SU.s.scp, m), TA.hi, TA.iw, sacc,
                    SU.s.X, stot, swt, ul, 1.0 / (TWO_PI * ((1.0 - ul) * 0.5 + ul / 3.0)), Gc[G_S], Gc[G_C],
                    SU.ab, sab, sbw, sdq};
-        // chunk c: items v = 64 c + lane (c < 13: WD, disc, spot; 13, 14: donor)
+        // chunk c: items v = 64 c + lane of one region each (c < 11: WD and
+        // disc; 11, 12: spot; 13, 14: donor), so that no wave runs two
+        // regions' code one after the other
         auto chunk = [&](int j) {
             const int c = kJobChunk[j - 1];
-            int v = -1;
-            if (c < 13) v = (c * 64 + lane < U_WD + U_DISC + U_BS) ? c * 64 + lane : -1;
-            else if (c == 13 || lane < U_DON - 64) v = U_WD + U_DISC + U_BS + (c - 13) * 64 + lane;
+            constexpr int V_BS = U_WD + U_DISC, V_DON = V_BS + U_BS;
+            const int r0 = c < 11 ? 0 : (c < 13 ? V_BS : V_DON), c0 = c < 11 ? 0 : (c < 13 ? 11 : 13);
+            const int r1 = c < 11 ? V_BS : (c < 13 ? V_DON : NUNIQ);
+            const int v = r0 + (c - c0) * 64 + lane < r1 ? r0 + (c - c0) * 64 + lane : -1;
+#ifdef LFG_PROFILE_PAIR
+            const bool rec = lane == 0 && blockIdx.x < 4096;
+            if (rec) g_pair_j[0][c][blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+            K.mk = rec ? &g_pair_j[1][c][blockIdx.x] : nullptr;
+#endif
             if (v >= 0) element_item_to(v, Gc, K);
+#ifdef LFG_PROFILE_PAIR
+            if (rec) g_pair_j[2][c][blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+#endif
         };
         auto grab = [&]() {
             int j = 0;
@@ -2951,9 +3097,10 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
         if (j < 16) chunk(j);
         j = grab();
         if (j < 16) chunk(j);
+        K.flush();
     }
-    static_assert(13 * 64 >= U_WD + U_DISC + U_BS && 12 * 64 < U_WD + U_DISC + U_BS, "13 chunks of WD/disc/spot");
-    static_assert(U_DON > 64 && U_DON <= 128, "two donor chunks");
+    static_assert(11 * 64 >= U_WD + U_DISC && 10 * 64 < U_WD + U_DISC, "11 chunks of WD/disc");
+    static_assert(U_BS > 64 && U_BS <= 128 && U_DON > 64 && U_DON <= 128, "two spot and two donor chunks");
     PAIR_STAMP(1 + wv, lane == 0);
     __syncthreads();  // B1: the sums (or the tables)
     PAIR_STAMP(9, tid == 0);
@@ -3563,11 +3710,17 @@ __global__ void k_accept(double* __restrict__ pos, double* __restrict__ lnp, int
 // k_accept with the proposal re-formed from the same draws (k_propose's
 // arithmetic): the sharded half-step keeps only its own shard of q, and the
 // partner half is unchanged until this half is accepted
-__global__ void k_accept_regen(double* __restrict__ pos, double* __restrict__ lnp, int W, int ndim, int half,
+// one wave per walker of the half (four per 256-lane block): the draws and
+// the decision are wave-uniform (scalar ALU and scalar loads), and an
+// accepted walker's row moves with one load round over the lanes (lane d:
+// dimension d) instead of one lane's serial chunks of 8
+constexpr int REGEN_WAVES = 4;
+__global__ __launch_bounds__(64 * REGEN_WAVES) void k_accept_regen(double* __restrict__ pos, double* __restrict__ lnp, int W, int ndim, int half,
                                double a, const double* __restrict__ lnp_new, unsigned long long seed,
                                unsigned long long step, int* __restrict__ naccept, int* __restrict__ accflag)
 {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * REGEN_WAVES + int(threadIdx.x >> 6));
+    const int lane = threadIdx.x & 63;
     const int ns = W / 2;
     if (i >= ns) return;
     const int w = half * ns + i;
@@ -3577,26 +3730,18 @@ __global__ void k_accept_regen(double* __restrict__ pos, double* __restrict__ ln
     const uint4 r = draw(seed, step, half, 1, i);
     const double lu = log(u53(r.x, r.y));
     const double diff = (ndim - 1.0) * log(z) + lnp_new[i] - lnp[w];
-    if (lu < diff) {
+    const bool acc = lu < diff;
+    if (acc) {
         const int j = int(__umulhi(r0.z, unsigned(ns)));
         double* p = pos + size_t(w) * ndim;
         const double* cj = pos + size_t((1 - half) * ns + j) * ndim;
-        // p and cj are rows of one array: the loads of a chunk are issued
-        // together before its stores (a load-fma-store loop waited on every
-        // load in turn)
-        for (int d0 = 0; d0 < ndim; d0 += 8) {
-            double pv[8], cv[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-                if (d0 + k < ndim) { pv[k] = p[d0 + k]; cv[k] = cj[d0 + k]; }
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-                if (d0 + k < ndim) p[d0 + k] = fma(pv[k] - cv[k], z, cv[k]);
+        for (int d = lane; d < ndim; d += 64) p[d] = fma(p[d] - cj[d], z, cj[d]);
+        if (lane == 0) {
+            lnp[w] = lnp_new[i];
+            if (naccept) naccept[w] += 1;
         }
-        lnp[w] = lnp_new[i];
-        if (naccept) naccept[w] += 1;
     }
-    if (accflag) accflag[i] = (lu < diff) ? 1 : 0;  // the speculative setup's candidate choice
+    if (accflag && lane == 0) accflag[i] = acc ? 1 : 0;  // the speculative setup's candidate choice
 }
 
 // ------------------------------------------------------ k_gp, k_wdphases
@@ -3751,16 +3896,34 @@ int lfg_flux(const double* pars, int W, int P, const double* x, const double* w,
     return LFG_OK;
 }
 
-// k_pair serves trees whose eclipses fit one tile with S = 1 and no GP
-// (LFG_PAIR=1 in the environment; k_elements + k_lnlike otherwise)
+// k_pair serves trees whose eclipses fit one tile with S = 1 (GP trees
+// included); k_elements + k_lnlike serve the rest, and every tree when
+// LFG_PAIR=0 is in the environment (the A/B switch of the two layouts)
+static bool pair_env()
+{
+    const char* e = getenv("LFG_PAIR");
+    return !(e && e[0] == '0');
+}
+static std::atomic<int> g_pair_layout{-2};  // -2: not read yet; 0 / 1: lfg_set_layout or the environment
+
 static bool pair_ok(int gp, int nsub, int max_n, int ndim)
 {
-    static const bool env = [] {
-        const char* e = getenv("LFG_PAIR");
-        return e && e[0] == '1';
-    }();
+    int m = g_pair_layout.load(std::memory_order_relaxed);
+    if (m == -2) {
+        m = pair_env() ? 1 : 0;
+        g_pair_layout.store(m, std::memory_order_relaxed);
+    }
     (void)gp;
-    return env && nsub == 1 && max_n <= LIKE_TILE && ndim <= LIKE_THREADS;
+    return m == 1 && nsub == 1 && max_n <= LIKE_TILE && ndim <= LIKE_THREADS;
+}
+
+int lfg_set_layout(int mode)
+{
+    if (mode < -1 || mode > 1) return LFG_E_ARGS;
+    int prev = g_pair_layout.load();
+    if (prev == -2) prev = pair_env() ? 1 : 0;
+    g_pair_layout.store(mode == -1 ? (pair_env() ? 1 : 0) : mode);
+    return prev;
 }
 
 int lfg_layout(const lfg_tree* T)
@@ -3909,7 +4072,14 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
     L.accflag = (sp && acc) ? ws.accflag + size_t(prop->half) * ws.accstride : nullptr;
     L.combine = T->E == 1;  // E > 1: k_combine_walkers after the likelihood kernels
     if (pair_path) {
-        PairArgs A{L, X, nullptr, nullptr, spl, nbc};
+        PairArgs A{L, X, nullptr, nullptr, spl, nbc, 0ull, 0ull, 0, 0, 0};
+        if (prop) {
+            A.jseed = prop->seed;
+            A.jstep = prop->step;
+            A.jhalf = prop->half;
+            A.jlo = prop->lo;
+            A.jns = prop->ns;
+        }
         if (sp && sp->out && acc && T->E == 1) {
             // this launch accepts moves of half h while its speculative lanes
             // read half h's rows: they read the snapshot of them instead (taken
@@ -4089,8 +4259,9 @@ int lfg_stretch_accept_regen(double* pos, double* lnp, int W, int ndim, int half
     if (W < 4 || (W & 1) || ndim <= 0 || (half != 0 && half != 1) || !(a > 1.0) || !pos || !lnp || !lnp_new)
         return LFG_E_ARGS;
     const int ns = W / 2;
-    hipLaunchKernelGGL(k_accept_regen, dim3((ns + 63) / 64), dim3(64), 0, static_cast<hipStream_t>(stream), pos,
-                       lnp, W, ndim, half, a, lnp_new, seed, step, naccept, nullptr);
+    hipLaunchKernelGGL(k_accept_regen, dim3((ns + REGEN_WAVES - 1) / REGEN_WAVES), dim3(64 * REGEN_WAVES), 0,
+                       static_cast<hipStream_t>(stream), pos, lnp, W, ndim, half, a, lnp_new, seed, step, naccept,
+                       nullptr);
     return launch_ok();
 }
 
@@ -4104,8 +4275,8 @@ int lfg_stretch_accept_regen_spec(double* pos, double* lnp, int W, int half, dou
     const Ws ws = carve(wsp, n, T->E, T->gp ? T->max_n : 0, T->ndim, W / 2);
     if (!wsp || ws_bytes < ws.total) return LFG_E_WORKSPACE;
     const int ns = W / 2;
-    hipLaunchKernelGGL(k_accept_regen, dim3((ns + 63) / 64), dim3(64), 0, static_cast<hipStream_t>(stream), pos,
-                       lnp, W, T->ndim, half, a, lnp_new, seed, step, naccept,
+    hipLaunchKernelGGL(k_accept_regen, dim3((ns + REGEN_WAVES - 1) / REGEN_WAVES), dim3(64 * REGEN_WAVES), 0,
+                       static_cast<hipStream_t>(stream), pos, lnp, W, T->ndim, half, a, lnp_new, seed, step, naccept,
                        ws.accflag + size_t(half) * ws.accstride);
     return launch_ok();
 }
@@ -4239,6 +4410,11 @@ int lfg_debug_like_waves(unsigned long long* host)
 int lfg_debug_pair(unsigned long long* host)
 {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pair_t), sizeof(g_pair_t)) == hipSuccess ? 0 : -1;
+}
+// its per-chunk job stamps (start, sink entry, end), host [3][16][4096]
+int lfg_debug_pair_jobs(unsigned long long* host)
+{
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pair_j), sizeof(g_pair_j)) == hipSuccess ? 0 : -1;
 }
 // and its per-wave sweep stamps, host [4][8][4096]
 int lfg_debug_pair_waves(unsigned long long* host)

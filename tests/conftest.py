@@ -48,4 +48,6 @@ def _native_library_is_this_tree(request):
     except Exception:
         return
     from lfit_python_amd import _native
+    if os.environ.get("LFG_LIB") and os.environ.get("LFG_DIAGNOSTIC") == "1":
+        return  # an explicitly loaded experiment build (tools/build_exp.sh)
     _native.verify()

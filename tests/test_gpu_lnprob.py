@@ -13,6 +13,20 @@ GOLD = os.path.join(os.path.dirname(__file__), "golden")
 LNP_RTOL = 1e-8   # ln_prob ~ -1e3: flux parity 1e-12 -> |d chi^2| << 1e-6
 
 
+@pytest.fixture
+def layout(request):
+    """Run the test on one kernel layout (lfg_set_layout): 1 = k_pair, the
+    default for one-tile S = 1 trees; 0 = k_elements + k_lnlike."""
+    from lfit_python_amd import _native
+    L = _native.lib()
+    prev = L.lfg_set_layout(request.param)
+    yield request.param
+    L.lfg_set_layout(prev)
+
+
+LAYOUTS = pytest.mark.parametrize("layout", [1, 0], indirect=True, ids=["pair", "two_kernel"])
+
+
 def _same(a, b, rtol):
     a, b = np.asarray(a, float), np.asarray(b, float)
     assert np.array_equal(np.isfinite(a), np.isfinite(b))
@@ -25,8 +39,9 @@ def _golden_tree(tag, tmpdir):
     return golden_tree(tag, tmpdir)
 
 
+@LAYOUTS
 @pytest.mark.parametrize("tag", ["tree", "simple"])
-def test_lnprob_matches_reference_tree(tag, tmp_path):
+def test_lnprob_matches_reference_tree(tag, tmp_path, layout):
     import torch
     from lfit_python_amd import batch
     d, m = _golden_tree(tag, tmp_path)
@@ -46,8 +61,9 @@ def _flux_fn(p, x, w, nsub):
     return f[0].cpu().numpy()
 
 
+@LAYOUTS
 @pytest.mark.parametrize("cfg", ["c1_simple", "c2_complex", "c3_tree", "c5_fine"])
-def test_lnprob_configs_match_oracle(oracle, cfg):
+def test_lnprob_configs_match_oracle(oracle, cfg, layout):
     import torch
     from lfit_python_amd import batch, synthetic
     if cfg == "c1_simple":
@@ -356,7 +372,8 @@ def test_graph_replay_matches_eager():
         np.testing.assert_array_equal(a, b)
 
 
-def test_spec_chain_with_interleaved_calls():
+@LAYOUTS
+def test_spec_chain_with_interleaved_calls(layout):
     """The speculative path stays bit-identical to the plain half-step when
     other entry points use the evaluator between steps (their workspace use
     overlaps the candidates, so the next step recomputes its setup)."""
@@ -451,7 +468,8 @@ def test_gp_kernel_matches_dense_oracle(oracle):
         assert abs(got[i] - ref) <= 1e-9 * abs(ref), (i, got[i], ref)
 
 
-def test_gp_tree_matches_reference():
+@LAYOUTS
+def test_gp_tree_matches_reference(layout):
     """Batched ln_prob of the shipped GP example (87 parameters, 6 eclipses)
     against the reference tree's own ln_prob (tests/golden/lnprob_gp.npz)."""
     import torch
@@ -468,7 +486,8 @@ def test_gp_tree_matches_reference():
     _same(lle.cpu().numpy().sum(1)[fin], d["ln_like"][fin], LNP_RTOL)
 
 
-def test_gp_tree_spec_chain():
+@LAYOUTS
+def test_gp_tree_spec_chain(layout):
     """The speculative half-step on the shipped GP tree (87 parameters, 6
     eclipses: acceptance through k_gp_like's per-walker combine) equals the
     plain half-step bit for bit."""

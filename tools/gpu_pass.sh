@@ -5,6 +5,7 @@
 # first fault / abort / timeout ends the pass -- tools/gpu_steps.sh):
 #   test   pytest -m gpu                    smoke  __graft_entry__.smoke()
 #   c2     bench config 2 (100 steps, CPU baselines)   c2_20  the driver's 20-step command
+#   c2_20two  the same on the two-kernel layout (LFG_PAIR=0)
 #   p2     rocprofv3 kernel trace of config 2          pmc2   PMC passes of config 2 (tools/pmc_profile.sh)
 #   c3 c4 c4e c5 gp xch   benches (config 4 one-of-eight rehearsal, GP example, exchange path)
 #   p5 pgp rocprofv3 kernel traces of config 5 and the GP example
@@ -25,6 +26,7 @@ for s in $steps; do
     smoke) args+=("${tag}_smoke:200:python3 -c 'import __graft_entry__ as g; g.smoke()'") ;;
     c2)    args+=("${tag}_c2:300:python3 bench.py > $O/${tag}_c2.json") ;;
     c2_20) args+=("${tag}_c2_20:200:python3 bench.py --steps 20 --warmup 5 --no-cpu > $O/${tag}_c2_20.json") ;;
+    c2_20two) args+=("${tag}_c2_20two:200:LFG_PAIR=0 python3 bench.py --steps 20 --warmup 5 --no-cpu > $O/${tag}_c2_20_two.json") ;;
     p2)    args+=("${tag}_p2:200:rocprofv3 --kernel-trace --stats -d $O/${tag}_prof2 -o run --output-format csv -- python3 bench.py --steps 100 --warmup 5 --no-cpu") ;;
     pmc2)  args+=("${tag}_pmc2:900:bash tools/pmc_profile.sh ${tag}2") ;;
     c3)    args+=("${tag}_c3:300:python3 bench.py --config 3 --steps 30 > $O/${tag}_c3.json") ;;

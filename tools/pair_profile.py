@@ -74,5 +74,15 @@ if L.lfg_debug_pair_waves(ctypes.c_void_p(wv.ctypes.data)) == 0 and wv.any():
         d = (wv[k] - b3[None, :]) / 100.0
         print("  %-20s earliest %6.2f  latest %6.2f" % (nm, np.median(d.min(0)), np.median(d.max(0))))
     print("  %-20s %6.2f" % ("scan done (thread 0)", np.median((t[12] - b3) / 100.0)))
+jb = np.zeros((3, 16, 4096), dtype=np.uint64)
+if hasattr(L, "lfg_debug_pair_jobs") and L.lfg_debug_pair_jobs(ctypes.c_void_p(jb.ctypes.data)) == 0 and jb.any():
+    jb = jb[:, :, :nb].astype(np.float64)
+    print("element jobs per chunk (us, median over blocks): solve (start -> sink entry), sink (-> end)")
+    for c in range(15):
+        ok = (jb[0, c] > 0) & (jb[1, c] >= jb[0, c]) & (jb[2, c] >= jb[1, c])
+        if ok.any():
+            sv = (jb[1, c][ok] - jb[0, c][ok]) / 100.0
+            sk = (jb[2, c][ok] - jb[1, c][ok]) / 100.0
+            print("  chunk %2d  solve %6.2f  sink %6.2f  (n %d)" % (c, np.median(sv), np.median(sk), ok.sum()))
 if len(sys.argv) > 2:  # raw stamps for offline analysis
     np.save(sys.argv[2], t)
