@@ -36,7 +36,7 @@ Roofline (MODEL_SPEC.md section 11; the path is FP64-VALU or latency bound,
 neither HBM- nor MFMA-bound):
   roofline.achieved / frac   the DOMINANT kernel (k_pair, or k_elements on
       the two-kernel layout, chosen by the warmup's events): its counted FP64
-      work per launch (profiles/r03/flops_<config>.json per pair x the pairs
+      work per launch (profiles/r04/flops_<config>.json per pair x the pairs
       of a launch) / its average launch time over the timed region (HIP events
       on its stream) / 78.6 TFLOP/s;
   roofline.traffic           HBM bytes per launch of that kernel from the
@@ -68,7 +68,7 @@ sys.path.insert(0, ROOT)
 # MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md; FP64 vector = spec)
 HBM_PEAK_GBS = 8000.0
 FP64_PEAK_TFLOPS = 78.6
-PMC_DIR = os.path.join(ROOT, "profiles", "r03")   # pmc_traffic_<config>.json (tools/pmc_traffic.py)
+PMC_DIR = os.path.join(ROOT, "profiles", "r04")   # pmc_traffic_<config>.json (tools/pmc_traffic.py)
 
 NEV = 4  # LFG_NEV (include/lfg.h)
 # (name as rocprofv3 prints it, start event, end event) per kernel layout
@@ -78,11 +78,11 @@ KERNELS_PAIR = [("k_setup", 0, 1), ("k_pair", 2, 3)]
 
 # Counted FP64 work per (walker, eclipse) pair of the algorithm the kernels
 # execute (MODEL_SPEC.md section 11; tools/flop_count.py + tools/like_count.py
-# -> profiles/r03/flops_<config>.json): per-kernel figures for the roofline's
+# -> profiles/r04/flops_<config>.json): per-kernel figures for the roofline's
 # kernel fraction and the whole step, and the direct-form count of SURVEY
 # 8(d) (900 roots x geometry + N S (1500 x 3 + 400 x 6 + 40)) kept apart as
 # direct_form_equivalent
-FLOPS_DIR = os.path.join(ROOT, "profiles", "r03")
+FLOPS_DIR = os.path.join(ROOT, "profiles", "r04")
 FLOPS_TABLE = {"2": "c2", "3": "c3", "4": "c2", "5": "c5", "gp": "gp"}
 
 # builder's intermediate tables per (walker, eclipse) pair:
@@ -541,7 +541,7 @@ def run(args):
 
     # counter-derived traffic and executed FP64 FLOPs of the dominant kernel
     # (rocprofv3 --pmc passes, tools/pmc_profile.sh -> tools/pmc_traffic.py ->
-    # profiles/r03/pmc_traffic_<config>.json); per-pair counters carry over only
+    # profiles/r04/pmc_traffic_<config>.json); per-pair counters carry over only
     # to the workload they were collected on
     row, pmc_path = pmc_row(kname, args.config, npts, tree.nsub, pairs)
     traffic = fp64x = None

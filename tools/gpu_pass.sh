@@ -5,7 +5,7 @@
 # first fault / abort / timeout ends the pass -- tools/gpu_steps.sh):
 #   test   pytest -m gpu                    smoke  __graft_entry__.smoke()
 #   c2     bench config 2 (100 steps, CPU baselines)   c2_20  the driver's 20-step command
-#   c2_20two  the same on the two-kernel layout (LFG_PAIR=0)
+#   c2_20two, gp_two, c3_two  the same on the two-kernel layout (LFG_PAIR=0)
 #   p2     rocprofv3 kernel trace of config 2          pmc2   PMC passes of config 2 (tools/pmc_profile.sh)
 #   c3 c4 c4e c5 gp xch   benches (config 4 one-of-eight rehearsal, GP example, exchange path)
 #   p5 pgp rocprofv3 kernel traces of config 5 and the GP example
@@ -34,6 +34,8 @@ for s in $steps; do
     c4e)   args+=("${tag}_c4e:300:python3 bench.py --config 4 --emulate-rank 0/8 --steps 20 --warmup 3 --no-cpu > $O/${tag}_c4_emu8.json") ;;
     c5)    args+=("${tag}_c5:300:python3 bench.py --config 5 --steps 20 --warmup 3 > $O/${tag}_c5.json") ;;
     gp)    args+=("${tag}_gp:300:python3 bench.py --config gp --steps 100 --warmup 5 > $O/${tag}_gp.json") ;;
+    gp_two) args+=("${tag}_gp_two:300:LFG_PAIR=0 python3 bench.py --config gp --steps 100 --warmup 5 > $O/${tag}_gp_two.json") ;;
+    c3_two) args+=("${tag}_c3_two:300:LFG_PAIR=0 python3 bench.py --config 3 --steps 30 --no-cpu > $O/${tag}_c3_two.json") ;;
     xch)   args+=("${tag}_xch:200:python3 bench.py --exchange-path --no-cpu > $O/${tag}_c2_xch.json") ;;
     p5)    args+=("${tag}_p5:300:rocprofv3 --kernel-trace --stats -d $O/${tag}_prof5 -o run --output-format csv -- python3 bench.py --config 5 --steps 6 --warmup 2 --no-cpu") ;;
     pgp)   args+=("${tag}_pgp:200:rocprofv3 --kernel-trace --stats -d $O/${tag}_profgp -o run --output-format csv -- python3 bench.py --config gp --steps 30 --warmup 3 --no-cpu") ;;
