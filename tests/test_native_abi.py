@@ -87,6 +87,30 @@ def test_argument_errors_without_gpu():
     assert L.lfg_version().startswith(b"lfg")
 
 
+def test_layout_switch_without_gpu():
+    """lfg_set_layout / lfg_layout (host-only): k_pair for one-tile S = 1
+    trees by default, the two-kernel layout for S > 1 and when switched off,
+    argument errors refused; the previous setting is returned and restored."""
+    L = _native.lib()
+
+    def tree(nsub, max_n):  # lfg_layout reads the sizes only
+        T = _native.LfgTree()
+        T.E, T.ndim, T.nsub, T.max_n = 1, 18, nsub, max_n
+        return ctypes.byref(T)
+
+    assert L.lfg_layout(None) == -1
+    assert L.lfg_set_layout(2) == -1 and L.lfg_set_layout(-3) == -1
+    prev = L.lfg_set_layout(1)
+    try:
+        assert L.lfg_layout(tree(1, 300)) == 1
+        assert L.lfg_layout(tree(5, 300)) == 0     # sub-binned: two kernels
+        assert L.lfg_layout(tree(1, 10000)) == 0   # more points than a tile
+        assert L.lfg_set_layout(0) == 1
+        assert L.lfg_layout(tree(1, 300)) == 0
+    finally:
+        L.lfg_set_layout(prev)
+
+
 def test_product_path_fails_loudly_without_gpu():
     import torch
     if torch.cuda.is_available():
