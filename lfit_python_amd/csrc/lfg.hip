@@ -2574,6 +2574,7 @@ struct PairArgs {
     // global load less before the candidate is known
     unsigned long long jseed, jstep;
     int jhalf, jlo, jns;
+    int prio;  // every workgroup resident at once (PAIR_PRIO)
 };
 
 // the chunks of k_pair's element jobs 1..15, longest first (spot, outer
@@ -2601,6 +2602,19 @@ __device__ unsigned long long g_pair_j[3][16][4096];  // per chunk: job start, s
 #define PAIR_STAMP(slot, cond)
 #define PAIR_WSTAMP(k)
 #endif
+
+// wave priority in a launch whose workgroups are all resident at once
+// (A.prio): the issue arbiter favours the older of a CU's two workgroups, so
+// one finished ~10 us before the other and the CU ran its last phases on
+// half its waves.  Element waves drop their priority with each job they
+// start (3, 2, 1, then 0), so both workgroups advance together; the
+// speculative setup waves (latency-bound, and the longest job) keep 3.  In a
+// launch of several rounds the older workgroup's early finish lets the next
+// round's start, so the default order stays.
+#define PAIR_PRIO(p)                                   \
+    do {                                               \
+        if (A.prio) __builtin_amdgcn_s_setprio(p);     \
+    } while (0)
 
 // k_pair's sweep of one solved item (the element phase's sink): element runs
 // over the tile's windows (WD, disc, spot) and the donor tiles' visibility
@@ -3006,6 +3020,7 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
     // instruction stream: SIMD issue slots of ~10x the work)
     const bool specblk = X.nspec > 0 && pair < 2 * A.nbc;
     if (wv == 0 && specblk) {
+        PAIR_PRIO(3);
         if (lane < A.spl) {
             // candidate uniform per block: X.S[c] stays in scalar registers
             const int c = pair < A.nbc ? 0 : 1;
@@ -3091,12 +3106,19 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
         // straight-line calls, not a loop: a loop's invariant constants (the
         // transcendental polynomials) were hoisted and spilled to scratch
         // (a block without speculative lanes starts wave w on job w + 1)
+        // wave priority falls with each job a wave starts, so that the two
+        // workgroups of a CU advance together (the issue arbiter otherwise
+        // favours the older workgroup's waves)
+        PAIR_PRIO(3);
         if (!specblk) chunk(wv + 1);
         else if (wv > 0) chunk(wv);
         int j = grab();
+        PAIR_PRIO(2);
         if (j < 16) chunk(j);
         j = grab();
+        PAIR_PRIO(1);
         if (j < 16) chunk(j);
+        PAIR_PRIO(0);
         K.flush();
     }
     static_assert(11 * 64 >= U_WD + U_DISC && 10 * 64 < U_WD + U_DISC, "11 chunks of WD/disc");
@@ -3899,6 +3921,19 @@ int lfg_flux(const double* pars, int W, int P, const double* x, const double* w,
 // k_pair serves trees whose eclipses fit one tile with S = 1 (GP trees
 // included); k_elements + k_lnlike serve the rest, and every tree when
 // LFG_PAIR=0 is in the environment (the A/B switch of the two layouts)
+// k_pair's workgroups all resident at once: two per CU (72.9 KB of LDS each)
+static bool pair_one_round(int npairs)
+{
+    static int cus = -1;
+    if (cus < 0) {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            n = 0;
+        cus = n;
+    }
+    return npairs <= 2 * cus;
+}
+
 static bool pair_env()
 {
     const char* e = getenv("LFG_PAIR");
@@ -3949,7 +3984,7 @@ int lfg_lnlike(const double* pars, int W, int P, const double* x, const double* 
                nsub, nullptr, nullptr, lnlike, W, nullptr, nullptr, nullptr, false, nullptr,
                nullptr, nullptr, nullptr, 0, 0, 0ull, 0ull, nullptr};
     L.bstatus = ws.bstatus;
-    if (pair) hipLaunchKernelGGL(k_pair<false>, dim3(W), dim3(LIKE_THREADS), 0, st, PairArgs{L, ElemSpec{}, nullptr, nullptr, 64, 0});
+    if (pair) hipLaunchKernelGGL(k_pair<false>, dim3(W), dim3(LIKE_THREADS), 0, st, PairArgs{L, ElemSpec{}, nullptr, nullptr, 64, 0, 0ull, 0ull, 0, 0, 0, pair_one_round(W) ? 1 : 0});
     else if (nsub > 1) hipLaunchKernelGGL((k_lnlike<1, true>), dim3(W), dim3(LIKE_THREADS), 0, st, L);
     else hipLaunchKernelGGL((k_lnlike<1, false>), dim3(W), dim3(LIKE_THREADS), 0, st, L);
     if ((rc = launch_ok())) return rc;
@@ -4072,7 +4107,7 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
     L.accflag = (sp && acc) ? ws.accflag + size_t(prop->half) * ws.accstride : nullptr;
     L.combine = T->E == 1;  // E > 1: k_combine_walkers after the likelihood kernels
     if (pair_path) {
-        PairArgs A{L, X, nullptr, nullptr, spl, nbc, 0ull, 0ull, 0, 0, 0};
+        PairArgs A{L, X, nullptr, nullptr, spl, nbc, 0ull, 0ull, 0, 0, 0, pair_one_round(npairs) ? 1 : 0};
         if (prop) {
             A.jseed = prop->seed;
             A.jstep = prop->step;
