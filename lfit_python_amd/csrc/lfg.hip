@@ -3186,13 +3186,38 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
     chi = wave_sum(chi);
     if (lane == 0) red[wv] = chi;
     __syncthreads();
+    // the finish (finish_walker's arithmetic) from the values thread 0
+    // holds: its ln_like, and the prior terms of the candidate it selected
+    // (what the standard slots hold now), without a barrier and a global
+    // round trip for each
     if (tid == 0) {
         double tot = 0.0;
         for (int i = 0; i < nw; ++i) tot += red[i];
-        L.lle[pair] = -0.5 * tot;
+        const double lp = lpr + Gc[G_RPRIOR] + Gc[G_RPRIOR_BS];  // finish_walker's sum, term for term
+        const double lle = isfinite(lp) ? -0.5 * tot : -INFINITY;
+        L.lle[pair] = lle;
+        PAIR_STAMP(13, true);
+        if (!acc1) {
+            combine_after(L, pair);
+        } else {
+            const int wg = L.half * L.npairs + pair;
+            const double v = isfinite(lp) ? lp + lle : -INFINITY;
+            if (L.lnp) L.lnp[pair] = v;
+            const bool a = sacc1[0] < sacc1[1] + v - sacc1[2];
+            if (a) {
+                L.lnp_ens[wg] = v;
+                if (L.naccept) L.naccept[wg] += 1;
+            }
+            sflag[0] = a ? 1 : 0;
+            if (L.accflag) L.accflag[pair] = a ? 1 : 0;
+        }
     }
-    PAIR_STAMP(13, tid == 0);
-    finish_walker(L, pair, tid, acc1, sq, sacc1, sflag);
+    if (acc1) {
+        __syncthreads();
+        const int wg = L.half * L.npairs + pair;
+        if (sflag[0] && tid < L.ndim)
+            L.pos[size_t(wg) * L.ndim + tid] = (tid < ACC_LDS) ? sq[tid] : L.qprop[size_t(pair) * L.ndim + tid];
+    }
     PAIR_STAMP(15, tid == 0);
 }
 
