@@ -3101,7 +3101,7 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
         auto grab = [&]() {
             int j = 0;
             if (lane == 0) j = atomicAdd(&sjob, 1);
-            return __builtin_amdgcn_readfirstlane(__shfl(j, 0, 64));
+            return __builtin_amdgcn_readfirstlane(j);  // every lane is active: the first is lane 0
         };
         // straight-line calls, not a loop: a loop's invariant constants (the
         // transcendental polynomials) were hoisted and spilled to scratch
