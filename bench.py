@@ -267,6 +267,16 @@ def pmc_row(kernel, config, npts, nsub, pairs):
     return {k: v * scale for k, v in out.items()}, os.path.relpath(path, ROOT)
 
 
+def line_value(W, steps, elapsed, emu=None):
+    """The line's value: walker ln_prob evaluations per second of the whole
+    job.  W is the ensemble over all ranks; each step evaluates every walker
+    once (two half-steps of W/2).  Emulating rank K of N (emu = (K, N)), the
+    process holds the whole ensemble but evaluates W / N walkers per step:
+    only those count."""
+    evaluated = W // emu[1] if emu else W
+    return evaluated * steps / elapsed
+
+
 def rank_block(dist, world, backend, own_ms, xch_ms, cnt, dev):
     """The line's "ranks" object (every rank calls it: one all_gather of each
     rank's own ms per step and exchange ms): world size, backend, the RCCL
@@ -513,9 +523,7 @@ def run(args):
     avg_dom = float(dom_ms[0])
     E = tree.E
     npts = int(np.max(np.diff(tree.offsets)))
-    # emulation: one rank of N evaluates W / N walkers per step (the rest of the
-    # ensemble is held, not evaluated): the line counts what was evaluated
-    value = (W // args.emu[1] if args.emu else W) * args.steps / elapsed
+    value = line_value(W, args.steps, elapsed, args.emu)
     acc = float(np.mean(S.acceptance_fraction))
 
     # ---- FP64 roofline on the counted work of the executed algorithm (MODEL_SPEC 11)

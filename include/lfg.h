@@ -4,9 +4,12 @@
  * wildjames/lfit_python (reference at /root/reference).
  *
  * Every entry point takes plain pointers and sizes (no torch types), is
- * re-entrant, keeps no global mutable state, never allocates, and enqueues its
- * kernels on the caller's HIP stream (`stream` = hipStream_t, NULL = default
- * stream).  Pointers marked [dev] are device (HBM) pointers; scratch space is
+ * re-entrant, never allocates, and enqueues its kernels on the caller's HIP
+ * stream (`stream` = hipStream_t, NULL = default stream).  The one piece of
+ * process-wide state is the kernel-layout switch (lfg_set_layout, read once
+ * from the environment's LFG_PAIR): a measurement and test control that
+ * selects between two implementations with identical results; every other
+ * input is an argument.  Pointers marked [dev] are device (HBM) pointers; scratch space is
  * passed in as `ws` of at least lfg_workspace_size() bytes.  All arithmetic is
  * FP64.  Return value: LFG_OK or an LFG_E_* code (launch/argument errors).
  * Per-parameter-set model failures are NOT call errors: they are reported in
@@ -185,9 +188,16 @@ int lfg_roche(int op, const double* a, const double* b, int n, double* out,
 
 /*
  * Same as lfg_lnprob, recording LFG_NEV caller-created hipEvent_t events on
- * `stream` around each kernel (bench timing): ev[0] before k_setup, ev[1]
- * after k_setup, ev[2] after k_elements, ev[3] after k_lnlike (which also
- * forms ln_prob).  NULL entries are skipped.
+ * `stream` around each phase (bench timing).  NULL entries are skipped.
+ *   ev[0] before k_setup (every layout);
+ *   ev[1] after k_setup (= ev[0]'s position when the speculative candidates
+ *         stand in for it);
+ *   ev[2] after k_elements on the two-kernel layout; on the k_pair layout
+ *         (lfg_layout = 1) nothing runs between ev[1] and ev[2];
+ *   ev[3] after the likelihood kernels: k_lnlike, or k_pair (element solve,
+ *         chi^2, ln_prob and the fused acceptance in one launch), followed
+ *         for GP trees by k_gp_like and for E > 1 by k_combine_walkers.
+ * So ev[2] -> ev[3] times k_pair alone for a one-eclipse chi^2 tree.
  */
 #define LFG_NEV 4
 int lfg_lnprob_timed(const double* walkers, int W, const lfg_tree* tree,
@@ -400,7 +410,10 @@ int lfg_layout(const lfg_tree* tree);
  * k_lnlike for every tree, 1 = k_pair where lfg_layout allows it (the
  * default), -1 = back to the environment's choice (LFG_PAIR=0 selects 0).
  * Returns the previous setting (0 or 1), LFG_E_ARGS for another value.  Not
- * synchronised with launches in flight on other host threads. */
+ * synchronised with launches in flight on other host threads.  A switch
+ * between the two halves of a speculative chain (spec_out = 1 then
+ * spec_in = 1) is safe: both layouts leave the partner-half snapshot the
+ * k_pair launch reads. */
 int lfg_set_layout(int mode);
 
 #ifdef __cplusplus

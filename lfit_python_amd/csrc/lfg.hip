@@ -2498,8 +2498,9 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
         // skipped the scan waits here instead
         if (TAB && !dir && !wdd) __syncthreads();
         if (own) {
-            const double fwv = SG[G_WDF] * (1.0 - fw), fdv = SG[G_DF] * (1.0 - fd);
-            const double fb = SG[G_SF] * sbs / S, fr = SG[G_RSF] * srs / S;
+            const double nw0 = isnan(wk) ? NAN : 1.0;  // MODEL_SPEC 3: a NaN width gives a NaN flux
+            const double fwv = nw0 * SG[G_WDF] * (1.0 - fw), fdv = nw0 * SG[G_DF] * (1.0 - fd);
+            const double fb = nw0 * SG[G_SF] * sbs / S, fr = nw0 * SG[G_RSF] * srs / S;
             const double f = fwv + fdv + fb + fr;
             const int pi = t0 + tid;
             if (!CHI && L.flux) L.flux[size_t(pair) * n + pi] = f;
@@ -2977,6 +2978,9 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
             L.gpx[size_t(pair) * L.N + tid] = exp(-(Gc[G_GP_LAM] * dx));
         }
     }
+    // GP: the changepoint distance is solved in this launch (the cache rule
+    // tripped, G_GP_OK = 2); wave 0 then owns the slot's G_GP_DCP / G_GP_OK
+    const bool pend = GP && st == ST_OK && Gc[G_GP_OK] == 2.0;
     if (wv == 7) {
         // housekeeping off the prologue's critical path: the selected candidate
         // into the standard slots (API readers, k_combine_walkers, k_gp_like),
@@ -2986,7 +2990,8 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
         if (X.jk) {
             const size_t cw = size_t(cand) * nwk + w;
             double* Gd = const_cast<double*>(L.geo) + size_t(pair) * LFG_NGEO;
-            if (l < LFG_NGEO) Gd[l] = G[l];
+            // (a pending changepoint's two words are wave 0's: one writer each)
+            if (l < LFG_NGEO && !(pend && (l == G_GP_DCP || l == G_GP_OK))) Gd[l] = G[l];
             if (l == 48) X.bstatus[pair] = bst;
             if (e == 0) {
                 const double* qc = X.qC + cw * X.ndim;
@@ -3039,7 +3044,6 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
         // the changepoint distance: the cache's, or (cache rule tripped,
         // G_GP_OK = 2) dist_cp = (dphi + phi4 - phi3) / 2 from ten limb
         // points' egress phases (CVModel.py:561-570; k_gp_dcp's solve)
-        const bool pend = st == ST_OK && Gc[G_GP_OK] == 2.0;
         if (pend && wv == 0 && lane >= 32 && lane < 32 + DCP_LANES) {
             const int k = lane - 32;
             bool ok = Gc[G_GP_RWD] > 0.0;
@@ -3146,7 +3150,9 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
             if (own) {
                 const double wk = L.w ? L.w[o0 + tid] : 0.0;
                 const double2 f2 = pair_direct_wd_disc(SU.ab, ul, swt, phc, wk, twd, swt[NDISC_R]);
-                fw = f2.x;
+                // MODEL_SPEC 3: a NaN width gives a NaN flux (such a tile is
+                // always point-major: its window fails the sortedness test)
+                fw = isnan(wk) ? NAN : f2.x;
                 fd = f2.y;
                 eb = direct_spot(sab, sbw, phc, wk, 1.0 / wspot);
             }
@@ -3949,15 +3955,14 @@ int lfg_flux(const double* pars, int W, int P, const double* x, const double* w,
 // k_pair's workgroups all resident at once: two per CU (72.9 KB of LDS each)
 static bool pair_one_round(int npairs)
 {
-    static int cus = -1;
-    if (cus < 0) {
-        int dev = 0, n = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            n = 0;
-        cus = n;
-    }
+    int dev = 0, cus = 0;  // the current device's (the runtime caches the attribute)
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 0;
     return npairs <= 2 * cus;
 }
+
+// the trees k_pair can serve: one-tile eclipses, S = 1
+static bool pair_fits(int nsub, int max_n, int ndim) { return nsub == 1 && max_n <= LIKE_TILE && ndim <= LIKE_THREADS; }
 
 static bool pair_env()
 {
@@ -3974,7 +3979,7 @@ static bool pair_ok(int gp, int nsub, int max_n, int ndim)
         g_pair_layout.store(m, std::memory_order_relaxed);
     }
     (void)gp;
-    return m == 1 && nsub == 1 && max_n <= LIKE_TILE && ndim <= LIKE_THREADS;
+    return m == 1 && pair_fits(nsub, max_n, ndim);
 }
 
 int lfg_set_layout(int mode)
@@ -4114,9 +4119,9 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
         }
     }
     // k_pair: the element solve and the likelihood of a pair in one
-    // workgroup (one-tile eclipses, S = 1, no GP); the speculative lanes must
-    // fit wave 7's spare lanes
-    // the speculative lanes: whole waves (wave 0 of blocks [0, 2 nbc)), nbc per candidate
+    // workgroup (one-tile eclipses, S = 1; GP trees through k_pair<true> and
+    // k_gp_like).  The speculative lanes fill whole waves: wave 0 of blocks
+    // [0, 2 nbc), nbc blocks per candidate, so there must be 2 nbc pairs
     const int spl = 64, nbc = (X.nspec + 63) / 64;
     const bool pair_path = pair_ok(T->gp, T->nsub, T->max_n, T->ndim) && (X.nspec == 0 || 2 * nbc <= npairs);
     int rc = run_front(S, ws, st, ev, !pair_path, &X, !(sp && sp->in));
@@ -4172,6 +4177,16 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
         }
         mark(3);
         return LFG_OK;
+    }
+    if (sp && sp->out && acc && T->E == 1 && pair_fits(T->nsub, T->max_n, T->ndim)) {
+        // a k_pair-eligible tree on the two-kernel layout (lfg_set_layout(0)):
+        // leave the partner-half snapshot a k_pair launch would have left, so
+        // that a layout switch before the chain's next half reads valid rows
+        const int hn = 1 - prop->half;
+        const size_t rows = size_t(prop->ns) * T->ndim;
+        if (hipMemcpyAsync(ws.snap + size_t(hn) * ws.accstride * T->ndim, prop->pos + size_t(hn) * rows,
+                           rows * sizeof(double), hipMemcpyDeviceToDevice, st) != hipSuccess)
+            return LFG_E_LAUNCH;
     }
     if (T->gp) {
         L.res = ws.res;

@@ -403,12 +403,18 @@ class EnsembleSampler:
         sync-free path is run_mcmc()."""
         buf, thin = self._begin(p0, lnprob0, rstate0, iterations,
                                 thin, storechain if store is None else store)
-        for i in range(int(iterations)):
-            self.step()
-            self._store(buf, i, thin)
-            if i == int(iterations) - 1:
-                self._end(buf)
-            yield _host(self.pos), _host(self.lnp), self.random_state
+        try:
+            for i in range(int(iterations)):
+                self.step()
+                self._store(buf, i, thin)
+                if i == int(iterations) - 1:
+                    self._end(buf)
+                    buf = None
+                yield _host(self.pos), _host(self.lnp), self.random_state
+        finally:
+            # a caller that leaves the generator early (break, GeneratorExit)
+            # still gets the chunk offloaded
+            self._end(buf)
 
     def run_mcmc(self, pos0, N, rstate0=None, lnprob0=None, storechain=True, store=None, thin=1, **kwargs):
         """emcee 2.x run_mcmc: N steps from pos0 (None: the current state);
@@ -424,7 +430,9 @@ class EnsembleSampler:
 
     def _concat(self):
         """the stored chain as one (chain, lnprob) pair, wherever the chunks
-        live (host after offload); not cached in place of the chunks"""
+        live (host after offload).  Host chunks are replaced by their
+        concatenation (one host copy of the chain), and the last
+        run's chunk becomes a view into it"""
         import torch
         if self._cat is None:
             if not self._chunks:
@@ -433,8 +441,16 @@ class EnsembleSampler:
             elif len(self._chunks) == 1:
                 self._cat = self._chunks[0]
             else:
+                on_host = all(c.device.type == "cpu" for c, _ in self._chunks)
+                last = self._chunks[-1]
                 self._cat = (torch.cat([c.cpu() for c, _ in self._chunks]),
                              torch.cat([l.cpu() for _, l in self._chunks]))
+                if on_host:
+                    n = last[0].shape[0]
+                    if self._last is last:
+                        self._last = (self._cat[0][self._cat[0].shape[0] - n:],
+                                      self._cat[1][self._cat[1].shape[0] - n:])
+                    self._chunks = [self._cat]
         return self._cat
 
     @property

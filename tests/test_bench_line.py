@@ -49,7 +49,17 @@ def test_rank_block_two_gloo_ranks():
 def test_emulation_counts_evaluated_walkers():
     """--emulate-rank K/N holds the whole ensemble but evaluates W / N walkers
     per step: the line's value must count those"""
-    import ast
-    src = open(os.path.join(ROOT, "bench.py")).read()
-    assert "value = (W // args.emu[1] if args.emu else W) * args.steps / elapsed" in src
-    ast.parse(src)
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    # config 4 rehearsed as rank 0 of 8: 16 384 walkers held, 2 048 evaluated per step
+    assert bench.line_value(16384, 20, 0.5, (0, 8)) == pytest.approx(2048 * 20 / 0.5)
+    assert bench.line_value(16384, 20, 0.5, (7, 8)) == pytest.approx(2048 * 20 / 0.5)
+    # no emulation: every walker of the ensemble, once per step
+    assert bench.line_value(1024, 100, 0.01) == pytest.approx(1024 * 100 / 0.01)
+    assert bench.line_value(2048, 10, 1.0, (1, 2)) == pytest.approx(1024 * 10)
+    # the CLI parses K/N into the tuple line_value takes
+    args = bench.parse(["--config", "4", "--emulate-rank", "3/8", "--steps", "7"])
+    assert args.emu == (3, 8) and args.exchange_path
+    assert bench.walker_count(args, 1) == 16384      # the whole ensemble is held
+    assert bench.line_value(bench.walker_count(args, 1), args.steps, 2.0, args.emu) == pytest.approx(2048 * 7 / 2.0)
