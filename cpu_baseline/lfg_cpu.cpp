@@ -352,7 +352,7 @@ double chisq(const Pair& G, const Tables& T, const double* x, const double* w, c
     double* xs = ds + ns + 1;   // spot direct
     bool sorted = true;
     for (int p = 0; p < n; ++p) {
-        const double ph = wrap_phase(x[p] - G.phi0), h = w ? w[p] : 0.0;
+        const double ph = wrap_phase(x[p] - G.phi0), h = (w && !(w[p] < 0.0)) ? w[p] : 0.0;  // MODEL_SPEC 3
         lo[p] = ph - h;
         hi[p] = ph + h;
         iw[p] = 1.0 / (2.0 * h);

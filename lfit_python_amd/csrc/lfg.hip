@@ -2370,7 +2370,9 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
                 if (!GP) sye[tid] = L.ye[p];
             }
         }
-        const double wk = own ? pw : 0.0;
+        // MODEL_SPEC 3: a negative width is a zero one (point evaluation at the
+        // centre for every S); NaN stays NaN
+        const double wk = own ? (pw < 0.0 ? 0.0 : pw) : 0.0;
         const double ph0 = own ? px - SG[G_PHI0] : 0.0;
         const double phc = wrap_phase(ph0);
         double fw = 0.0, fd = 0.0, sbs = 0.0, srs = 0.0;
