@@ -389,15 +389,15 @@ def run(args):
             events.append((evs, q.shape[0]))
         ev.step_half(pos, lnp, half, a, seed, step, q, zfac, naccept, lnp_new=lnp_new, events=evs, spec=spec)
 
-    def timed_shard(pos, half, a, seed, step, lo, q, zfac, lnp_sh, spec=False):
-        """the multi-rank path: this rank's lfg_stretch_step_shard(_spec) with the events"""
+    def timed_shard(pos, half, a, seed, step, lo, q, zfac, lnp_sh, spec=False, fold=None):
+        """the multi-rank path: this rank's lfg_stretch_step_shard(_spec / _fold) with the events"""
         evs = None
         if sampled():
             evs = make_evs()
             events.append((evs, lnp_sh.shape[0]))
-        ev.step_shard(pos, half, a, seed, step, lo, q, zfac, lnp_sh, events=evs, spec=spec)
+        ev.step_shard(pos, half, a, seed, step, lo, q, zfac, lnp_sh, events=evs, spec=spec, fold=fold)
 
-    timed_half.takes_spec = timed_shard.takes_spec = True
+    timed_half.takes_spec = timed_shard.takes_spec = timed_shard.takes_fold = True
 
     # the per-half-step ln_prob exchange, timed by HIP events on the stream it
     # is enqueued on, on the calls whose shard kernels are sampled too

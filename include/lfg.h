@@ -330,6 +330,49 @@ int lfg_stretch_accept_regen(double* pos, double* lnp, int W, int ndim,
                              int* naccept, void* stream);
 
 /*
+ * The sharded half-step with the acceptance deferred into the next launch
+ * (the multi-rank replacement of the reference's pool.map fan-out,
+ * mcmcfit.py:273-288, in ONE kernel plus the collective per half-step):
+ *
+ *   rank r, half h:  lfg_stretch_step_shard_fold(.., verdict_prev = V[1-h],
+ *                                                 verdict = v_r, ..)
+ *                    all_gather(V[h] <- v_r over ranks)
+ *
+ * A verdict is the walker's new ln_prob where its move was accepted and NaN
+ * where it was not (k_accept_regen's test, made by the rank that evaluated
+ * the walker, whose old ln_prob is at hand).  The call applies verdict_prev
+ * (the other half's moves of the half-step before: rows re-formed from the
+ * draws, lnp, naccept) to pos / lnp / naccept, chooses each pair's
+ * speculative candidate by the same verdicts, evaluates walkers lo .. lo+n-1
+ * of half `half` (q, zfac, lnp_new [dev] n as lfg_stretch_step_shard) and
+ * writes their verdicts to verdict [dev] n.  On the k_pair layout with one
+ * eclipse and chi^2 that is one launch; other trees run the apply, the
+ * shard's kernels and a verdict kernel in sequence (same results).
+ *   verdict_prev [dev] W/2 or NULL (nothing pending: the chain's first call,
+ *                or after lfg_stretch_apply_verdicts); it must be the other
+ *                half's verdicts of the immediately preceding half-step
+ *   spec_in / spec_out as lfg_stretch_step_shard_spec; spec_in = 1 needs
+ *                verdict_prev and the same workspace as that call
+ * Until the pending verdicts are applied, pos / lnp / naccept of that half
+ * hold the state before its last move: lfg_stretch_apply_verdicts(.., half,
+ * step of that half's proposal, V[half]) brings them up to date (the flush at
+ * the end of a run).  Workspace: lfg_workspace_size_tree(W/2, tree).  The
+ * chain equals lfg_stretch_step_shard_spec + lfg_stretch_accept_regen_spec's.
+ */
+int lfg_stretch_step_shard_fold(double* pos, double* lnp, int W, int half,
+                                double a, unsigned long long seed,
+                                unsigned long long step, int lo, int n,
+                                double* q, double* zfac, const lfg_tree* tree,
+                                const double* verdict_prev, double* verdict,
+                                double* lnp_new, int* naccept, int spec_in,
+                                int spec_out, void* ws, size_t ws_bytes,
+                                void* stream, void* const* ev);
+int lfg_stretch_apply_verdicts(double* pos, double* lnp, int W, int ndim,
+                               int half, double a, unsigned long long seed,
+                               unsigned long long step, const double* verdict,
+                               int* naccept, void* stream);
+
+/*
  * The same two moves with the step counter read from device memory
  * (step_dev [dev] 1 x uint64), so that one emcee iteration can be captured
  * in a HIP graph and replayed; the caller advances *step_dev after half 1.

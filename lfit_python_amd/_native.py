@@ -70,7 +70,7 @@ class LfgTree(ctypes.Structure):
 EXPORTS = ("lfg_workspace_size", "lfg_workspace_size_tree", "lfg_flux", "lfg_lnlike", "lfg_lnprob", "lfg_lnprior", "lfg_lnprob_timed",
            "lfg_stretch_lnprob_accept", "lfg_stretch_step_half", "lfg_stretch_step_half_spec",
            "lfg_stretch_step_shard", "lfg_stretch_step_shard_spec", "lfg_stretch_accept_regen_spec",
-           "lfg_stretch_accept_regen",
+           "lfg_stretch_accept_regen", "lfg_stretch_step_shard_fold", "lfg_stretch_apply_verdicts",
            "lfg_elements", "lfg_roche", "lfg_stretch_propose", "lfg_stretch_accept",
            "lfg_stretch_propose_dev", "lfg_stretch_accept_dev", "lfg_event_create", "lfg_event_destroy",
            "lfg_event_elapsed_ms", "lfg_wdphases", "lfg_gp_lnlike", "lfg_component_workspace_size",
@@ -204,6 +204,12 @@ def lib():
         L.lfg_stretch_accept_regen_spec.restype = ip
         L.lfg_stretch_accept_regen_spec.argtypes = [vp, vp, ip, ip, f64, u64, u64, vp, vp, ctypes.POINTER(LfgTree),
                                                     ip, vp, sz, vp]
+        L.lfg_stretch_step_shard_fold.restype = ip
+        L.lfg_stretch_step_shard_fold.argtypes = [vp, vp, ip, ip, f64, u64, u64, ip, ip, vp, vp,
+                                                  ctypes.POINTER(LfgTree), vp, vp, vp, vp, ip, ip, vp, sz, vp,
+                                                  ctypes.POINTER(vp)]
+        L.lfg_stretch_apply_verdicts.restype = ip
+        L.lfg_stretch_apply_verdicts.argtypes = [vp, vp, ip, ip, ip, f64, u64, u64, vp, vp, vp]
         L.lfg_stretch_accept_regen.restype = ip
         L.lfg_stretch_accept_regen.argtypes = [vp, vp, ip, ip, ip, f64, u64, u64, vp, vp, vp]
         L.lfg_stretch_propose_dev.restype = ip

@@ -276,12 +276,18 @@ class LnProbEvaluator:
         step_half)."""
         self._spec_key = None
 
-    def step_shard(self, pos, half, a, seed, step, lo, q, zfac, lnp_new, events=None, spec=False):
+    def step_shard(self, pos, half, a, seed, step, lo, q, zfac, lnp_new, events=None, spec=False, fold=None):
         """This rank's part of a sharded half-step (lfg_stretch_step_shard):
         the proposals of walkers lo .. lo + n - 1 of half `half` (n =
         lnp_new.numel()) into q / zfac and their ln_prob into lnp_new.
         spec=True (lfg_stretch_step_shard_spec): speculative setup as in
-        step_half; pair it with accept_regen() on this evaluator."""
+        step_half; pair it with accept_regen() on this evaluator.
+        fold=(lnp, verdict_prev, verdict, naccept): the deferred acceptance
+        instead (step_shard_fold)."""
+        if fold is not None:
+            lnp, vprev, verdict, naccept = fold
+            return self.step_shard_fold(pos, lnp, half, a, seed, step, lo, q, zfac, lnp_new, vprev, verdict, naccept,
+                                        events=events)
         W, n = pos.shape[0], lnp_new.shape[0]
         vp = lambda t: ctypes.c_void_p(t.data_ptr())
         if not spec:
@@ -303,6 +309,42 @@ class LnProbEvaluator:
                                                 self._ws.numel(), _native.stream_ptr(self.device), events)
         _native.check(rc, "lfg_stretch_step_shard_spec")
         self._spec_key = ens + (half, step, "pending")
+
+    def step_shard_fold(self, pos, lnp, half, a, seed, step, lo, q, zfac, lnp_new, verdict_prev, verdict, naccept,
+                        events=None):
+        """This rank's part of a sharded half-step with the acceptance
+        deferred (lfg_stretch_step_shard_fold): applies verdict_prev (the
+        other half's gathered verdicts of the half-step before, or None),
+        evaluates walkers lo .. lo + n - 1 of half `half` into q / zfac /
+        lnp_new and leaves their verdicts (ln_prob where accepted, NaN) in
+        verdict [n] for the exchange.  The speculative candidates are used
+        when the previous call on this evaluator was the preceding fold
+        half-step of the same ensemble."""
+        W, n = pos.shape[0], lnp_new.shape[0]
+        gen = self.generation
+        self._ensure(W // 2)
+        vp = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
+        ens = ("fold", W, pos.data_ptr(), lnp.data_ptr(), q.data_ptr(), zfac.data_ptr(), seed, float(a), lo, n,
+               pos._version, lnp._version)
+        spec_in = verdict_prev is not None and gen == self.generation and self._spec_key == ens + (half, step)
+        self._spec_key = None
+        rc = self.L.lfg_stretch_step_shard_fold(vp(pos), vp(lnp), W, half, a, seed, step, lo, n, vp(q), vp(zfac),
+                                                ctypes.byref(self.ctree), vp(verdict_prev), vp(verdict), vp(lnp_new),
+                                                vp(naccept), int(spec_in), 1, vp(self._ws), self._ws.numel(),
+                                                _native.stream_ptr(self.device), events)
+        _native.check(rc, "lfg_stretch_step_shard_fold")
+        self._spec_key = ens + (1 - half, step + half)
+
+    def apply_verdicts(self, pos, lnp, half, a, seed, step, verdict, naccept):
+        """Apply half `half`'s pending verdicts (the proposals of `step`) to
+        the ensemble (lfg_stretch_apply_verdicts): the flush of the deferred
+        acceptance.  The next fold half-step starts without candidates."""
+        W, ndim = pos.shape
+        self._spec_key = None
+        vp = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
+        rc = self.L.lfg_stretch_apply_verdicts(vp(pos), vp(lnp), W, ndim, half, a, seed, step, vp(verdict),
+                                               vp(naccept), _native.stream_ptr(self.device))
+        _native.check(rc, "lfg_stretch_apply_verdicts")
 
     def accept_regen(self, pos, lnp, half, a, seed, step, lnp_new, naccept, n):
         """Metropolis step of the whole half after the gather

@@ -185,6 +185,15 @@ struct SetupArgs {
     // began ([ns][ndim]; k_pair's speculative lanes, whose launch accepts
     // moves of that half while they read it)
     const double* ppos;
+    // deferred acceptance (k_pair<_, true>, lfg_stretch_step_shard_fold):
+    // this half's previous moves are accepted by the launch these lanes run
+    // in, so a row of this half is its snapshot fsnap [ns][ndim] (taken by
+    // the launch before) re-formed as the proposal of step fstep where the
+    // gathered verdict fv [ns] says accepted (not NaN).  fv nullptr: nothing
+    // pending, the rows are read from pos
+    const double* fv;
+    const double* fsnap;
+    unsigned long long fstep;
 };
 
 // where a lane reads walker w's parameters: the walker row, or the
@@ -197,11 +206,28 @@ struct Prop {
     double z;
     const double* ci;
     double zj;
+    // deferred acceptance (FOLD): s and ci are snapshot rows; where their
+    // pending move was accepted, the row is the proposal spp + sz (s - spp)
+    // (cpp, cz for ci), as k_apply_verdicts will write it
+    const double* spp;
+    double sz;
+    const double* cpp;
+    double cz;
 };
 
+// the stretch-move draw of walker i of half h at step t: z and the partner
+__device__ __forceinline__ int stretch_draw(const SetupArgs& A, unsigned long long t, int h, int i, double& z)
+{
+    const uint4 r = draw(A.seed, t, h, 0, i);
+    const double zr = (A.a - 1.0) * u53(r.x, r.y) + 1.0;
+    z = zr * zr / A.a;
+    return int(__umulhi(r.z, unsigned(A.ns)));
+}
+
+template <bool FOLD = false>
 __device__ inline Prop make_prop(const SetupArgs& A, int w)
 {
-    if (!A.pos) return Prop{A.walkers + size_t(w) * A.ndim, nullptr, 0.0, nullptr, 0.0};
+    if (!A.pos) return Prop{A.walkers + size_t(w) * A.ndim, nullptr, 0.0, nullptr, 0.0, nullptr, 0.0, nullptr, 0.0};
     const int ns = A.ns, i = A.lo + w;  // walker i of the half, as k_propose's lane i
     const uint4 r = draw(A.seed, A.step, A.half, 0, i);
     const double u = u53(r.x, r.y);
@@ -210,7 +236,12 @@ __device__ inline Prop make_prop(const SetupArgs& A, int w)
     if (A.jkout && A.cand == 0) A.jkout[w] = j;
     Prop P{A.pos + size_t(A.half * ns + i) * A.ndim,
            A.ppos ? A.ppos + size_t(j) * A.ndim : A.pos + size_t((1 - A.half) * ns + j) * A.ndim, zr * zr / A.a,
-           nullptr, 0.0};
+           nullptr, 0.0, nullptr, 0.0, nullptr, 0.0};
+    const double* other = A.pos + size_t(1 - A.half) * ns * A.ndim;  // the partner half's rows (FOLD: final)
+    if (FOLD && A.fv) {  // this half's rows as the pending verdicts leave them
+        P.s = A.fsnap + size_t(i) * A.ndim;
+        if (!isnan(A.fv[i])) P.spp = other + size_t(stretch_draw(A, A.fstep, A.half, i, P.sz)) * A.ndim;
+    }
     if (A.cand) {  // partner j's proposal in the other half (step_prev), as its own make_prop forms it
         const int hp = 1 - A.half;
         const uint4 rj = draw(A.seed, A.step_prev, hp, 0, j);
@@ -218,6 +249,10 @@ __device__ inline Prop make_prop(const SetupArgs& A, int w)
         const int ij = int(__umulhi(rj.z, unsigned(ns)));
         P.ci = A.pos + size_t(A.half * ns + ij) * A.ndim;
         P.zj = zrj * zrj / A.a;
+        if (FOLD && A.fv) {
+            P.ci = A.fsnap + size_t(ij) * A.ndim;
+            if (!isnan(A.fv[ij])) P.cpp = other + size_t(stretch_draw(A, A.fstep, A.half, ij, P.cz)) * A.ndim;
+        }
     }
     return P;
 }
@@ -241,12 +276,25 @@ __device__ __forceinline__ int npars_of(const SetupArgs& A, int e)
     return A.npars ? A.npars[e] : P;
 }
 
+template <bool FOLD = false>
 __device__ __forceinline__ double gather_par(const SetupArgs& A, const Prop& P, int g)
 {
     if (g < 0) return A.consts[-1 - g];
     if (!P.cj) return P.s[g];
-    const double cj = P.ci ? fma(P.cj[g] - P.ci[g], P.zj, P.ci[g]) : P.cj[g];
-    return fma(P.s[g] - cj, P.z, cj);
+    if (!FOLD) {
+        const double cj = P.ci ? fma(P.cj[g] - P.ci[g], P.zj, P.ci[g]) : P.cj[g];
+        return fma(P.s[g] - cj, P.z, cj);
+    }
+    // FOLD: an accepted pending move re-formed exactly as k_apply_verdicts
+    // (k_accept_regen) writes it: fma(old - partner, z, partner)
+    double s = P.s[g], cj = P.cj[g];
+    if (P.spp) s = fma(s - P.spp[g], P.sz, P.spp[g]);
+    if (P.ci) {
+        double ci = P.ci[g];
+        if (P.cpp) ci = fma(ci - P.cpp[g], P.cz, P.cpp[g]);
+        cj = fma(cj - ci, P.zj, ci);
+    }
+    return fma(s - cj, P.z, cj);
 }
 
 // Diagnostic build only (-DLFG_PROFILE_SETUP): s_memtime cycle counts of the
@@ -272,17 +320,18 @@ __device__ unsigned long long g_setup_cyc[11][4096];
 // Needs only q, rdisc, az, exp1 and exp2, so these lanes run beside the setup
 // lanes of the same launch; the stream status goes to bstatus and is folded
 // into the pair status by k_elements.
+template <bool FOLD = false>
 __device__ inline void bspot_lane(const SetupArgs& A, int t)
 {
     LFG_T0(tl);
     const int w = t / A.E, e = t - w * A.E;
-    const Prop P = make_prop(A, w);
+    const Prop P = make_prop<FOLD>(A, w);
     const int np = npars_of(A, e);
-    const double q = gather_par(A, P, gat_at(A, e * 18 + 4));
-    const double rdisc = gather_par(A, P, gat_at(A, e * 18 + 6));
-    const double az = gather_par(A, P, gat_at(A, e * 18 + 10));
-    const double a1 = (np == 18) ? gather_par(A, P, gat_at(A, e * 18 + 14)) : 2.0;  // MODEL_SPEC 5.3 simple: 2, 1
-    const double a2 = (np == 18) ? gather_par(A, P, gat_at(A, e * 18 + 15)) : 1.0;
+    const double q = gather_par<FOLD>(A, P, gat_at(A, e * 18 + 4));
+    const double rdisc = gather_par<FOLD>(A, P, gat_at(A, e * 18 + 6));
+    const double az = gather_par<FOLD>(A, P, gat_at(A, e * 18 + 10));
+    const double a1 = (np == 18) ? gather_par<FOLD>(A, P, gat_at(A, e * 18 + 14)) : 2.0;  // MODEL_SPEC 5.3 simple: 2, 1
+    const double a2 = (np == 18) ? gather_par<FOLD>(A, P, gat_at(A, e * 18 + 15)) : 1.0;
     double* G = A.geo + size_t(t) * LFG_NGEO;
 #ifdef LFG_PROFILE_SETUP
     unsigned long long tb = tl;
@@ -324,19 +373,20 @@ __device__ inline void bspot_lane(const SetupArgs& A, int t)
 // per-walker lane: LCModel.ln_prior dphi check (CVModel.py:452-473) and
 // Node.ln_prior over the variable parameters (model.py:439-449); with the
 // fused stretch move it also stores the proposal
+template <bool FOLD = false>
 __device__ inline void prior_lane(const SetupArgs& A, int w)
 {
     LFG_T0(tl);
 #ifdef LFG_PROFILE_SETUP
     unsigned long long trl = __builtin_amdgcn_s_memrealtime(), tr = tl;  // 100 MHz: calibrates s_memtime
 #endif
-    const Prop P = make_prop(A, w);
+    const Prop P = make_prop<FOLD>(A, w);
     double lp = 0.0;
     if (A.roche_priors) {
         // LCModel.ln_prior: dphi <= findphi(q, 90) - 1e-6, findphi from the
         // q series of the stream table (~1e-16; the solver outside its range)
-        const double q = gather_par(A, P, gat_at(A, 4));
-        const double dphi = gather_par(A, P, gat_at(A, 5));
+        const double q = gather_par<FOLD>(A, P, gat_at(A, 4));
+        const double dphi = gather_par<FOLD>(A, P, gat_at(A, 5));
         const QPatch qp = q_patch(q);
         double maxphi;
         if (qp.iq >= 0) {
@@ -356,7 +406,7 @@ __device__ inline void prior_lane(const SetupArgs& A, int w)
     for (int d0 = 0; d0 < A.ndim; d0 += PCH) {
         double v[PCH];
 #pragma unroll
-        for (int k = 0; k < PCH; ++k) v[k] = (d0 + k < A.ndim) ? gather_par(A, P, d0 + k) : 0.0;
+        for (int k = 0; k < PCH; ++k) v[k] = (d0 + k < A.ndim) ? gather_par<FOLD>(A, P, d0 + k) : 0.0;
         if (qo) {  // store the proposal: k_lnlike copies an accepted one into pos
 #pragma unroll
             for (int k = 0; k < PCH; ++k)
@@ -411,29 +461,30 @@ __device__ inline void prior_lane(const SetupArgs& A, int w)
 
 // one lane of k_setup: t < npairs setup lanes, then W prior lanes, then
 // npairs stream lanes
+template <bool FOLD = false>
 __device__ __forceinline__ void setup_any(const SetupArgs& A, int t)
 {
     const int npairs = A.W * A.E;
     if (t >= 2 * npairs + A.W) return;
     if (t >= npairs + A.W) {  // stream lanes (own waves: npairs + W is a multiple of 64 in the bench)
-        bspot_lane(A, t - npairs - A.W);
+        bspot_lane<FOLD>(A, t - npairs - A.W);
         return;
     }
     if (t >= npairs) {
-        prior_lane(A, t - npairs);
+        prior_lane<FOLD>(A, t - npairs);
         return;
     }
 
     // setup lane: one per (walker, eclipse)
     LFG_T0(tl);
     const int w = t / A.E, e = t - (t / A.E) * A.E;
-    const Prop P = make_prop(A, w);
+    const Prop P = make_prop<FOLD>(A, w);
     const int np = npars_of(A, e);
     double p[18];
     bool finite = (np == 14 || np == 18);
 #pragma unroll  // p[] stays in registers (a rolled loop kept it in scratch)
     for (int k = 0; k < 18; ++k) {
-        p[k] = (k < np) ? gather_par(A, P, gat_at(A, e * 18 + k)) : 0.0;
+        p[k] = (k < np) ? gather_par<FOLD>(A, P, gat_at(A, e * 18 + k)) : 0.0;
         finite = finite && isfinite(p[k]);
     }
     if (np == 14) { p[14] = 2.0; p[15] = 1.0; p[16] = 90.0; p[17] = 0.0; }  // MODEL_SPEC 5.3
@@ -511,8 +562,8 @@ __device__ __forceinline__ void setup_any(const SetupArgs& A, int t)
         // this lane, whose registers the speculative copies inside
         // k_elements share)
         const int* gg = A.gp_gather + e * 3;
-        const double ain = exp(gather_par(A, P, gg[0])), aout = exp(gather_par(A, P, gg[1]));
-        const double tau = exp(gather_par(A, P, gg[2]));
+        const double ain = exp(gather_par<FOLD>(A, P, gg[0])), aout = exp(gather_par<FOLD>(A, P, gg[1]));
+        const double tau = exp(gather_par<FOLD>(A, P, gg[2]));
         const double* B = A.gp_base + e * 4;
         const double q = R.q, rwd = p[8];
         const bool pend = fabs(B[1] - dphi) / dphi > 1.2 || fabs(B[0] - q) / q > 1.2 || fabs(B[2] - rwd) / rwd > 1.2;
@@ -2578,6 +2629,20 @@ struct PairArgs {
     unsigned long long jseed, jstep;
     int jhalf, jlo, jns;
     int prio;  // every workgroup resident at once (PAIR_PRIO)
+    // FOLD (lfg_stretch_step_shard_fold): the partner half's moves of the
+    // half-step before are accepted here, from the verdicts every rank
+    // gathered (fv [jns]: ln_prob where accepted, NaN where not; nullptr:
+    // nothing pending), each workgroup taking rows w, w + nwk, ...; the pair's
+    // candidate is chosen by the same verdicts, and the launch leaves its own
+    // verdicts in vout [npairs] (the next exchange's payload)
+    const double* fv = nullptr;
+    double* vout = nullptr;
+    double* fpos = nullptr;   // the ensemble [W][ndim], ln_prob [W], counters [W]
+    double* flnp = nullptr;
+    int* fnacc = nullptr;
+    double* fsnap = nullptr;  // [jns][ndim]: this half's rows, for the next launch's speculative lanes
+    unsigned long long fstep = 0;  // the step of the pending moves' proposals
+    double fa = 2.0;               // the stretch scale a
 };
 
 // the chunks of k_pair's element jobs 1..15, longest first (spot, outer
@@ -2812,7 +2877,7 @@ __device__ __forceinline__ void pair_cells(int* cell, int p, int m, double vprev
 // point's e^{-lam dx} and changepoint block go to the workspace for
 // k_gp_like, and a walker that tripped the changepoint cache rule has its
 // distance solved here (k_gp_dcp's ten limb points, on wave 0's lanes 32..)
-template <bool GP>
+template <bool GP, bool FOLD = false>
 __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
 {
     const LikeArgs& L = A.L;
@@ -2902,7 +2967,10 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
         const double rp0 = G0[G_RPRIOR] + G0[G_RPRIOR_BS], rp1 = G1[G_RPRIOR] + G1[G_RPRIOR_BS];
         const double ph0 = G0[G_PHI0], ph1 = G1[G_PHI0];
         const int jw = int(__umulhi(draw(A.jseed, A.jstep, A.jhalf, 0, A.jlo + w).z, unsigned(A.jns)));
-        cand = __builtin_amdgcn_readfirstlane(X.accflag[__builtin_amdgcn_readfirstlane(jw)]);
+        if (FOLD)  // the partner's pending verdict: accepted unless NaN
+            cand = __builtin_amdgcn_readfirstlane(int(!isnan(A.fv[__builtin_amdgcn_readfirstlane(jw)])));
+        else
+            cand = __builtin_amdgcn_readfirstlane(X.accflag[__builtin_amdgcn_readfirstlane(jw)]);
         PAIR_STAMP(10, tid == 0 && cand >= 0);
         G = cand ? G1 : G0;
         st0 = cand ? sa1 : sa0;
@@ -3005,6 +3073,40 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
         if (l == 51) const_cast<int*>(L.status)[pair] = stp;
         if (A.snap_dst && e == 0)
             for (int d = l; d < L.ndim; d += 64) A.snap_dst[size_t(w) * L.ndim + d] = A.snap_src[size_t(w) * L.ndim + d];
+        if (FOLD) {
+            // rows w, w + nwk, ... of each half: the snapshot of this half's
+            // (final in this launch) and the pending verdicts of the partner
+            // half's, an accepted row becoming its proposal (k_accept_regen's
+            // arithmetic); the verdict's draw, zf and old ln_prob prefetched
+            const int ns = A.jns, h = L.half, hp = 1 - h, nd = L.ndim, r = (ns + nwk - 1) / nwk;
+            for (int f = l; f < r * nd; f += 64) {
+                const int k = f / nd, d = f - k * nd, j = w + k * nwk;
+                if (j < ns) A.fsnap[size_t(j) * nd + d] = A.fpos[(size_t(h) * ns + j) * nd + d];
+            }
+            if (A.fv) {
+                for (int f = l; f < r * nd; f += 64) {
+                    const int k = f / nd, d = f - k * nd, j = w + k * nwk;
+                    if (j >= ns) continue;
+                    const double v = A.fv[j];
+                    if (isnan(v)) continue;
+                    const uint4 rr = draw(L.seed, A.fstep, hp, 0, j);
+                    const double zr = (A.fa - 1.0) * u53(rr.x, rr.y) + 1.0, z = zr * zr / A.fa;
+                    const double* cj = A.fpos + (size_t(h) * ns + int(__umulhi(rr.z, unsigned(ns)))) * nd;
+                    double* row = A.fpos + (size_t(hp) * ns + j) * nd;
+                    row[d] = fma(row[d] - cj[d], z, cj[d]);
+                    if (d == 0) {
+                        A.flnp[size_t(hp) * ns + j] = v;
+                        if (A.fnacc) A.fnacc[size_t(hp) * ns + j] += 1;
+                    }
+                }
+            }
+            if (l == 63) {
+                const uint4 r1 = draw(L.seed, L.step, h, 1, A.jlo + w);
+                sacc1[0] = log(u53(r1.x, r1.y));
+                sacc1[1] = X.jk ? X.zfC[size_t(cand) * nwk + w] : L.zfac[w];
+                sacc1[2] = A.flnp[size_t(h) * ns + A.jlo + w];
+            }
+        }
         if (acc1) {
             const double* qsrc = X.jk ? X.qC + (size_t(cand) * nwk + w) * X.ndim : L.qprop + size_t(w) * L.ndim;
             for (int d = l; d < L.ndim && d < ACC_LDS; d += 64) sq[d] = qsrc[d];
@@ -3032,7 +3134,7 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
             // candidate uniform per block: X.S[c] stays in scalar registers
             const int c = pair < A.nbc ? 0 : 1;
             const int t = (pair - c * A.nbc) * A.spl + lane;
-            if (t < X.nspec) setup_any(X.S[__builtin_amdgcn_readfirstlane(c)], t);
+            if (t < X.nspec) setup_any<FOLD>(X.S[__builtin_amdgcn_readfirstlane(c)], t);
 #ifdef LFG_PROFILE_PAIR
             if (lane == 0 && blockIdx.x < 4096) {
                 const int np = X.S[0].W * X.S[0].E;
@@ -3135,6 +3237,15 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
 
     if (st != ST_OK) {
         if (GP) return;  // k_gp_like sees the status (or the prior) and finishes the pair
+        if (FOLD) {  // ln_prob -inf (combine_walker's value): rejected unless the old one is -inf too
+            if (tid == 0) {
+                L.lle[pair] = -INFINITY;
+                if (L.lnp) L.lnp[pair] = -INFINITY;
+                const double v = -INFINITY;
+                A.vout[pair] = (sacc1[0] < sacc1[1] + v - sacc1[2]) ? v : NAN;
+            }
+            return;
+        }
         if (tid == 0) L.lle[pair] = -INFINITY;
         finish_walker(L, pair, tid, acc1, sq, sacc1, sflag);
         return;
@@ -3205,7 +3316,11 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
         const double lle = isfinite(lp) ? -0.5 * tot : -INFINITY;
         L.lle[pair] = lle;
         PAIR_STAMP(13, true);
-        if (!acc1) {
+        if (FOLD) {  // this pair's verdict for the exchange (k_accept_regen's test)
+            const double v = isfinite(lp) ? lp + lle : -INFINITY;
+            if (L.lnp) L.lnp[pair] = v;
+            A.vout[pair] = (sacc1[0] < sacc1[1] + v - sacc1[2]) ? v : NAN;
+        } else if (!acc1) {
             combine_after(L, pair);
         } else {
             const int wg = L.half * L.npairs + pair;
@@ -3799,6 +3914,52 @@ __global__ __launch_bounds__(64 * REGEN_WAVES) void k_accept_regen(double* __res
     if (accflag && lane == 0) accflag[i] = acc ? 1 : 0;  // the speculative setup's candidate choice
 }
 
+// the deferred acceptance's two halves outside k_pair<_, true>:
+//  k_apply_verdicts: half `half`'s gathered verdicts (ln_prob where the move
+//  was accepted, NaN where not) applied to the ensemble, the proposal
+//  re-formed from its draws as k_accept_regen does (the flush at a chain's
+//  end, and the fold's fallback); one wave per walker
+//  k_verdict: a shard's verdicts from its ln_prob (k_accept_regen's test)
+__global__ __launch_bounds__(64 * REGEN_WAVES) void k_apply_verdicts(double* __restrict__ pos, double* __restrict__ lnp,
+                                                                      int W, int ndim, int half, double a,
+                                                                      const double* __restrict__ verdict,
+                                                                      unsigned long long seed, unsigned long long step,
+                                                                      int* __restrict__ naccept, int* __restrict__ accflag)
+{
+    const int i = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * REGEN_WAVES + int(threadIdx.x >> 6));
+    const int lane = threadIdx.x & 63;
+    const int ns = W / 2;
+    if (i >= ns) return;
+    const double v = verdict[i];
+    const bool acc = !isnan(v);
+    if (acc) {
+        const int w = half * ns + i;
+        const uint4 r0 = draw(seed, step, half, 0, i);
+        const double zr = (a - 1.0) * u53(r0.x, r0.y) + 1.0;
+        const double z = zr * zr / a;
+        const int j = int(__umulhi(r0.z, unsigned(ns)));
+        double* p = pos + size_t(w) * ndim;
+        const double* cj = pos + size_t((1 - half) * ns + j) * ndim;
+        for (int d = lane; d < ndim; d += 64) p[d] = fma(p[d] - cj[d], z, cj[d]);
+        if (lane == 0) {
+            lnp[w] = v;
+            if (naccept) naccept[w] += 1;
+        }
+    }
+    if (accflag && lane == 0) accflag[i] = acc ? 1 : 0;
+}
+
+__global__ void k_verdict(const double* __restrict__ lnp_new, const double* __restrict__ lnp,
+                          const double* __restrict__ zfac, int n, int lo, int ns, int half, unsigned long long seed,
+                          unsigned long long step, double* __restrict__ vout)
+{
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const uint4 r = draw(seed, step, half, 1, lo + k);
+    const double v = lnp_new[k];
+    vout[k] = (log(u53(r.x, r.y)) < zfac[k] + v - lnp[size_t(half) * ns + lo + k]) ? v : NAN;
+}
+
 // ------------------------------------------------------ k_gp, k_wdphases
 __device__ __forceinline__ double readlane_f64(double v, int j)
 {
@@ -4049,15 +4210,51 @@ struct SpecCtl {  // lfg_stretch_step_half_spec
     bool out;  // form the next half's candidates inside this k_elements
 };
 
+struct FoldCtl {  // lfg_stretch_step_shard_fold: deferred acceptance
+    const double* fv;  // [ns] the partner half's pending verdicts (nullptr: none)
+    double* vout;      // [n] this shard's verdicts
+    double* pos;       // the ensemble the verdicts apply to
+    double* lnp;
+    int* naccept;
+};
+
+static int apply_verdicts(double* pos, double* lnp, int W, int ndim, int half, double a, const double* verdict,
+                          unsigned long long seed, unsigned long long step, int* naccept, int* accflag,
+                          hipStream_t st)
+{
+    const int ns = W / 2;
+    hipLaunchKernelGGL(k_apply_verdicts, dim3((ns + REGEN_WAVES - 1) / REGEN_WAVES), dim3(64 * REGEN_WAVES), 0, st,
+                       pos, lnp, W, ndim, half, a, verdict, seed, step, naccept, accflag);
+    return launch_ok();
+}
+
 static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* lnp, double* lnlike_e, void* wsp,
                        size_t ws_bytes, void* stream, void* const* ev, const Accept* acc = nullptr,
-                       const Propose* prop = nullptr, const SpecCtl* sp = nullptr)
+                       const Propose* prop = nullptr, const SpecCtl* sp = nullptr, const FoldCtl* fold = nullptr)
 {
     if (W <= 0 || !T || T->E <= 0 || T->ndim <= 0 || T->nsub < 1 || !walkers || (!lnp && !acc)) return LFG_E_ARGS;
     if (sp && (!prop || (acc && (prop->lo != 0 || prop->ns != W)))) return LFG_E_ARGS;
+    if (fold && (!sp || !prop || acc || !lnp || !fold->vout || !fold->pos || !fold->lnp || (sp->in && !fold->fv)))
+        return LFG_E_ARGS;
     Ws ws = carve(wsp, W, T->E, T->gp ? T->max_n : 0, sp ? T->ndim : 0, prop ? prop->ns : 0);
     if (!wsp || ws_bytes < ws.total) return LFG_E_WORKSPACE;
     hipStream_t st = static_cast<hipStream_t>(stream);
+    // the deferred acceptance runs inside k_pair for one-eclipse chi^2 trees
+    // on the k_pair layout; otherwise (and when no candidates are in the
+    // workspace: k_setup reads the rows directly) the pending verdicts are
+    // applied first, recording the acceptances for the candidate choice, and
+    // the shard's verdicts are formed after its ln_prob (k_verdict)
+    const double* fv = fold ? fold->fv : nullptr;
+    const bool fold_pair = fold && T->E == 1 && !T->gp && pair_ok(T->gp, T->nsub, T->max_n, T->ndim) &&
+                           (!sp->out || 2 * ((2 * W + W + 63) / 64) <= W);
+    const unsigned long long fstep = prop && prop->half == 0 ? prop->step - 1 : (prop ? prop->step : 0);
+    if (fv && (!fold_pair || !sp->in)) {
+        const int rc = apply_verdicts(fold->pos, fold->lnp, 2 * prop->ns, T->ndim, 1 - prop->half, prop->a, fv,
+                                      prop->seed, fstep, fold->naccept,
+                                      ws.accflag + size_t(1 - prop->half) * ws.accstride, st);
+        if (rc) return rc;
+        fv = nullptr;
+    }
     auto mark = [&](int i) {
         if (ev && ev[i]) (void)hipEventRecord(static_cast<hipEvent_t>(ev[i]), st);
     };
@@ -4115,6 +4312,11 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
                 N.qout = ws.qC + k * size_t(W) * T->ndim;
                 N.zfout = ws.zfC + k * W;
                 N.jkout = ws.jk + size_t(hn) * W;
+                if (fold_pair && fv) {  // the next half's rows as the pending verdicts leave them
+                    N.fv = fv;
+                    N.fsnap = ws.snap + size_t(hn) * ws.accstride * T->ndim;
+                    N.fstep = N.step - 1;
+                }
             }
             X.nspec = 2 * npairs + W;
             X.nspecblk = (2 * ((X.nspec + ELEM_BLOCK - 1) / ELEM_BLOCK) + 7) / 8 * 8;  // keeps the pair -> XCD map
@@ -4126,6 +4328,18 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
     // [0, 2 nbc), nbc blocks per candidate, so there must be 2 nbc pairs
     const int spl = 64, nbc = (X.nspec + 63) / 64;
     const bool pair_path = pair_ok(T->gp, T->nsub, T->max_n, T->ndim) && (X.nspec == 0 || 2 * nbc <= npairs);
+    if (fold_pair && !pair_path) return LFG_E_ARGS;  // (fold_pair's test is pair_path's)
+    // the end of every path but the fold's own: the shard's verdicts from its
+    // ln_prob (fold fallback), then the last event
+    auto finish = [&]() {
+        if (fold) {
+            hipLaunchKernelGGL(k_verdict, dim3((W + 63) / 64), dim3(64), 0, st, lnp, fold->lnp, prop->zfac, W,
+                               prop->lo, prop->ns, prop->half, prop->seed, prop->step, fold->vout);
+            if (launch_ok()) return LFG_E_LAUNCH;
+        }
+        mark(3);
+        return LFG_OK;
+    };
     int rc = run_front(S, ws, st, ev, !pair_path, &X, !(sp && sp->in));
     if (rc) return rc;
     double* lle = lnlike_e ? lnlike_e : ws.lle;
@@ -4146,6 +4360,25 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
             A.jhalf = prop->half;
             A.jlo = prop->lo;
             A.jns = prop->ns;
+        }
+        if (fold_pair) {
+            const int h = prop->half;
+            A.fv = fv;
+            A.vout = fold->vout;
+            A.fpos = fold->pos;
+            A.flnp = fold->lnp;
+            A.fnacc = fold->naccept;
+            A.fsnap = ws.snap + size_t(h) * ws.accstride * T->ndim;
+            A.fstep = fstep;
+            A.fa = prop->a;
+            A.L.seed = prop->seed;
+            A.L.step = prop->step;
+            A.L.half = h;
+            A.L.zfac = prop->zfac;
+            hipLaunchKernelGGL((k_pair<false, true>), dim3(npairs), dim3(LIKE_THREADS), 0, st, A);
+            if ((rc = launch_ok())) return rc;
+            mark(3);
+            return LFG_OK;
         }
         if (sp && sp->out && acc && T->E == 1) {
             // this launch accepts moves of half h while its speculative lanes
@@ -4177,8 +4410,7 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
             hipLaunchKernelGGL(k_combine_walkers, dim3((W + 3) / 4), dim3(256), 0, st, L);
             if ((rc = launch_ok())) return rc;
         }
-        mark(3);
-        return LFG_OK;
+        return finish();
     }
     if (sp && sp->out && acc && T->E == 1 && pair_fits(T->nsub, T->max_n, T->ndim)) {
         // a k_pair-eligible tree on the two-kernel layout (lfg_set_layout(0)):
@@ -4210,8 +4442,7 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
         hipLaunchKernelGGL(k_combine_walkers, dim3((W + 3) / 4), dim3(256), 0, st, L);
         if ((rc = launch_ok())) return rc;
     }
-    mark(3);
-    return LFG_OK;
+    return finish();
 }
 
 int lfg_lnprior(const double* walkers, int W, const lfg_tree* T, double* lnprior, void* wsp, size_t ws_bytes,
@@ -4294,6 +4525,30 @@ int lfg_stretch_step_shard_spec(const double* pos, int W, int half, double a, un
     const Propose prop{pos, a, q, zfac, half, seed, step, lo, W / 2};
     const SpecCtl sp{spec_in != 0, spec_out != 0};
     return lnprob_impl(q, n, T, lnp_new, nullptr, wsp, ws_bytes, stream, ev, nullptr, &prop, &sp);
+}
+
+int lfg_stretch_step_shard_fold(double* pos, double* lnp, int W, int half, double a, unsigned long long seed,
+                                unsigned long long step, int lo, int n, double* q, double* zfac, const lfg_tree* T,
+                                const double* verdict_prev, double* verdict, double* lnp_new, int* naccept,
+                                int spec_in, int spec_out, void* wsp, size_t ws_bytes, void* stream, void* const* ev)
+{
+    if (W < 4 || (W & 1) || (half != 0 && half != 1) || !(a > 1.0) || !pos || !lnp || !q || !zfac || !T ||
+        !lnp_new || !verdict || n <= 0 || lo < 0 || lo + n > W / 2 || (spec_in && !verdict_prev) ||
+        (verdict_prev && half == 0 && step == 0))
+        return LFG_E_ARGS;
+    const Propose prop{pos, a, q, zfac, half, seed, step, lo, W / 2};
+    const SpecCtl sp{spec_in != 0, spec_out != 0};
+    const FoldCtl fold{verdict_prev, verdict, pos, lnp, naccept};
+    return lnprob_impl(q, n, T, lnp_new, nullptr, wsp, ws_bytes, stream, ev, nullptr, &prop, &sp, &fold);
+}
+
+int lfg_stretch_apply_verdicts(double* pos, double* lnp, int W, int ndim, int half, double a, unsigned long long seed,
+                               unsigned long long step, const double* verdict, int* naccept, void* stream)
+{
+    if (W < 4 || (W & 1) || ndim <= 0 || (half != 0 && half != 1) || !(a > 1.0) || !pos || !lnp || !verdict)
+        return LFG_E_ARGS;
+    return apply_verdicts(pos, lnp, W, ndim, half, a, verdict, seed, step, naccept, nullptr,
+                          static_cast<hipStream_t>(stream));
 }
 
 int lfg_stretch_lnprob_accept(double* pos, double* lnp, int W, int half, const double* q, const double* zfac,

@@ -113,12 +113,12 @@ class EnsembleSampler:
             raise ValueError("W/2 = %d walkers per half must divide over %d ranks" % (ns, self.world))
         self.shard = ns // self.world
         f64 = dict(dtype=torch.float64, device=self.dev)
-        self.pos = torch.empty((self.W, self.ndim), **f64)
-        self.lnp = torch.empty(self.W, **f64)
+        self._pos = torch.empty((self.W, self.ndim), **f64)
+        self._lnp = torch.empty(self.W, **f64)
         self.q = torch.empty((ns, self.ndim), **f64)
         self.zfac = torch.empty(ns, **f64)
         self.lnp_new = torch.empty(ns, **f64)
-        self.naccept = torch.zeros(self.W, dtype=torch.int32, device=self.dev)
+        self._naccept = torch.zeros(self.W, dtype=torch.int32, device=self.dev)
         self.iteration = 0   # emcee's counter: reset() clears it (acceptance fractions)
         # Philox step counter of every draw: monotone over the sampler's life,
         # so the production run after reset() never replays burn-in draws
@@ -153,6 +153,17 @@ class EnsembleSampler:
         self.force_exchange = False  # one rank: still exchange through the collective (rehearsal)
         self.shard_timer = None
         self._q_sh = self._zf_sh = self._lnp_sh = None
+        # deferred acceptance on the sharded path (lfg_stretch_step_shard_fold):
+        # each half-step is ONE launch + the exchange; the launch applies the
+        # other half's gathered verdicts of the half-step before.  _V: the
+        # gathered verdicts per half (ln_prob where accepted, NaN); _pending:
+        # (half, step) of verdicts not yet applied; _store_next: a chain record
+        # of the step before, taken once its last verdicts are applied
+        self.fold = os.environ.get("LFG_FOLD", "1") != "0"
+        self._V = None
+        self._v_sh = None
+        self._pending = None
+        self._store_next = None
         self._emu = None   # (rank, nranks) of emulate_rank()
         self._rccl = None  # direct RCCL all-gather (built at the first nccl exchange)
         # HIP-graph replay of whole iterations (single rank, HIP ops): the first
@@ -196,16 +207,55 @@ class EnsembleSampler:
     def _eval(self, x, out):
         return (self.timer or self.ev)(x, out=out)
 
+    # the ensemble, brought up to date first: with the deferred acceptance the
+    # last half-step's moves are applied by the next launch, or here
+    @property
+    def pos(self):
+        self.sync()
+        return self._pos
+
+    @property
+    def lnp(self):
+        self.sync()
+        return self._lnp
+
+    @property
+    def naccept(self):
+        self.sync()
+        return self._naccept
+
+    def _flush(self):
+        if self._pending is not None:
+            half, step = self._pending
+            self._pending = None
+            self.ev.apply_verdicts(self._pos, self._lnp, half, self.a, self.seed, step, self._V[half],
+                                   self._naccept)
+
+    def sync(self):
+        """Apply pending verdicts (lfg_stretch_apply_verdicts) and take a
+        deferred chain record: afterwards pos / lnp / naccept are the state
+        after the last step, as on the other paths."""
+        self._flush()
+        if self._store_next is not None:
+            rec, self._store_next = self._store_next, None
+            self._store(*rec)
+
+    def _fold_ok(self):
+        return (self.fold and self.spec and hasattr(self.ev, "step_shard_fold") and
+                (self.shard_timer is None or getattr(self.shard_timer, "takes_fold", False)))
+
     def set_state(self, p0, lnp0=None):
         import torch
         if hasattr(self.ev, "invalidate_spec"):
             self.ev.invalidate_spec()  # the candidates were formed from the old positions
-        self.pos.copy_(torch.as_tensor(np.asarray(p0), dtype=torch.float64))
+        self._pending = None   # verdicts of the old state are void
+        self._store_next = None
+        self._pos.copy_(torch.as_tensor(np.asarray(p0), dtype=torch.float64))
         if lnp0 is None:
-            self.lnp.copy_(self.ln_prob(self.pos))
+            self._lnp.copy_(self.ln_prob(self._pos))
         else:
-            self.lnp.copy_(torch.as_tensor(np.asarray(lnp0), dtype=torch.float64))
-        self.naccept.zero_()
+            self._lnp.copy_(torch.as_tensor(np.asarray(lnp0), dtype=torch.float64))
+        self._naccept.zero_()
 
     def ln_prob(self, x):
         """ln_prob of walkers x [n, ndim], sharded over ranks when n divides."""
@@ -227,10 +277,10 @@ class EnsembleSampler:
 
     def _graph_body(self, ev):
         for half in (0, 1):
-            self.ops.propose_dev(self.pos, half, self.a, self.seed, self._step_dev, self.q, self.zfac)
+            self.ops.propose_dev(self._pos, half, self.a, self.seed, self._step_dev, self.q, self.zfac)
             ev(self.q, out=self.lnp_new)
-            self.ops.accept_dev(self.pos, self.lnp, half, self.q, self.zfac, self.lnp_new, self.seed,
-                                self._step_dev, self.naccept)
+            self.ops.accept_dev(self._pos, self._lnp, half, self.q, self.zfac, self.lnp_new, self.seed,
+                                self._step_dev, self._naccept)
         self._step_dev.add_(1)
 
     def _sync_step_dev(self):
@@ -275,6 +325,9 @@ class EnsembleSampler:
 
     def step(self):
         """One emcee iteration: both halves, in place."""
+        if self._pending is not None and not (
+                (self.world > 1 or self.force_shard) and self.fuse_shard and self.timer is None and self._fold_ok()):
+            self.sync()  # a path without the deferred acceptance follows
         if self._graphable() and self._warm:
             self._graph_step()
             return
@@ -285,21 +338,21 @@ class EnsembleSampler:
                 # a replacement step_half (bench timing, tests) takes spec only if it says so
                 kw = dict(spec=True) if self.spec and (self.half_timer is None or
                                                        getattr(self.half_timer, "takes_spec", False)) else {}
-                f(self.pos, self.lnp, half, self.a, self.seed, self.rng_step, self.q, self.zfac, self.naccept,
+                f(self._pos, self._lnp, half, self.a, self.seed, self.rng_step, self.q, self.zfac, self._naccept,
                   lnp_new=self.lnp_new, **kw)
                 continue
             if (self.world > 1 or self.force_shard) and self.fuse_shard and self.timer is None:
                 self._shard_half(half)
                 continue
-            self.ops.propose(self.pos, half, self.a, self.seed, self.rng_step, self.q, self.zfac)
+            self.ops.propose(self._pos, half, self.a, self.seed, self.rng_step, self.q, self.zfac)
             if self.world == 1:
                 self._eval(self.q, self.lnp_new)
             else:
                 lo = self.rank * self.shard
                 mine = self._eval(self.q[lo:lo + self.shard], None)
                 self._gather(self.lnp_new, mine)
-            self.ops.accept(self.pos, self.lnp, half, self.q, self.zfac, self.lnp_new, self.seed,
-                            self.rng_step, self.naccept)
+            self.ops.accept(self._pos, self._lnp, half, self.q, self.zfac, self.lnp_new, self.seed,
+                            self.rng_step, self._naccept)
         self.iteration += 1
         self.rng_step += 1
 
@@ -321,6 +374,8 @@ class EnsembleSampler:
         self._emu = (int(k), int(nranks))
         self._q_sh = self._zf_sh = self._lnp_sh = None
         self.lnp_new.fill_(float("-inf"))
+        self.sync()
+        self._V = self._v_sh = None
 
     def _shard_half(self, half):
         import torch
@@ -330,10 +385,14 @@ class EnsembleSampler:
             self._zf_sh = torch.empty(self.shard, **f64)
             self._lnp_sh = torch.empty(self.shard, **f64)
         lo = (self._emu[0] if self._emu else self.rank) * self.shard
+        if self._fold_ok():
+            self._fold_half(half, lo)
+            return
+        self._flush()
         f = self.shard_timer or self.ev.step_shard
         spec = self.spec and hasattr(self.ev, "accept_regen") and (
             self.shard_timer is None or getattr(self.shard_timer, "takes_spec", False))
-        f(self.pos, half, self.a, self.seed, self.rng_step, lo, self._q_sh, self._zf_sh,
+        f(self._pos, half, self.a, self.seed, self.rng_step, lo, self._q_sh, self._zf_sh,
           self._lnp_sh, **(dict(spec=True) if spec else {}))
         dst = self.lnp_new[lo:lo + self.shard] if self._emu else self.lnp_new
         if self.world > 1 or self.force_exchange:
@@ -341,11 +400,38 @@ class EnsembleSampler:
         else:
             dst.copy_(self._lnp_sh)
         if spec:  # records the acceptances for the next half's speculative setup
-            self.ev.accept_regen(self.pos, self.lnp, half, self.a, self.seed, self.rng_step, self.lnp_new,
-                                 self.naccept, self.shard)
+            self.ev.accept_regen(self._pos, self._lnp, half, self.a, self.seed, self.rng_step, self.lnp_new,
+                                 self._naccept, self.shard)
         else:
-            self.ops.accept_regen(self.pos, self.lnp, half, self.a, self.lnp_new, self.seed, self.rng_step,
-                                  self.naccept)
+            self.ops.accept_regen(self._pos, self._lnp, half, self.a, self.lnp_new, self.seed, self.rng_step,
+                                  self._naccept)
+
+    def _fold_half(self, half, lo):
+        import torch
+        if self._V is None:
+            f64 = dict(dtype=torch.float64, device=self.dev)
+            # NaN: no move accepted (the other shards' entries when emulating one rank)
+            self._V = [torch.full((self.W // 2,), float("nan"), **f64) for _ in range(2)]
+            self._v_sh = torch.empty(self.shard, **f64)
+        want = (1 - half, self.rng_step - 1 if half == 0 else self.rng_step)
+        if self._pending is not None and self._pending != want:
+            self._flush()   # not the half-step just before: apply on its own
+        vprev = self._V[1 - half] if self._pending is not None else None
+        f = self.shard_timer or self.ev.step_shard
+        f(self._pos, half, self.a, self.seed, self.rng_step, lo, self._q_sh, self._zf_sh, self._lnp_sh, spec=True,
+          fold=(self._lnp, vprev, self._v_sh, self._naccept))
+        self._pending = None
+        if half == 0 and self._store_next is not None:
+            # the launch applied the previous step's last verdicts and none of
+            # this step's yet: the ensemble is the previous step's state
+            rec, self._store_next = self._store_next, None
+            self._store(*rec)
+        dst = self._V[half][lo:lo + self.shard] if self._emu else self._V[half]
+        if self.world > 1 or self.force_exchange:
+            self._gather(dst, self._v_sh)
+        else:
+            dst.copy_(self._v_sh)
+        self._pending = (half, self.rng_step)
 
     def close(self):
         """Release the direct RCCL communicator (every rank, before the
@@ -387,10 +473,18 @@ class EnsembleSampler:
         self._last = host
         self._cat = None
 
+    def _record(self, buf, i, thin):
+        """the chain record of step i: at once, or (verdicts pending) when
+        the next step's first launch has applied them (sync() at the end)"""
+        if self._pending is not None and buf is not None and i % thin == 0:
+            self._store_next = (buf, i, thin)
+        else:
+            self._store(buf, i, thin)
+
     def _store(self, buf, i, thin):
         if buf is not None and i % thin == 0:
-            buf[0][i // thin].copy_(self.pos)
-            buf[1][i // thin].copy_(self.lnp)
+            buf[0][i // thin].copy_(self._pos)
+            buf[1][i // thin].copy_(self._lnp)
 
     def sample(self, p0=None, lnprob0=None, rstate0=None, blobs0=None, iterations=1, thin=1,
                storechain=True, store=None, skip_initial_state_check=False, **kwargs):
@@ -406,11 +500,12 @@ class EnsembleSampler:
         try:
             for i in range(int(iterations)):
                 self.step()
+                self.sync()
                 self._store(buf, i, thin)
                 if i == int(iterations) - 1:
                     self._end(buf)
                     buf = None
-                yield _host(self.pos), _host(self.lnp), self.random_state
+                yield _host(self._pos), _host(self._lnp), self.random_state
         finally:
             # a caller that leaves the generator early (break, GeneratorExit)
             # still gets the chunk offloaded
@@ -424,9 +519,10 @@ class EnsembleSampler:
         buf, thin = self._begin(pos0, lnprob0, rstate0, N, thin, storechain if store is None else store)
         for i in range(int(N)):
             self.step()
-            self._store(buf, i, thin)
+            self._record(buf, i, thin)
+        self.sync()
         self._end(buf)
-        return _host(self.pos), _host(self.lnp), self.random_state
+        return _host(self._pos), _host(self._lnp), self.random_state
 
     def _concat(self):
         """the stored chain as one (chain, lnprob) pair, wherever the chunks
@@ -495,17 +591,18 @@ class EnsembleSampler:
 
     @property
     def naccepted(self):
-        return self.naccept.cpu().numpy()
+        return self._naccept.cpu().numpy()
 
     @property
     def acceptance_fraction(self):
-        return (self.naccept.double() / max(self.iteration, 1)).cpu().numpy()
+        return (self._naccept.double() / max(self.iteration, 1)).cpu().numpy()
 
     def reset(self):
         """emcee's reset: clears the chain, the iteration count and the
         acceptance counters; the RNG stream carries on (rng_step is kept)."""
+        self.sync()
         self.iteration = 0
-        self.naccept.zero_()
+        self._naccept.zero_()
         self._chunks = []
         self._cat = None
         self._last = None
