@@ -3051,6 +3051,34 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
     // GP: the changepoint distance is solved in this launch (the cache rule
     // tripped, G_GP_OK = 2); wave 0 then owns the slot's G_GP_DCP / G_GP_OK
     const bool pend = GP && st == ST_OK && Gc[G_GP_OK] == 2.0;
+    // FOLD: rows w, w + nwk, ... of each half (wave 7's lanes): the snapshot
+    // of this half's (final in this launch) for the next launch's speculative
+    // lanes, and the pending verdicts of the partner half's, an accepted row
+    // becoming its proposal (k_accept_regen's arithmetic)
+    auto fold_rows = [&](int l) {
+        const int ns = A.jns, h = L.half, hp = 1 - h, nd = L.ndim, r = (ns + nwk - 1) / nwk;
+        for (int f = l; f < r * nd; f += 64) {
+            const int k = f / nd, d = f - k * nd, j = w + k * nwk;
+            if (j < ns) A.fsnap[size_t(j) * nd + d] = A.fpos[(size_t(h) * ns + j) * nd + d];
+        }
+        if (A.fv) {
+            for (int f = l; f < r * nd; f += 64) {
+                const int k = f / nd, d = f - k * nd, j = w + k * nwk;
+                if (j >= ns) continue;
+                const double v = A.fv[j];
+                const uint4 rr = draw(L.seed, A.fstep, hp, 0, j);
+                if (isnan(v)) continue;
+                const double zr = (A.fa - 1.0) * u53(rr.x, rr.y) + 1.0, z = zr * zr / A.fa;
+                const double* cj = A.fpos + (size_t(h) * ns + int(__umulhi(rr.z, unsigned(ns)))) * nd;
+                double* row = A.fpos + (size_t(hp) * ns + j) * nd;
+                row[d] = fma(row[d] - cj[d], z, cj[d]);
+                if (d == 0) {
+                    A.flnp[size_t(hp) * ns + j] = v;
+                    if (A.fnacc) A.fnacc[size_t(hp) * ns + j] += 1;
+                }
+            }
+        }
+    };
     if (wv == 7) {
         // housekeeping off the prologue's critical path: the selected candidate
         // into the standard slots (API readers, k_combine_walkers, k_gp_like),
@@ -3074,33 +3102,9 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
         if (A.snap_dst && e == 0)
             for (int d = l; d < L.ndim; d += 64) A.snap_dst[size_t(w) * L.ndim + d] = A.snap_src[size_t(w) * L.ndim + d];
         if (FOLD) {
-            // rows w, w + nwk, ... of each half: the snapshot of this half's
-            // (final in this launch) and the pending verdicts of the partner
-            // half's, an accepted row becoming its proposal (k_accept_regen's
-            // arithmetic); the verdict's draw, zf and old ln_prob prefetched
-            const int ns = A.jns, h = L.half, hp = 1 - h, nd = L.ndim, r = (ns + nwk - 1) / nwk;
-            for (int f = l; f < r * nd; f += 64) {
-                const int k = f / nd, d = f - k * nd, j = w + k * nwk;
-                if (j < ns) A.fsnap[size_t(j) * nd + d] = A.fpos[(size_t(h) * ns + j) * nd + d];
-            }
-            if (A.fv) {
-                for (int f = l; f < r * nd; f += 64) {
-                    const int k = f / nd, d = f - k * nd, j = w + k * nwk;
-                    if (j >= ns) continue;
-                    const double v = A.fv[j];
-                    if (isnan(v)) continue;
-                    const uint4 rr = draw(L.seed, A.fstep, hp, 0, j);
-                    const double zr = (A.fa - 1.0) * u53(rr.x, rr.y) + 1.0, z = zr * zr / A.fa;
-                    const double* cj = A.fpos + (size_t(h) * ns + int(__umulhi(rr.z, unsigned(ns)))) * nd;
-                    double* row = A.fpos + (size_t(hp) * ns + j) * nd;
-                    row[d] = fma(row[d] - cj[d], z, cj[d]);
-                    if (d == 0) {
-                        A.flnp[size_t(hp) * ns + j] = v;
-                        if (A.fnacc) A.fnacc[size_t(hp) * ns + j] += 1;
-                    }
-                }
-            }
-            if (l == 63) {
+            fold_rows(l);
+            if (l == 63) {  // the verdict's draw, zf and old ln_prob
+                const int ns = A.jns, h = L.half;
                 const uint4 r1 = draw(L.seed, L.step, h, 1, A.jlo + w);
                 sacc1[0] = log(u53(r1.x, r1.y));
                 sacc1[1] = X.jk ? X.zfC[size_t(cand) * nwk + w] : L.zfac[w];

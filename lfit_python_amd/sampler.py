@@ -464,8 +464,17 @@ class EnsembleSampler:
         self._cat = None
         return buf, thin
 
-    def _end(self, buf):
-        """end of a stored run: its device chunk moves to host memory (offload)"""
+    def _end(self, buf, rows=None):
+        """end of a stored run: its device chunk moves to host memory
+        (offload); rows: the chunk's rows actually written (a sample()
+        generator left early), the rest is dropped"""
+        if buf is not None and rows is not None and rows < buf[0].shape[0]:
+            cut = (buf[0][:rows], buf[1][:rows])
+            self._chunks = [cut if c is buf else c for c in self._chunks]
+            if self._last is buf:
+                self._last = cut
+            self._cat = None
+            buf = cut
         if buf is None or not self.offload or self.dev.type != "cuda":
             return
         host = tuple(t.cpu() for t in buf)
@@ -497,19 +506,22 @@ class EnsembleSampler:
         sync-free path is run_mcmc()."""
         buf, thin = self._begin(p0, lnprob0, rstate0, iterations,
                                 thin, storechain if store is None else store)
+        done = 0
         try:
             for i in range(int(iterations)):
                 self.step()
                 self.sync()
                 self._store(buf, i, thin)
+                done = i + 1
                 if i == int(iterations) - 1:
                     self._end(buf)
                     buf = None
                 yield _host(self._pos), _host(self._lnp), self.random_state
         finally:
             # a caller that leaves the generator early (break, GeneratorExit)
-            # still gets the chunk offloaded
-            self._end(buf)
+            # keeps the steps it ran, offloaded
+            if buf is not None:
+                self._end(buf, rows=-(-done // thin))
 
     def run_mcmc(self, pos0, N, rstate0=None, lnprob0=None, storechain=True, store=None, thin=1, **kwargs):
         """emcee 2.x run_mcmc: N steps from pos0 (None: the current state);

@@ -295,3 +295,23 @@ def test_two_rank_run_mcmc_save_writes_once(tmp_path):
     one = str(tmp_path / "one.txt")
     mcmc_utils.run_mcmc_save(S, pos, 5, state, one, col_names="walker_no a b c d e ln_prob")
     assert open(one).read() == open(path).read()
+
+
+def test_sample_generator_left_early_keeps_its_steps():
+    """A sample() generator the caller leaves early (break -> GeneratorExit)
+    keeps the steps it ran in the chain and no unwritten rows (ADVICE r04:
+    the end-of-run handling now runs in a finally); a later run appends."""
+    ev = GaussLnProb()
+    S = EnsembleSampler(W, NDIM, ev, seed=5, ops=sd.TorchCpuOps())
+    S.set_state(_p0())
+    for i, (pos, lnp, _) in enumerate(S.sample(iterations=10, thin=2)):
+        last = pos
+        if i == 4:
+            break                       # 5 steps ran: steps 0, 2, 4 stored
+    assert S.chain.shape == (W, 3, NDIM)
+    np.testing.assert_array_equal(S.chain[:, -1], last)
+    assert S.last_run()[0].shape == (3, W, NDIM)
+    S.run_mcmc(None, 4)
+    assert S.chain.shape == (W, 7, NDIM)
+    # the host chunks were replaced by one concatenation: a second read is the same object
+    assert S._concat() is S._concat() and len(S._chunks) == 1
