@@ -2628,7 +2628,7 @@ struct PairArgs {
     // global load less before the candidate is known
     unsigned long long jseed, jstep;
     int jhalf, jlo, jns;
-    int prio;  // every workgroup resident at once (PAIR_PRIO)
+    int prio;  // blocks [0, prio) take the wave priorities (PAIR_PRIO; pair_prio)
     // FOLD (lfg_stretch_step_shard_fold): the partner half's moves of the
     // half-step before are accepted here, from the verdicts every rank
     // gathered (fv [jns]: ln_prob where accepted, NaN where not; nullptr:
@@ -2671,17 +2671,17 @@ __device__ unsigned long long g_pair_j[3][16][4096];  // per chunk: job start, s
 #define PAIR_WSTAMP(k)
 #endif
 
-// wave priority in a launch whose workgroups are all resident at once
-// (A.prio): the issue arbiter favours the older of a CU's two workgroups, so
-// one finished ~10 us before the other and the CU ran its last phases on
-// half its waves.  Element waves drop their priority with each job they
-// start (3, 2, 1, then 0), so both workgroups advance together; the
-// speculative setup waves (latency-bound, and the longest job) keep 3.  In a
-// launch of several rounds the older workgroup's early finish lets the next
-// round's start, so the default order stays.
-#define PAIR_PRIO(p)                                   \
-    do {                                               \
-        if (A.prio) __builtin_amdgcn_s_setprio(p);     \
+// wave priority in a launch of at most two rounds (blocks [0, A.prio)): the
+// issue arbiter favours the older of a CU's two workgroups, so one finished
+// ~10 us before the other and the CU ran its last phases on half its waves.
+// Element waves drop their priority with each job they start (3, 2, 1, then
+// 0), so both workgroups advance together; the speculative setup waves
+// (latency-bound, and the longest job) keep 3.  In a launch of many rounds
+// the older workgroup's early finish lets the next round's start, so the
+// default order stays (pair_prio)
+#define PAIR_PRIO(p)                                                    \
+    do {                                                                \
+        if (int(blockIdx.x) < A.prio) __builtin_amdgcn_s_setprio(p);    \
     } while (0)
 
 // k_pair's sweep of one solved item (the element phase's sink): element runs
@@ -4120,12 +4120,20 @@ int lfg_flux(const double* pars, int W, int P, const double* x, const double* w,
 // included); k_elements + k_lnlike serve the rest, and every tree when
 // LFG_PAIR=0 is in the environment (the A/B switch of the two layouts)
 // k_pair's workgroups all resident at once: two per CU (72.9 KB of LDS each)
-static bool pair_one_round(int npairs)
+// PairArgs.prio: the workgroups that take the wave-priority scheme
+// (PAIR_PRIO).  Launches of at most two rounds (two workgroups per CU
+// resident): all of them -- the one-round launches of config 2 and of the
+// weak-scaling shards, and the two-round 1 024-pair shard of config 4 over 8
+// ranks, whose projected 1 -> 8 speed-up rose 5.7x -> 6.1x with it (A/B,
+// rounds 1 and 2 both prioritised vs none: 173 vs 183 us per step).  Longer
+// launches none: there an early finish lets the next round's workgroup in
+// (the GP example's 6 rounds: 1.92 vs 1.95 M evals/s with the scheme on)
+static int pair_prio(int npairs)
 {
     int dev = 0, cus = 0;  // the current device's (the runtime caches the attribute)
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         cus = 0;
-    return npairs <= 2 * cus;
+    return npairs <= 4 * cus ? npairs : 0;
 }
 
 // the trees k_pair can serve: one-tile eclipses, S = 1
@@ -4181,7 +4189,7 @@ int lfg_lnlike(const double* pars, int W, int P, const double* x, const double* 
                nsub, nullptr, nullptr, lnlike, W, nullptr, nullptr, nullptr, false, nullptr,
                nullptr, nullptr, nullptr, 0, 0, 0ull, 0ull, nullptr};
     L.bstatus = ws.bstatus;
-    if (pair) hipLaunchKernelGGL(k_pair<false>, dim3(W), dim3(LIKE_THREADS), 0, st, PairArgs{L, ElemSpec{}, nullptr, nullptr, 64, 0, 0ull, 0ull, 0, 0, 0, pair_one_round(W) ? 1 : 0});
+    if (pair) hipLaunchKernelGGL(k_pair<false>, dim3(W), dim3(LIKE_THREADS), 0, st, PairArgs{L, ElemSpec{}, nullptr, nullptr, 64, 0, 0ull, 0ull, 0, 0, 0, pair_prio(W)});
     else if (nsub > 1) hipLaunchKernelGGL((k_lnlike<1, true>), dim3(W), dim3(LIKE_THREADS), 0, st, L);
     else hipLaunchKernelGGL((k_lnlike<1, false>), dim3(W), dim3(LIKE_THREADS), 0, st, L);
     if ((rc = launch_ok())) return rc;
@@ -4357,7 +4365,7 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
     L.accflag = (sp && acc) ? ws.accflag + size_t(prop->half) * ws.accstride : nullptr;
     L.combine = T->E == 1;  // E > 1: k_combine_walkers after the likelihood kernels
     if (pair_path) {
-        PairArgs A{L, X, nullptr, nullptr, spl, nbc, 0ull, 0ull, 0, 0, 0, pair_one_round(npairs) ? 1 : 0};
+        PairArgs A{L, X, nullptr, nullptr, spl, nbc, 0ull, 0ull, 0, 0, 0, pair_prio(npairs)};
         if (prop) {
             A.jseed = prop->seed;
             A.jstep = prop->step;
