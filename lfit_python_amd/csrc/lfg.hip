@@ -1899,7 +1899,11 @@ __device__ __forceinline__ double2 sub_point(const SubTables& T, const SubEntrie
         bool chg = false;
         if (j == 0 || !(phn >= ph)) {  // a fresh lookup
             sv = false;
+#ifdef LFG_ABL_FRESH  // diagnostic ablation: no donor table lookup
+            cur = nd;
+#else
             cur = sub_donor(T, D, sdq, VN[1], phn, vx, vy, vz);
+#endif
             chg = true;
             const double4 e4 = sincospi2_ool(2.0 * phn, 4.0 * h);  // the turn per sub-bin: 2 pi (2 h)
             sn = e4.x;
@@ -1933,7 +1937,11 @@ __device__ __forceinline__ double2 sub_point(const SubTables& T, const SubEntrie
         // inside a window give its partial overlaps); zero widths: points
         double ebj = 0.0;
         const double lo = ph - h, hi = ph + h;
+#ifdef LFG_ABL_SPOT  // diagnostic ablation: no spot eclipse
+        if (false) {
+#else
         if (!(h > 0.0)) {
+#endif
             ebj = sub_spot(T, sab, sbw, VN[0], lo, hi, shull[2], shull[3]);
         } else if (hi > shull[2] && lo < shull[3]) {
             const double itb = VN[0];
@@ -2459,7 +2467,11 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
         // any unsorted / mixed window (or invalid width) of the tile: the
         // pass goes point-major (every element against each point)
         const bool dir = (sflag[0] & 7) != 0 || (!TAB && sflag[1] != 0);
+#ifdef LFG_ABL_WDD  // diagnostic ablation: no WD/disc sweep
+        const bool wdd = false;
+#else
         const bool wdd = !hull || (sflag[0] & 8) != 0;  // the WD/disc elements touch the tile
+#endif
         LIKE_STAMP(1);
         double eb = 0.0, R3 = 0.0, R4 = 0.0, R5 = 0.0;
         if (dir) {
@@ -2539,7 +2551,11 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
             sbs = beam * (1.0 - eb);
             srs = D / snorm[2];
         } else if (own) {
+#ifdef LFG_ABL_SUBPOINT  // diagnostic ablation: no sub-bin spot / donor terms
+            const double2 r2 = make_double2(ph0 * 1e-30, wk * 1e-30);
+#else
             const double2 r2 = sub_point(SU.tb, DE, sab, sbw, sdq, snorm, shull, SG, ph0, wk, S);
+#endif
             sbs = r2.x;
             srs = r2.y;
         }
@@ -2873,13 +2889,300 @@ __device__ __forceinline__ void pair_cells(int* cell, int p, int m, double vprev
         for (int g = g1 + 1; g <= LIKE_NC; ++g) cell[g] = m;
 }
 
+// ---- LONG: eclipses of any length and sub-binned exposures in k_pair ----
+// The element phase stores every solved item (k_pair's point-major sinks:
+// WD/disc intervals, spot intervals and weights, donor tiles) and the pair's
+// breakpoints are then bucketed into per-pair tables in LDS, so that every
+// point is evaluated on its own, with no tile loop, block scan or barrier per
+// 512 points (config 5: 10 000 points x 5 sub-bins):
+//  * WD and disc (one table each, the symmetry-unique elements; a mirror
+//    element [-b, -a] is the unique one seen from -phase): the eclipsed
+//    fraction of window [lo, hi] is the integral of the covering weight,
+//      int_lo^hi C(t) dt = C(lo) (hi - lo) + sum_{lo <= pos < hi} q (hi - pos),
+//    with q = +w at a start a_k and -w at an end b_k (int64 fixed point, so
+//    C(lo) -- the cell's prefix plus its entries below lo -- is exact); a
+//    zero-width window takes the elements with a_k < ph < b_k;
+//  * spot and donor at the sub-bins: the S > 1 breakpoint tables of k_lnlike
+//    (SubTables, SubEntries, sub_point), built here from LDS.
+// Each thread takes a contiguous run of points (MODEL_SPEC 3 for every
+// width, order and wrap: no sortedness is assumed).
+constexpr int NE_W = 2 * U_WD, NE_D = 2 * U_DISC;  // WD / disc table entries (two per unique element)
+struct LongTabs {
+    long long cpre[2][TCELLS];  // WD / disc: covering weight at each cell's start
+    int cend[2][TCELLS];        // counts -> exclusive offsets -> (after the scatter) cell ends
+    double epos[NE_W + NE_D];   // entries: WD [0, NE_W), disc after
+    long long ewq[NE_W + NE_D];
+    double t0, ginv, amin, bmax;  // cells over the WD/disc hull
+    double snorm[4];            // sub_point's: 1 / spot total, 1 / donor |v| sum, donor norm, |v| sum
+    double shull[4];            // [2], [3]: the spot hull (sub_point)
+    double sgeo[LFG_NGEO];      // the record, for sub_point's LDS reads
+    double part[6][LIKE_THREADS / 64];  // wave partials of the hulls and sums
+};
+
+// eclipsed fraction of table t over window [lo, hi] (hi > lo): the integral
+// of the covering weight over the window / its width
+__device__ __forceinline__ double long_window(const LongTabs& W, int t, double lo, double hi)
+{
+    if (!(hi > W.amin && lo < W.bmax)) return 0.0;
+    const int g0 = tcell(lo, W.t0, W.ginv), g1 = tcell(hi, W.t0, W.ginv);
+    const int base = t ? NE_W : 0;
+    long long C = W.cpre[t][g0];
+    double corr = 0.0;
+    for (int g = g0; g <= g1; ++g) {
+        for (int i = g ? W.cend[t][g - 1] : 0, ie = W.cend[t][g]; i < ie; ++i) {
+            const double pos = W.epos[base + i];
+            const long long q = W.ewq[base + i];
+            if (g == g0 && pos < lo) C += q;
+            else if (pos < hi) corr = fma(double(q), hi - pos, corr);
+        }
+    }
+    return fma(corr, FX_INV / (hi - lo), double(C) * FX_INV);
+}
+
+// table t at a point (zero-width window): the elements with a_k < ph < b_k
+__device__ __forceinline__ double long_point(const LongTabs& W, int t, double ph)
+{
+    if (!(ph > W.amin && ph < W.bmax)) return 0.0;
+    const int g = tcell(ph, W.t0, W.ginv);
+    const int base = t ? NE_W : 0;
+    long long C = W.cpre[t][g];
+    for (int i = g ? W.cend[t][g - 1] : 0, ie = W.cend[t][g]; i < ie; ++i) {
+        const double pos = W.epos[base + i];
+        const long long q = W.ewq[base + i];
+        if (q > 0 ? pos < ph : pos <= ph) C += q;
+    }
+    return double(C) * FX_INV;
+}
+
+// WD and disc eclipsed fractions of a point's window (phase phc, half-width
+// wk >= 0): the unique elements over [lo, hi] and, for their mirrors, over
+// [-hi, -lo]
+__device__ __forceinline__ double2 long_wd_disc(const LongTabs& W, double phc, double wk)
+{
+    if (wk > 0.0) {
+        const double lo = phc - wk, hi = phc + wk;
+        return make_double2(long_window(W, 0, lo, hi) + long_window(W, 0, -hi, -lo),
+                            long_window(W, 1, lo, hi) + long_window(W, 1, -hi, -lo));
+    }
+    return make_double2(long_point(W, 0, phc) + long_point(W, 0, -phc), long_point(W, 1, phc) + long_point(W, 1, -phc));
+}
+
+// the LONG tables from the element phase's results in LDS (all threads of
+// the block, after the phase barrier; five barriers).  abw: the WD/disc
+// intervals by sweep slot; the spot (sab, sbw), the donor tiles (sdq), the
+// disc ring weights (swt) and the spot / donor fixed-point totals (stot) as
+// k_pair's point-major sinks leave them.  The tables must be zero (k_pair's
+// prologue clears them)
+__device__ __forceinline__ void long_tables(LongTabs& W, SubTables& T, SubEntries& D, const double2* abw,
+                                            const double2* sab, const double* sbw, const double* sdq,
+                                            const double* swt, const unsigned long long* stot, double ul, double itwd,
+                                            long long (*spart)[LIKE_THREADS / 64], int tid)
+{
+    constexpr int nt = LIKE_THREADS, nw = LIKE_THREADS / 64;
+    const int lane = tid & 63, wv = tid >> 6;
+    // (a) hulls of the WD/disc and spot intervals, the donor |v| sum
+    double amin = INFINITY, bmax = -INFINITY, sa = INFINITY, sb = -INFINITY, vs = 0.0;
+    for (int g = tid; g < NU_WDD; g += nt) {
+        const double2 ab = abw[g];
+        if (ab.x < ab.y) { amin = fmin(amin, ab.x); bmax = fmax(bmax, ab.y); }
+    }
+    if (tid < NBS && sab[tid].x < sab[tid].y) { sa = sab[tid].x; sb = sab[tid].y; }
+    if (tid < U_DON)  // the four mirror images of a tile have the same |vx| + |vy| + |vz|
+        vs = 4.0 * (fabs(sdq[tid * DON_STRIDE]) + fabs(sdq[tid * DON_STRIDE + 1]) + fabs(sdq[tid * DON_STRIDE + 2]));
+    amin = wave_min(amin); bmax = wave_max(bmax); sa = wave_min(sa); sb = wave_max(sb); vs = wave_sum(vs);
+    if (lane == 0) { W.part[0][wv] = amin; W.part[1][wv] = bmax; W.part[2][wv] = sa; W.part[3][wv] = sb; W.part[4][wv] = vs; }
+    __syncthreads();
+    amin = INFINITY; bmax = -INFINITY; sa = INFINITY; sb = -INFINITY; vs = 0.0;
+    for (int k = 0; k < nw; ++k) {  // every thread forms the block's values (no barrier for a broadcast)
+        amin = fmin(amin, W.part[0][k]); bmax = fmax(bmax, W.part[1][k]);
+        sa = fmin(sa, W.part[2][k]); sb = fmax(sb, W.part[3][k]); vs += W.part[4][k];
+    }
+    const double t0 = amin, ginv = (bmax > amin) ? TCELLS / (bmax - amin) : 0.0;
+    const double st0 = sa, sginv = (sb > sa) ? TCELLS / (sb - sa) : 0.0;
+    constexpr double t0d = -0.5, t1d = 0.5, dginv = TCELLS;  // donor cells: the whole phase circle
+    const double itb = 1.0 / (double(static_cast<long long>(stot[0])) * (FX_INV / PAIR_SPOT_S)), ivs = 1.0 / vs;
+    if (tid == 0) {
+        W.t0 = t0; W.ginv = ginv; W.amin = amin; W.bmax = bmax;
+        W.snorm[0] = itb;
+        W.snorm[1] = ivs;
+        W.snorm[2] = double(static_cast<long long>(stot[1])) * (FX_INV / PAIR_DON_S);
+        W.snorm[3] = vs;
+        W.shull[0] = amin; W.shull[1] = bmax; W.shull[2] = sa; W.shull[3] = sb;
+        T.dt0 = t0d; T.dginv = dginv; T.st0 = st0; T.sginv = sginv;
+    }
+    // (b) counts and fixed-point sums per cell
+    auto wd_entry = [&](int g, double2& ab, int& t, long long& q) {
+        ab = abw[g];
+        if (!(ab.x < ab.y)) return false;
+        const int u = uitem(g), ir = uring(u);
+        t = u < U_WD ? 0 : 1;
+        q = to_fx(u < U_WD ? wd_ring_weight(ir, ul) * itwd : swt[ir - NWD_RINGS] * (1.0 / swt[NDISC_R]));
+        return true;
+    };
+    for (int g = tid; g < NU_WDD; g += nt) {
+        double2 ab;
+        int t;
+        long long q;
+        if (!wd_entry(g, ab, t, q)) continue;
+        const int ga = tcell(ab.x, t0, ginv), gb = tcell(ab.y, t0, ginv);
+        atomicAdd(&W.cend[t][ga], 1);
+        atomicAdd(&W.cend[t][gb], 1);
+        atomicAdd(reinterpret_cast<unsigned long long*>(&W.cpre[t][ga]), static_cast<unsigned long long>(q));
+        atomicAdd(reinterpret_cast<unsigned long long*>(&W.cpre[t][gb]), static_cast<unsigned long long>(-q));
+    }
+    {
+        double p0, p1;
+        bool in0, in1;
+        int v0;
+        lane_breakpoints(tid, sdq, sab, t0d, t1d, p0, p1, in0, in1, v0);
+        if (tid >= nt - NDONOR) {
+            long long q[3];
+            donor_q(sdq, tid - (nt - NDONOR), ivs, q[0], q[1], q[2]);
+            if (v0)
+                for (int k = 0; k < 3; ++k)
+                    atomicAdd(reinterpret_cast<unsigned long long*>(&T.dv0[k]), static_cast<unsigned long long>(v0 * q[k]));
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                if (!(b ? in1 : in0)) continue;
+                const int g = tcell(b ? p1 : p0, t0d, dginv);
+                atomicAdd(&T.dend[g], 1);
+                for (int k = 0; k < 3; ++k)
+                    atomicAdd(reinterpret_cast<unsigned long long*>(&T.dpre[g][k]),
+                              static_cast<unsigned long long>(b ? -q[k] : q[k]));
+            }
+        } else if (in0) {
+            const long long Wq = to_fx(sbw[tid] * itb);
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                const int g = tcell(b ? p1 : p0, st0, sginv);
+                atomicAdd(&T.send[g], 1);
+                atomicAdd(reinterpret_cast<unsigned long long*>(&T.spre[g]), static_cast<unsigned long long>(b ? -Wq : Wq));
+            }
+        }
+    }
+    __syncthreads();
+    // (c) exclusive prefixes over the cells
+    {
+        long long v[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        if (tid < TCELLS) {
+            v[0] = W.cend[0][tid]; v[1] = W.cend[1][tid]; v[2] = W.cpre[0][tid]; v[3] = W.cpre[1][tid];
+            v[4] = T.dend[tid]; v[5] = T.send[tid]; v[6] = T.dpre[tid][0]; v[7] = T.dpre[tid][1];
+            v[8] = T.dpre[tid][2]; v[9] = T.spre[tid];
+        }
+        cell_scan<10>(v, spart, tid);
+        if (tid < TCELLS) {
+            W.cend[0][tid] = int(v[0]); W.cend[1][tid] = int(v[1]); W.cpre[0][tid] = v[2]; W.cpre[1][tid] = v[3];
+            T.dend[tid] = int(v[4]); T.send[tid] = int(v[5]);
+            T.dpre[tid][0] = v[6] + T.dv0[0]; T.dpre[tid][1] = v[7] + T.dv0[1]; T.dpre[tid][2] = v[8] + T.dv0[2];
+            T.spre[tid] = v[9];
+        }
+    }
+    __syncthreads();
+    // (d) the entries into cell order; afterwards cend / dend / send hold the cell ends
+    for (int g = tid; g < NU_WDD; g += nt) {
+        double2 ab;
+        int t;
+        long long q;
+        if (!wd_entry(g, ab, t, q)) continue;
+        const int base = t ? NE_W : 0;
+        const int ia = atomicAdd(&W.cend[t][tcell(ab.x, t0, ginv)], 1);
+        W.epos[base + ia] = ab.x;
+        W.ewq[base + ia] = q;
+        const int ib = atomicAdd(&W.cend[t][tcell(ab.y, t0, ginv)], 1);
+        W.epos[base + ib] = ab.y;
+        W.ewq[base + ib] = -q;
+    }
+    {
+        double p0, p1;
+        bool in0, in1;
+        int v0;
+        lane_breakpoints(tid, sdq, sab, t0d, t1d, p0, p1, in0, in1, v0);
+        const int base = (tid >= nt - NDONOR) ? 2 * (tid - (nt - NDONOR)) : 2 * tid;
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            if (!(b ? in1 : in0)) continue;
+            const double pos = b ? p1 : p0;
+            if (tid >= nt - NDONOR) {
+                const int slot = atomicAdd(&T.dend[tcell(pos, t0d, dginv)], 1);
+                D.dpos[slot] = pos;
+                D.dcode[slot] = base + b;
+            } else {
+                const int slot = atomicAdd(&T.send[tcell(pos, st0, sginv)], 1);
+                T.spos[slot] = pos;
+                T.scode[slot] = base + b;
+            }
+        }
+    }
+    __syncthreads();
+    // (e) the donor and spot entries of each cell by position (sub_point's
+    // cursors; a donor end before a start at equal positions), and the
+    // WD/disc entries by (position, weight): the atomics' slot order is
+    // arbitrary, and long_window's double sums must not depend on it
+#ifndef LFG_ABL_LSORT
+    for (int c = tid; c < 2 * TCELLS; c += nt) {
+        const int t = c / TCELLS, g = c - t * TCELLS, base = t ? NE_W : 0;
+        const int i0 = base + (g ? W.cend[t][g - 1] : 0), i1 = base + W.cend[t][g];
+        for (int i = i0 + 1; i < i1; ++i) {
+            const double p = W.epos[i];
+            const long long q = W.ewq[i];
+            int k = i;
+            for (; k > i0 && (W.epos[k - 1] > p || (W.epos[k - 1] == p && W.ewq[k - 1] > q)); --k) {
+                W.epos[k] = W.epos[k - 1];
+                W.ewq[k] = W.ewq[k - 1];
+            }
+            W.epos[k] = p;
+            W.ewq[k] = q;
+        }
+    }
+#endif
+#ifndef LFG_ABL_DSORT
+    if (tid < TCELLS) {
+#else
+    if (false) {
+#endif
+        const int i0 = tid ? T.dend[tid - 1] : 0, i1 = T.dend[tid];
+        for (int i = i0 + 1; i < i1; ++i) {
+            const double p = D.dpos[i];
+            const int c = D.dcode[i];
+            int k = i;
+            for (; k > i0; --k) {
+                const double pk = D.dpos[k - 1];
+                const int ck = D.dcode[k - 1];
+                if (!(pk > p || (pk == p && (c & 1) && !(ck & 1)))) break;
+                D.dpos[k] = pk;
+                D.dcode[k] = ck;
+            }
+            D.dpos[k] = p;
+            D.dcode[k] = c;
+        }
+        const int j0 = tid ? T.send[tid - 1] : 0, j1 = T.send[tid];
+        for (int i = j0 + 1; i < j1; ++i) {
+            const double p = T.spos[i];
+            const int c = T.scode[i];
+            int k = i;
+            for (; k > j0 && T.spos[k - 1] > p; --k) {
+                T.spos[k] = T.spos[k - 1];
+                T.scode[k] = T.scode[k - 1];
+            }
+            T.spos[k] = p;
+            T.scode[k] = c;
+        }
+    }
+    __syncthreads();
+}
+
 // GP (GP trees, MODE 2 of k_lnlike): instead of chi^2 the residuals, each
 // point's e^{-lam dx} and changepoint block go to the workspace for
 // k_gp_like, and a walker that tripped the changepoint cache rule has its
 // distance solved here (k_gp_dcp's ten limb points, on wave 0's lanes 32..)
-template <bool GP, bool FOLD = false>
+// LONG: eclipses longer than a tile and sub-binned exposures (the LONG
+// tables above, long_tables / long_wd_disc / sub_point): the element phase
+// keeps the point-major sinks, and after the phase barrier the tables are
+// built and every thread evaluates a contiguous run of points
+template <bool GP, bool FOLD = false, bool LONG = false>
 __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
 {
+    static_assert(!(GP && LONG), "GP trees keep the one-tile layout or the two kernels");
     const LikeArgs& L = A.L;
     const ElemSpec& X = A.X;
     __shared__ double swt[NDISC_R + 1];           // disc ring weights and the disc total (prologue)
@@ -2907,6 +3210,12 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
     __shared__ int sjob;
     __shared__ double sq[ACC_LDS];
     __shared__ double sy[LIKE_TILE], sye[LIKE_TILE];
+    // LONG only (the one-tile instantiations reference none of these)
+    __shared__ LongTabs LT;
+    __shared__ SubTables LST;
+    __shared__ SubEntries LSE;
+    __shared__ double2 Lab[NU_WDD];
+    __shared__ long long lspart[10][LIKE_THREADS / 64];
 
     constexpr int nt = LIKE_THREADS, nw = LIKE_THREADS / 64;
     const int pair = blockIdx.x, npairs = L.npairs;
@@ -2930,19 +3239,19 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
 
     // the point loads the windows need, issued first: they overlap the
     // candidate chain below (own point, predecessor, first and last)
-    const bool own = tid < n;
+    const bool own = !LONG && tid < n;
     const int m = n;
     const int pl = own ? tid : 0;
     const double* xe = L.x + o0;
     double xw_own = 0.0, xw_prv = 0.0, xw_0 = 0.0, xw_1 = 0.0;
     double ww_own = 0.0, ww_prv = 0.0, ww_0 = 0.0, ww_1 = 0.0;
-    if (n > 0) {
+    if (!LONG && n > 0) {
         xw_own = xe[pl];
         xw_prv = xe[pl > 0 ? pl - 1 : 0];
         xw_0 = xe[0];
         xw_1 = xe[n - 1];
     }
-    if (L.w && n > 0) {
+    if (!LONG && L.w && n > 0) {
         const double* we = L.w + o0;
         ww_own = we[pl];
         ww_prv = we[pl > 0 ? pl - 1 : 0];
@@ -3020,13 +3329,29 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
         const int wf = wave_or4(fl);
         if (lane == 0) sflagw[wv] = wf;
     }
-    for (int i = 0; i < 6; ++i) sacc[i][tid] = 0ull;
-    SU.s.X[0][tid] = 0ull;
-    SU.s.X[1][tid] = 0ull;
+    if constexpr (LONG) {  // the tables' counters and sums; the record for sub_point's LDS reads
+        if (tid < TCELLS) {
+            LT.cpre[0][tid] = LT.cpre[1][tid] = 0;
+            LT.cend[0][tid] = LT.cend[1][tid] = 0;
+            LST.dpre[tid][0] = LST.dpre[tid][1] = LST.dpre[tid][2] = 0;
+            LST.spre[tid] = 0;
+            LST.dend[tid] = LST.send[tid] = 0;
+        } else if (tid < TCELLS + 3) {
+            LST.dv0[tid - TCELLS] = 0;
+        } else if (tid >= nt - LFG_NGEO) {
+            LT.sgeo[tid - (nt - LFG_NGEO)] = G[tid - (nt - LFG_NGEO)];
+        }
+    } else {
+        for (int i = 0; i < 6; ++i) sacc[i][tid] = 0ull;
+        SU.s.X[0][tid] = 0ull;
+        SU.s.X[1][tid] = 0ull;
+    }
     if (tid == 0) {
-        for (int i = 0; i < 6; ++i) sacc[i][nt] = 0ull;
-        SU.s.X[0][nt] = 0ull;
-        SU.s.X[1][nt] = 0ull;
+        if constexpr (!LONG) {
+            for (int i = 0; i < 6; ++i) sacc[i][nt] = 0ull;
+            SU.s.X[0][nt] = 0ull;
+            SU.s.X[1][nt] = 0ull;
+        }
         stot[0] = stot[1] = 0ull;
         sjob = (X.nspec > 0 && pair < 2 * A.nbc) ? 8 : 9;
     }
@@ -3036,8 +3361,9 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
     __syncthreads();  // B0: windows, cells, flags, zeroed sums, ring weights, sjob
     PAIR_STAMP(16, tid == 0);
 
-    bool dir = false;
-    for (int k = 0; k < nw; ++k) dir = dir || sflagw[k] != 0;
+    bool dir = LONG;  // LONG: the point-major sinks always
+    if (!LONG)
+        for (int k = 0; k < nw; ++k) dir = dir || sflagw[k] != 0;
     // this thread's data point (read after the phase barrier), the GP
     // filter's transition factor of the point (k_gp_like)
     if (own) {
@@ -3188,9 +3514,16 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
     }
     if (st == ST_OK && m > 0) {
         const double ul = Gc[G_ULIMB];
-        PairSink K{dir, lane, phase_index(TA.lo, TA.cell, m), phase_index(sph, SU.s.scp, m), TA.hi, TA.iw, sacc,
-                   SU.s.X, stot, swt, ul, 1.0 / (TWO_PI * ((1.0 - ul) * 0.5 + ul / 3.0)), Gc[G_S], Gc[G_C],
-                   SU.ab, sab, sbw, sdq};
+        const double itwd = 1.0 / (TWO_PI * ((1.0 - ul) * 0.5 + ul / 3.0));
+        auto make_sink = [&]() {
+            if constexpr (LONG)  // the point-major sinks only (no tile arrays in this instantiation)
+                return PairSink{true, lane, PhaseIndex{}, PhaseIndex{}, nullptr, nullptr, nullptr, nullptr, stot, swt,
+                                ul, itwd, Gc[G_S], Gc[G_C], Lab, sab, sbw, sdq};
+            else
+                return PairSink{dir, lane, phase_index(TA.lo, TA.cell, m), phase_index(sph, SU.s.scp, m), TA.hi,
+                                TA.iw, sacc, SU.s.X, stot, swt, ul, itwd, Gc[G_S], Gc[G_C], SU.ab, sab, sbw, sdq};
+        };
+        PairSink K = make_sink();
         // chunk c: items v = 64 c + lane of one region each (c < 11: WD and
         // disc; 11, 12: spot; 13, 14: donor), so that no wave runs two
         // regions' code one after the other
@@ -3256,7 +3589,42 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
     }
     // ---- each point's flux and chi^2 (GP: residual, changepoint block)
     double chi = 0.0;
-    if (m > 0) {
+    if constexpr (LONG) {
+        // the pair's tables, then this thread's run of points [p0, p1)
+        const double ul = Gc[G_ULIMB];
+        long_tables(LT, LST, LSE, Lab, sab, sbw, sdq, swt, stot, ul, 1.0 / (TWO_PI * ((1.0 - ul) * 0.5 + ul / 3.0)),
+                    lspart, tid);
+        PAIR_STAMP(12, tid == 0);
+        const int S = L.nsub, R = (n + nt - 1) / nt, p0 = tid * R, p1 = min(p0 + R, n);
+        const double* xe = L.x + o0;
+        const double* we = L.w ? L.w + o0 : nullptr;
+        const double* ye = L.y + o0;
+        const double* ee = L.ye + o0;
+        const double fwd = Gc[G_WDF], fds = Gc[G_DF], fsp = Gc[G_SF], frs = Gc[G_RSF];
+#ifdef LFG_LONG_INTERLEAVE
+        for (int p = tid; p < n; p += nt) {
+#else
+        for (int p = p0; p < p1; ++p) {
+#endif
+            const double xp = xe[p], wp = we ? we[p] : 0.0, yp = ye[p], ep = ee[p];
+            const double wk = wp < 0.0 ? 0.0 : wp;  // MODEL_SPEC 3 (NaN stays NaN)
+            const double ph0 = xp - phi0, phc = wrap_phase(ph0);
+#ifdef LFG_ABL_LWD
+            const double2 f2 = make_double2(phc * 1e-30, wk * 1e-30);
+#else
+            const double2 f2 = long_wd_disc(LT, phc, wk);
+#endif
+#ifdef LFG_ABL_LSUB
+            const double2 r2 = make_double2(phc * 1e-30, wk * 1e-30);
+#else
+            const double2 r2 = sub_point(LST, LSE, sab, sbw, sdq, LT.snorm, LT.shull, LT.sgeo, ph0, wk, S);
+#endif
+            // k_lnlike's sum, term for term (MODEL_SPEC 3: a NaN width, a NaN flux)
+            const double f = isnan(wk) ? NAN : fwd * (1.0 - f2.x) + fds * (1.0 - f2.y) + fsp * r2.x / S + frs * r2.y / S;
+            const double rr = (yp - f) / ep;
+            chi += isnan(f) ? INFINITY : rr * rr;
+        }
+    } else if (m > 0) {
         const double s = Gc[G_S], c = Gc[G_C], ul = Gc[G_ULIMB];
         const double twd = TWO_PI * ((1.0 - ul) * 0.5 + ul / 3.0);  // 2 pi [F(1) - F(0)]
         const double wspot = double(static_cast<long long>(stot[0])) * (FX_INV / PAIR_SPOT_S);
@@ -4136,8 +4504,14 @@ static int pair_prio(int npairs)
     return npairs <= 4 * cus ? npairs : 0;
 }
 
-// the trees k_pair can serve: one-tile eclipses, S = 1
+// the trees k_pair can serve: one-tile eclipses, S = 1 (kind 1); and, with
+// the LONG tables, chi^2 trees of any eclipse length and sub-binning (kind 2)
 static bool pair_fits(int nsub, int max_n, int ndim) { return nsub == 1 && max_n <= LIKE_TILE && ndim <= LIKE_THREADS; }
+static int pair_eligible(int gp, int nsub, int max_n, int ndim)
+{
+    if (pair_fits(nsub, max_n, ndim)) return 1;
+    return (!gp && nsub >= 1 && ndim <= LIKE_THREADS) ? 2 : 0;
+}
 
 static bool pair_env()
 {
@@ -4146,15 +4520,15 @@ static bool pair_env()
 }
 static std::atomic<int> g_pair_layout{-2};  // -2: not read yet; 0 / 1: lfg_set_layout or the environment
 
-static bool pair_ok(int gp, int nsub, int max_n, int ndim)
+// the kernels a tree runs on: 0 k_elements + k_lnlike, 1 k_pair, 2 k_pair LONG
+static int pair_kind(int gp, int nsub, int max_n, int ndim)
 {
     int m = g_pair_layout.load(std::memory_order_relaxed);
     if (m == -2) {
         m = pair_env() ? 1 : 0;
         g_pair_layout.store(m, std::memory_order_relaxed);
     }
-    (void)gp;
-    return m == 1 && pair_fits(nsub, max_n, ndim);
+    return m == 1 ? pair_eligible(gp, nsub, max_n, ndim) : 0;
 }
 
 int lfg_set_layout(int mode)
@@ -4169,7 +4543,7 @@ int lfg_set_layout(int mode)
 int lfg_layout(const lfg_tree* T)
 {
     if (!T || T->E <= 0) return LFG_E_ARGS;
-    return pair_ok(T->gp, T->nsub, T->max_n, T->ndim) ? 1 : 0;
+    return pair_kind(T->gp, T->nsub, T->max_n, T->ndim);
 }
 
 int lfg_lnlike(const double* pars, int W, int P, const double* x, const double* w, int N, int nsub, const double* y,
@@ -4182,14 +4556,17 @@ int lfg_lnlike(const double* pars, int W, int P, const double* x, const double* 
     hipStream_t st = static_cast<hipStream_t>(stream);
     SetupArgs S{pars, W, P, 1, P, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
                 ws.geo, ws.status, ws.prior, ws.bstatus, 0, nullptr, nullptr};
-    const bool pair = pair_ok(0, nsub, N, 0);
+    const int kind = pair_kind(0, nsub, N, 0);
+    const bool pair = kind > 0;
     int rc = run_front(S, ws, st, nullptr, !pair);
     if (rc) return rc;
     LikeArgs L{ws.geo, ws.status, ws.ab, ws.donor, ws.wts, 1, nullptr, N, x, y, ye, w,
                nsub, nullptr, nullptr, lnlike, W, nullptr, nullptr, nullptr, false, nullptr,
                nullptr, nullptr, nullptr, 0, 0, 0ull, 0ull, nullptr};
     L.bstatus = ws.bstatus;
-    if (pair) hipLaunchKernelGGL(k_pair<false>, dim3(W), dim3(LIKE_THREADS), 0, st, PairArgs{L, ElemSpec{}, nullptr, nullptr, 64, 0, 0ull, 0ull, 0, 0, 0, pair_prio(W)});
+    const PairArgs A{L, ElemSpec{}, nullptr, nullptr, 64, 0, 0ull, 0ull, 0, 0, 0, pair_prio(W)};
+    if (kind == 2) hipLaunchKernelGGL((k_pair<false, false, true>), dim3(W), dim3(LIKE_THREADS), 0, st, A);
+    else if (pair) hipLaunchKernelGGL(k_pair<false>, dim3(W), dim3(LIKE_THREADS), 0, st, A);
     else if (nsub > 1) hipLaunchKernelGGL((k_lnlike<1, true>), dim3(W), dim3(LIKE_THREADS), 0, st, L);
     else hipLaunchKernelGGL((k_lnlike<1, false>), dim3(W), dim3(LIKE_THREADS), 0, st, L);
     if ((rc = launch_ok())) return rc;
@@ -4257,7 +4634,8 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
     // applied first, recording the acceptances for the candidate choice, and
     // the shard's verdicts are formed after its ln_prob (k_verdict)
     const double* fv = fold ? fold->fv : nullptr;
-    const bool fold_pair = fold && T->E == 1 && !T->gp && pair_ok(T->gp, T->nsub, T->max_n, T->ndim) &&
+    const int kind = pair_kind(T->gp, T->nsub, T->max_n, T->ndim);
+    const bool fold_pair = fold && T->E == 1 && !T->gp && kind > 0 &&
                            (!sp->out || 2 * ((2 * W + W + 63) / 64) <= W);
     const unsigned long long fstep = prop && prop->half == 0 ? prop->step - 1 : (prop ? prop->step : 0);
     if (fv && (!fold_pair || !sp->in)) {
@@ -4339,7 +4717,7 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
     // k_gp_like).  The speculative lanes fill whole waves: wave 0 of blocks
     // [0, 2 nbc), nbc blocks per candidate, so there must be 2 nbc pairs
     const int spl = 64, nbc = (X.nspec + 63) / 64;
-    const bool pair_path = pair_ok(T->gp, T->nsub, T->max_n, T->ndim) && (X.nspec == 0 || 2 * nbc <= npairs);
+    const bool pair_path = kind > 0 && (X.nspec == 0 || 2 * nbc <= npairs);
     if (fold_pair && !pair_path) return LFG_E_ARGS;  // (fold_pair's test is pair_path's)
     // the end of every path but the fold's own: the shard's verdicts from its
     // ln_prob (fold fallback), then the last event
@@ -4387,7 +4765,8 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
             A.L.step = prop->step;
             A.L.half = h;
             A.L.zfac = prop->zfac;
-            hipLaunchKernelGGL((k_pair<false, true>), dim3(npairs), dim3(LIKE_THREADS), 0, st, A);
+            if (kind == 2) hipLaunchKernelGGL((k_pair<false, true, true>), dim3(npairs), dim3(LIKE_THREADS), 0, st, A);
+            else hipLaunchKernelGGL((k_pair<false, true>), dim3(npairs), dim3(LIKE_THREADS), 0, st, A);
             if ((rc = launch_ok())) return rc;
             mark(3);
             return LFG_OK;
@@ -4414,6 +4793,8 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
             hipLaunchKernelGGL(k_pair<true>, dim3(npairs), dim3(LIKE_THREADS), 0, st, A);
             if ((rc = launch_ok())) return rc;
             hipLaunchKernelGGL(k_gp_like, dim3(T->E * ((W + GP_PAIRS - 1) / GP_PAIRS)), dim3(GP_BLOCK), 0, st, L);
+        } else if (kind == 2) {
+            hipLaunchKernelGGL((k_pair<false, false, true>), dim3(npairs), dim3(LIKE_THREADS), 0, st, A);
         } else {
             hipLaunchKernelGGL(k_pair<false>, dim3(npairs), dim3(LIKE_THREADS), 0, st, A);
         }
@@ -4424,7 +4805,7 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
         }
         return finish();
     }
-    if (sp && sp->out && acc && T->E == 1 && pair_fits(T->nsub, T->max_n, T->ndim)) {
+    if (sp && sp->out && acc && T->E == 1 && pair_eligible(T->gp, T->nsub, T->max_n, T->ndim)) {
         // a k_pair-eligible tree on the two-kernel layout (lfg_set_layout(0)):
         // leave the partner-half snapshot a k_pair launch would have left, so
         // that a layout switch before the chain's next half reads valid rows

@@ -89,13 +89,14 @@ def test_argument_errors_without_gpu():
 
 def test_layout_switch_without_gpu():
     """lfg_set_layout / lfg_layout (host-only): k_pair for one-tile S = 1
-    trees by default, the two-kernel layout for S > 1 and when switched off,
-    argument errors refused; the previous setting is returned and restored."""
+    trees by default, its LONG variant for sub-binned or longer chi^2
+    eclipses, the two-kernel layout for long GP eclipses and when switched
+    off; argument errors refused; the previous setting is returned and restored."""
     L = _native.lib()
 
-    def tree(nsub, max_n):  # lfg_layout reads the sizes only
+    def tree(nsub, max_n, gp=0):  # lfg_layout reads the sizes only
         T = _native.LfgTree()
-        T.E, T.ndim, T.nsub, T.max_n = 1, 18, nsub, max_n
+        T.E, T.ndim, T.nsub, T.max_n, T.gp = 1, 18, nsub, max_n, gp
         return ctypes.byref(T)
 
     assert L.lfg_layout(None) == -1
@@ -103,10 +104,13 @@ def test_layout_switch_without_gpu():
     prev = L.lfg_set_layout(1)
     try:
         assert L.lfg_layout(tree(1, 300)) == 1
-        assert L.lfg_layout(tree(5, 300)) == 0     # sub-binned: two kernels
-        assert L.lfg_layout(tree(1, 10000)) == 0   # more points than a tile
+        assert L.lfg_layout(tree(1, 300, gp=1)) == 1   # GP trees: k_pair<true> for one tile
+        assert L.lfg_layout(tree(5, 300)) == 2     # sub-binned: k_pair LONG
+        assert L.lfg_layout(tree(1, 10000)) == 2   # more points than a tile: LONG
+        assert L.lfg_layout(tree(1, 10000, gp=1)) == 0   # a long GP eclipse: two kernels
         assert L.lfg_set_layout(0) == 1
         assert L.lfg_layout(tree(1, 300)) == 0
+        assert L.lfg_layout(tree(5, 10000)) == 0
     finally:
         L.lfg_set_layout(prev)
 
