@@ -2919,52 +2919,171 @@ struct LongTabs {
     double part[6][LIKE_THREADS / 64];  // wave partials of the hulls and sums
 };
 
+// a thread's cursor into one sorted WD/disc table: the position x it stands
+// at, the first entry at or above x, and C(x) = sum of q over the entries
+// below x (exact int64).  Points that follow each other in phase move it by
+// the few entries between them; a jump to another cell starts over from the
+// cell's prefix (the same integer either way)
+struct LongCur {
+    double x;
+    int i;
+    long long C;
+};
+
+__device__ __forceinline__ void long_seek(const LongTabs& W, int t, LongCur& K, double x)
+{
+    const int base = t ? NE_W : 0, g = tcell(x, W.t0, W.ginv);
+    if (!(K.x == K.x && tcell(K.x, W.t0, W.ginv) == g)) {  // another cell (or no position yet): its prefix
+        K.C = W.cpre[t][g];
+        K.i = base + (g ? W.cend[t][g - 1] : 0);
+        const int ie = base + W.cend[t][g];
+        while (K.i < ie && W.epos[K.i] < x) K.C += W.ewq[K.i++];
+        K.x = x;
+        return;
+    }
+    const int ib = base, ie = base + W.cend[t][TCELLS - 1];
+    if (x >= K.x)
+        while (K.i < ie && W.epos[K.i] < x) K.C += W.ewq[K.i++];
+    else
+        while (K.i > ib && W.epos[K.i - 1] >= x) K.C -= W.ewq[--K.i];
+    K.x = x;
+}
+
 // eclipsed fraction of table t over window [lo, hi] (hi > lo): the integral
-// of the covering weight over the window / its width
-__device__ __forceinline__ double long_window(const LongTabs& W, int t, double lo, double hi)
+// of the covering weight over the window / its width; the cursor ends at hi
+__device__ __forceinline__ double long_window(const LongTabs& W, int t, LongCur& K, double lo, double hi)
 {
     if (!(hi > W.amin && lo < W.bmax)) return 0.0;
-    const int g0 = tcell(lo, W.t0, W.ginv), g1 = tcell(hi, W.t0, W.ginv);
-    const int base = t ? NE_W : 0;
-    long long C = W.cpre[t][g0];
+    long_seek(W, t, K, lo);
+    const long long C = K.C;
+    const int ie = (t ? NE_W : 0) + W.cend[t][TCELLS - 1];
     double corr = 0.0;
-    for (int g = g0; g <= g1; ++g) {
-        for (int i = g ? W.cend[t][g - 1] : 0, ie = W.cend[t][g]; i < ie; ++i) {
-            const double pos = W.epos[base + i];
-            const long long q = W.ewq[base + i];
-            if (g == g0 && pos < lo) C += q;
-            else if (pos < hi) corr = fma(double(q), hi - pos, corr);
-        }
+    while (K.i < ie && W.epos[K.i] < hi) {
+        corr = fma(double(W.ewq[K.i]), hi - W.epos[K.i], corr);
+        K.C += W.ewq[K.i++];
     }
+    K.x = hi;
     return fma(corr, FX_INV / (hi - lo), double(C) * FX_INV);
 }
 
 // table t at a point (zero-width window): the elements with a_k < ph < b_k
-__device__ __forceinline__ double long_point(const LongTabs& W, int t, double ph)
+// (the starts below ph, the ends at or below it)
+__device__ __forceinline__ double long_point(const LongTabs& W, int t, LongCur& K, double ph)
 {
     if (!(ph > W.amin && ph < W.bmax)) return 0.0;
-    const int g = tcell(ph, W.t0, W.ginv);
-    const int base = t ? NE_W : 0;
-    long long C = W.cpre[t][g];
-    for (int i = g ? W.cend[t][g - 1] : 0, ie = W.cend[t][g]; i < ie; ++i) {
-        const double pos = W.epos[base + i];
-        const long long q = W.ewq[base + i];
-        if (q > 0 ? pos < ph : pos <= ph) C += q;
-    }
+    long_seek(W, t, K, ph);
+    long long C = K.C;
+    const int ie = (t ? NE_W : 0) + W.cend[t][TCELLS - 1];
+    for (int i = K.i; i < ie && W.epos[i] == ph; ++i)
+        if (W.ewq[i] < 0) C += W.ewq[i];
     return double(C) * FX_INV;
 }
 
 // WD and disc eclipsed fractions of a point's window (phase phc, half-width
 // wk >= 0): the unique elements over [lo, hi] and, for their mirrors, over
-// [-hi, -lo]
-__device__ __forceinline__ double2 long_wd_disc(const LongTabs& W, double phc, double wk)
+// [-hi, -lo]; K: the thread's four cursors (WD, disc) x (window, mirror)
+__device__ __forceinline__ double2 long_wd_disc(const LongTabs& W, LongCur (&K)[4], double phc, double wk)
 {
     if (wk > 0.0) {
         const double lo = phc - wk, hi = phc + wk;
-        return make_double2(long_window(W, 0, lo, hi) + long_window(W, 0, -hi, -lo),
-                            long_window(W, 1, lo, hi) + long_window(W, 1, -hi, -lo));
+        return make_double2(long_window(W, 0, K[0], lo, hi) + long_window(W, 0, K[1], -hi, -lo),
+                            long_window(W, 1, K[2], lo, hi) + long_window(W, 1, K[3], -hi, -lo));
     }
-    return make_double2(long_point(W, 0, phc) + long_point(W, 0, -phc), long_point(W, 1, phc) + long_point(W, 1, -phc));
+    return make_double2(long_point(W, 0, K[0], phc) + long_point(W, 0, K[1], -phc),
+                        long_point(W, 1, K[2], phc) + long_point(W, 1, K[3], -phc));
+}
+
+// sub_point with its donor cursor carried from point to point (SubCur): a
+// point whose first sub-bin lies at or above the last one's phase walks on
+// from there instead of a fresh lookup (a thread's run of sorted points);
+// the line of sight is formed afresh at each point's first sub-bin
+struct SubCur {
+    double ph, npos;
+    long long vx, vy, vz;
+    int cur, ncode;
+};
+
+__device__ __forceinline__ double2 sub_point_c(const SubTables& T, const SubEntries& D, const double2* sab,
+                                               const double* sbw, const double* sdq, const double* snorm,
+                                               const double* shull, const double* SG, double ph0, double wk, int S,
+                                               SubCur& U)
+{
+    using lds_cvd = const volatile __attribute__((address_space(3))) double*;
+    const lds_cvd VG = (lds_cvd)SG;
+    const lds_cvd VN = (lds_cvd)snorm;
+    const int nd = T.dend[TCELLS - 1], nsp = T.send[TCELLS - 1];
+    const double h = wk / S, ih = 0.5 / h;
+    double sbs = 0.0, srs = 0.0, sn = 0.0, cs = 1.0, rs = 0.0, rc = 1.0;
+    long long Cs = 0;
+    int scur = 0;
+    bool sv = false;  // Cs / scur hold C at this sub-bin's lo
+    for (int j = 0; j < S; ++j) {
+        const double phn = wrap_phase(ph0 - wk + (2 * j + 1) * h);
+        bool chg = false;
+        if (!(phn >= U.ph)) {  // a fresh lookup (the first point, a step back in phase)
+            U.cur = sub_donor(T, D, sdq, VN[1], phn, U.vx, U.vy, U.vz);
+            U.npos = U.cur < nd ? D.dpos[U.cur] : INFINITY;
+            U.ncode = U.cur < nd ? D.dcode[U.cur] : 0;
+            chg = true;
+        } else {
+            while (donor_counted(U.npos, U.ncode, phn)) {  // npos = inf past the last entry
+                donor_apply(sdq, U.ncode, VN[1], U.vx, U.vy, U.vz);
+                chg = true;
+                ++U.cur;
+                U.npos = U.cur < nd ? D.dpos[U.cur] : INFINITY;
+                U.ncode = U.cur < nd ? D.dcode[U.cur] : 0;
+            }
+        }
+        if (j == 0 || !(phn >= U.ph)) {
+            const double4 e4 = sincospi2_ool(2.0 * phn, 4.0 * h);  // the turn per sub-bin: 2 pi (2 h)
+            sn = e4.x;
+            cs = e4.y;
+            rs = e4.z;
+            rc = e4.w;
+        } else {
+            const double c2 = fma(cs, rc, -sn * rs);
+            sn = fma(sn, rc, cs * rs);
+            cs = c2;
+        }
+        (void)chg;
+        U.ph = phn;
+        // spot: as sub_point (the windows of a point abut; each point starts afresh)
+        double ebj = 0.0;
+        const double lo = phn - h, hi = phn + h;
+        if (!(h > 0.0)) {
+            ebj = sub_spot(T, sab, sbw, VN[0], lo, hi, shull[2], shull[3]);
+        } else if (hi > shull[2] && lo < shull[3]) {
+            const double itb = VN[0];
+            if (!sv) Cs = spot_C(T, sbw, itb, lo, scur);
+            sv = true;
+            long long Cn = Cs;
+            double corr = 0.0;
+            for (; scur < nsp && T.spos[scur] <= hi; ++scur) {
+                const int code = T.scode[scur], k = code >> 1;
+                const double wn = sbw[k] * itb;
+                const double2 ab = sab[k];
+                const long long Wq = to_fx(wn);
+                if (!(code & 1)) {
+                    Cn += Wq;
+                    corr = fma(wn, fmin(ab.y, hi) - ab.x, corr);
+                } else {
+                    Cn -= Wq;
+                    if (ab.x <= lo) corr = fma(-wn, hi - ab.y, corr);
+                }
+            }
+            ebj = fma(corr, ih, double(Cs) * FX_INV);
+            Cs = Cn;
+        } else {
+            sv = false;
+        }
+        const double sg = VG[G_S], cg = VG[G_C];
+        const double e0 = sg * cs, e1 = -sg * sn;
+        srs = fma(e0, double(U.vx), fma(e1, double(U.vy), fma(cg, double(U.vz), srs)));
+        const double fis = VG[G_FIS];
+        sbs = fma(fis + (1.0 - fis) * fmax(VG[G_NB0] * e0 + VG[G_NB1] * e1 + VG[G_NB2] * cg, 0.0), 1.0 - ebj, sbs);
+    }
+    const double bden = VG[G_BDEN];
+    return make_double2(bden > 0.0 ? sbs / bden : 0.0, srs * (FX_INV * VN[3]) / VN[2]);
 }
 
 // the LONG tables from the element phase's results in LDS (all threads of
@@ -3114,58 +3233,88 @@ __device__ __forceinline__ void long_tables(LongTabs& W, SubTables& T, SubEntrie
         }
     }
     __syncthreads();
-    // (e) the donor and spot entries of each cell by position (sub_point's
-    // cursors; a donor end before a start at equal positions), and the
-    // WD/disc entries by (position, weight): the atomics' slot order is
-    // arbitrary, and long_window's double sums must not depend on it
-#ifndef LFG_ABL_LSORT
-    for (int c = tid; c < 2 * TCELLS; c += nt) {
-        const int t = c / TCELLS, g = c - t * TCELLS, base = t ? NE_W : 0;
-        const int i0 = base + (g ? W.cend[t][g - 1] : 0), i1 = base + W.cend[t][g];
-        for (int i = i0 + 1; i < i1; ++i) {
+    // (e) every cell's entries in order: each entry counts the entries of its
+    // cell that sort before it and moves to that rank (all entries at once;
+    // an insertion sort per cell took O(n^2) steps in the cells where the WD
+    // contacts crowd).  WD/disc by (position, weight), donor by position with
+    // an end before a start (sub_point's cursor), spot by (position, code):
+    // total orders, so the tables (and long_window's double sums) do not
+    // depend on the atomics' slot order
+    {
+        constexpr int RW = (NE_W + NE_D + nt - 1) / nt, RD = (TD_MAX + nt - 1) / nt;
+        double wp[RW], dp[RD], sp = 0.0;
+        long long wq[RW];
+        int wslot[RW], dc[RD], dslot[RD], sc = 0, sslot = -1;
+#pragma unroll
+        for (int r = 0; r < RW; ++r) {
+            wslot[r] = -1;
+            wp[r] = 0.0;
+            wq[r] = 0;
+            const int i = tid + r * nt, t = i < NE_W ? 0 : 1, base = t ? NE_W : 0, li = i - base;
+            if (i >= NE_W + NE_D || li >= W.cend[t][TCELLS - 1]) continue;
             const double p = W.epos[i];
             const long long q = W.ewq[i];
-            int k = i;
-            for (; k > i0 && (W.epos[k - 1] > p || (W.epos[k - 1] == p && W.ewq[k - 1] > q)); --k) {
-                W.epos[k] = W.epos[k - 1];
-                W.ewq[k] = W.ewq[k - 1];
+            const int g = tcell(p, t0, ginv), c0 = g ? W.cend[t][g - 1] : 0, c1 = W.cend[t][g];
+            int rank = 0;
+            for (int k = c0; k < c1; ++k) {
+                const double pk = W.epos[base + k];
+                const long long qk = W.ewq[base + k];
+                rank += (pk < p || (pk == p && (qk < q || (qk == q && k < li)))) ? 1 : 0;
             }
-            W.epos[k] = p;
-            W.ewq[k] = q;
+            wp[r] = p;
+            wq[r] = q;
+            wslot[r] = base + c0 + rank;
         }
-    }
-#endif
-#ifndef LFG_ABL_DSORT
-    if (tid < TCELLS) {
-#else
-    if (false) {
-#endif
-        const int i0 = tid ? T.dend[tid - 1] : 0, i1 = T.dend[tid];
-        for (int i = i0 + 1; i < i1; ++i) {
+        const int ndn = T.dend[TCELLS - 1], nsn = T.send[TCELLS - 1];
+#pragma unroll
+        for (int r = 0; r < RD; ++r) {
+            dslot[r] = -1;
+            dp[r] = 0.0;
+            dc[r] = 0;
+            const int i = tid + r * nt;
+            if (i >= ndn) continue;
             const double p = D.dpos[i];
-            const int c = D.dcode[i];
-            int k = i;
-            for (; k > i0; --k) {
-                const double pk = D.dpos[k - 1];
-                const int ck = D.dcode[k - 1];
-                if (!(pk > p || (pk == p && (c & 1) && !(ck & 1)))) break;
-                D.dpos[k] = pk;
-                D.dcode[k] = ck;
+            const int c = D.dcode[i], g = tcell(p, t0d, dginv), c0 = g ? T.dend[g - 1] : 0, c1 = T.dend[g];
+            int rank = 0;
+            for (int k = c0; k < c1; ++k) {
+                const double pk = D.dpos[k];
+                const int ck = D.dcode[k];
+                rank += (pk < p || (pk == p && ((ck & 1) > (c & 1) || ((ck & 1) == (c & 1) && (ck < c || (ck == c && k < i))))))
+                            ? 1 : 0;
             }
-            D.dpos[k] = p;
-            D.dcode[k] = c;
+            dp[r] = p;
+            dc[r] = c;
+            dslot[r] = c0 + rank;
         }
-        const int j0 = tid ? T.send[tid - 1] : 0, j1 = T.send[tid];
-        for (int i = j0 + 1; i < j1; ++i) {
-            const double p = T.spos[i];
-            const int c = T.scode[i];
-            int k = i;
-            for (; k > j0 && T.spos[k - 1] > p; --k) {
-                T.spos[k] = T.spos[k - 1];
-                T.scode[k] = T.scode[k - 1];
+        if (tid < nsn) {
+            const double p = T.spos[tid];
+            const int c = T.scode[tid], g = tcell(p, st0, sginv), c0 = g ? T.send[g - 1] : 0, c1 = T.send[g];
+            int rank = 0;
+            for (int k = c0; k < c1; ++k) {
+                const double pk = T.spos[k];
+                const int ck = T.scode[k];
+                rank += (pk < p || (pk == p && (ck < c || (ck == c && k < tid)))) ? 1 : 0;
             }
-            T.spos[k] = p;
-            T.scode[k] = c;
+            sp = p;
+            sc = c;
+            sslot = c0 + rank;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < RW; ++r)
+            if (wslot[r] >= 0) {
+                W.epos[wslot[r]] = wp[r];
+                W.ewq[wslot[r]] = wq[r];
+            }
+#pragma unroll
+        for (int r = 0; r < RD; ++r)
+            if (dslot[r] >= 0) {
+                D.dpos[dslot[r]] = dp[r];
+                D.dcode[dslot[r]] = dc[r];
+            }
+        if (sslot >= 0) {
+            T.spos[sslot] = sp;
+            T.scode[sslot] = sc;
         }
     }
     __syncthreads();
@@ -3601,29 +3750,29 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
         const double* ye = L.y + o0;
         const double* ee = L.ye + o0;
         const double fwd = Gc[G_WDF], fds = Gc[G_DF], fsp = Gc[G_SF], frs = Gc[G_RSF];
-#ifdef LFG_LONG_INTERLEAVE
-        for (int p = tid; p < n; p += nt) {
-#else
+        LongCur KC[4];
+        for (int k = 0; k < 4; ++k) KC[k] = LongCur{NAN, 0, 0};
+        SubCur SC{INFINITY, INFINITY, 0, 0, 0, 0, 0};
         for (int p = p0; p < p1; ++p) {
-#endif
             const double xp = xe[p], wp = we ? we[p] : 0.0, yp = ye[p], ep = ee[p];
             const double wk = wp < 0.0 ? 0.0 : wp;  // MODEL_SPEC 3 (NaN stays NaN)
             const double ph0 = xp - phi0, phc = wrap_phase(ph0);
 #ifdef LFG_ABL_LWD
             const double2 f2 = make_double2(phc * 1e-30, wk * 1e-30);
 #else
-            const double2 f2 = long_wd_disc(LT, phc, wk);
+            const double2 f2 = long_wd_disc(LT, KC, phc, wk);
 #endif
 #ifdef LFG_ABL_LSUB
             const double2 r2 = make_double2(phc * 1e-30, wk * 1e-30);
 #else
-            const double2 r2 = sub_point(LST, LSE, sab, sbw, sdq, LT.snorm, LT.shull, LT.sgeo, ph0, wk, S);
+            const double2 r2 = sub_point_c(LST, LSE, sab, sbw, sdq, LT.snorm, LT.shull, LT.sgeo, ph0, wk, S, SC);
 #endif
             // k_lnlike's sum, term for term (MODEL_SPEC 3: a NaN width, a NaN flux)
             const double f = isnan(wk) ? NAN : fwd * (1.0 - f2.x) + fds * (1.0 - f2.y) + fsp * r2.x / S + frs * r2.y / S;
             const double rr = (yp - f) / ep;
             chi += isnan(f) ? INFINITY : rr * rr;
         }
+        PAIR_WSTAMP(0);  // (diagnostic builds) this wave's points done
     } else if (m > 0) {
         const double s = Gc[G_S], c = Gc[G_C], ul = Gc[G_ULIMB];
         const double twd = TWO_PI * ((1.0 - ul) * 0.5 + ul / 3.0);  // 2 pi [F(1) - F(0)]

@@ -18,6 +18,8 @@ from lfit_python_amd.lfit import flux_batch  # noqa: E402
 
 dev = torch.device("cuda", 0)
 W = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+NPTS = int(sys.argv[2]) if len(sys.argv) > 2 else 300    # config 5: 1024 10000 5 (the LONG variant)
+NSUB = int(sys.argv[3]) if len(sys.argv) > 3 else 1
 L = _native.lib()
 
 
@@ -26,8 +28,9 @@ def flux_fn(pars, x, w, nsub):
     return f[0].cpu().numpy()
 
 
-model = synthetic.config_single(npts=300, flux_fn=flux_fn)
-tree = batch.compile_tree(model)
+model = synthetic.config_single(npts=NPTS, flux_fn=flux_fn, nsub=NSUB)
+tree = batch.compile_tree(model, nsub=NSUB)
+LONG = L.lfg_layout(ctypes.byref(batch.LnProbEvaluator(tree, device=dev).ctree)) == 2
 ev = batch.LnProbEvaluator(tree, device=dev, max_walkers=W)
 p0 = np.array(model.dynasty_par_vals)
 init = sampler.initialise_walkers(p0, sampler.comp_scatter(model.dynasty_par_names, 0.1), W,
@@ -46,8 +49,8 @@ span = (t[15].max() - t0.min()) / 100.0
 print("blocks %d, launch span %.2f us (first start -> last finish)" % (nb, span))
 print("block start spread: %s us" % np.percentile((t0 - t0.min()) / 100.0, [0, 50, 90, 100]).round(2))
 rows = [("candidate known", 10), ("own window (phi0)", 11), ("prologue before B0", 19), ("B0 (prologue)", 16)] + [("wave %d elements" % k, 1 + k) for k in range(8)] + [
-    ("B1 (phase barrier)", 9), ("B2 (items, norms)", 10), ("B3 (cells)", 11), ("scan", 12),
-    ("chi^2", 13), ("finish", 15)]
+    ("B1 (phase barrier)", 9)] + ([("LONG tables built", 12), ("LONG points, chi^2", 13), ("finish", 15)] if LONG else [
+    ("B2 (items, norms)", 10), ("B3 (cells)", 11), ("scan", 12), ("chi^2", 13), ("finish", 15)])
 for name, k in rows:
     if not t[k].any():
         continue
@@ -68,6 +71,7 @@ print("block finish times from launch start: %s us" % np.percentile(fin, [0, 10,
 wv = np.zeros((4, 8, 4096), dtype=np.uint64)
 if L.lfg_debug_pair_waves(ctypes.c_void_p(wv.ctypes.data)) == 0 and wv.any():
     wv = wv[:, :, :nb].astype(np.float64)
+if wv.any() and not LONG:
     b3 = t[11]
     print("sweep per wave from B3 (us): median over blocks of [earliest wave, latest wave]")
     for k, nm in enumerate(("counts", "WD/disc applied", "spot/donor applied", "after B4")):
@@ -84,5 +88,8 @@ if hasattr(L, "lfg_debug_pair_jobs") and L.lfg_debug_pair_jobs(ctypes.c_void_p(j
             sv = (jb[1, c][ok] - jb[0, c][ok]) / 100.0
             sk = (jb[2, c][ok] - jb[1, c][ok]) / 100.0
             print("  chunk %2d  solve %6.2f  sink %6.2f  (n %d)" % (c, np.median(sv), np.median(sk), ok.sum()))
-if len(sys.argv) > 2:  # raw stamps for offline analysis
-    np.save(sys.argv[2], t)
+if LONG and wv.any():
+    d = (wv[0] - t[12][None, :]) / 100.0
+    print("LONG point loop per wave after the tables (us, median over blocks): %s" % np.median(d, axis=1).round(2))
+if len(sys.argv) > 4:  # raw stamps for offline analysis
+    np.save(sys.argv[4], t)
