@@ -356,7 +356,7 @@ def run(args):
         S.emulate_rank(*args.emu)
     S.set_state(init)
     layout = L.lfg_layout(ctypes.byref(ev.ctree))
-    KERNELS = KERNELS_PAIR if layout == 1 else KERNELS_TWO
+    KERNELS = KERNELS_PAIR if layout >= 1 else KERNELS_TWO   # 2: k_pair's LONG variant
 
     # HIP events around kernels of lfg_lnprob calls (include/lfg.h LFG_NEV)
     events = []
@@ -614,6 +614,10 @@ def run(args):
                             "equivalent work, not a utilisation, and may exceed the peak"},
                 "flops_per_pair": fpp,
                 **({"flops_note": fl["note"]} if fl["note"] else {}),
+                **({"long_note": "k_pair's LONG variant executes the same element work and per sub-phase model "
+                                 "terms as k_elements + k_lnlike; its counted figure is theirs (the table lookups "
+                                 "replace the sweep's integer scan, which the count does not include)"}
+                   if layout == 2 else {}),
                 "kernels_warmup": kern,
                 "hbm": {"algorithmic_bytes_per_half_step": hbm_bytes, "achieved": hbm_gbs, "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": hbm_gbs / HBM_PEAK_GBS,
@@ -623,7 +627,8 @@ def run(args):
                                                                   "(DESIGN.md 3): an intermediate, not 8(d) work"}},
             },
             "acceptance_fraction": acc,
-            "kernel_layout": "k_pair" if layout == 1 else "k_elements + k_lnlike",
+            "kernel_layout": {1: "k_pair", 2: "k_pair (LONG: per-pair breakpoint tables in LDS, a run of points "
+                                                "per thread)"}.get(layout, "k_elements + k_lnlike"),
             **({"ranks": ranks} if ranks else {}),
             **({"exchange_ms_per_half_step": xch_ms} if (xch_ms is not None and not ranks) else {}),
             **({"emulation": emu, "emulated_rank": True} if emu else {}),

@@ -2899,143 +2899,284 @@ __device__ __forceinline__ void pair_cells(int* cell, int p, int m, double vprev
 //    element [-b, -a] is the unique one seen from -phase): the eclipsed
 //    fraction of window [lo, hi] is the integral of the covering weight,
 //      int_lo^hi C(t) dt = C(lo) (hi - lo) + sum_{lo <= pos < hi} q (hi - pos),
-//    with q = +w at a start a_k and -w at an end b_k (int64 fixed point, so
-//    C(lo) -- the cell's prefix plus its entries below lo -- is exact); a
-//    zero-width window takes the elements with a_k < ph < b_k;
+//    with q = +w at a start a_k and -w at an end b_k; each sorted entry holds
+//    C just after it (int64 fixed point, exact), so C(lo) is one read once the
+//    first entry at or above lo is found -- in its fine cell (1 024 per table
+//    over the table's own hull, a few entries even where the WD contacts
+//    crowd); a zero-width window takes the elements with a_k < ph < b_k;
 //  * spot and donor at the sub-bins: the S > 1 breakpoint tables of k_lnlike
 //    (SubTables, SubEntries, sub_point), built here from LDS.
 // Each thread takes a contiguous run of points (MODEL_SPEC 3 for every
 // width, order and wrap: no sortedness is assumed).
 constexpr int NE_W = 2 * U_WD, NE_D = 2 * U_DISC;  // WD / disc table entries (two per unique element)
+constexpr int LONG_FC = 4 * TCELLS;                 // fine cells per table (four per build cell)
 struct LongTabs {
-    long long cpre[2][TCELLS];  // WD / disc: covering weight at each cell's start
+    union {
+        long long cpre[2][TCELLS];        // build: covering weight at each cell's start
+        unsigned short fcell[2][LONG_FC];  // lookup: the first entry of each fine cell
+    };
     int cend[2][TCELLS];        // counts -> exclusive offsets -> (after the scatter) cell ends
     double epos[NE_W + NE_D];   // entries: WD [0, NE_W), disc after
-    long long ewq[NE_W + NE_D];
-    double t0, ginv, amin, bmax;  // cells over the WD/disc hull
+    long long ecb[NE_W + NE_D];  // build: q; after the sort: C just after the entry
+    double t0[2], ginv[2], amin[2], bmax[2];  // per table: cells over its hull
     double snorm[4];            // sub_point's: 1 / spot total, 1 / donor |v| sum, donor norm, |v| sum
     double shull[4];            // [2], [3]: the spot hull (sub_point)
     double sgeo[LFG_NGEO];      // the record, for sub_point's LDS reads
-    double part[6][LIKE_THREADS / 64];  // wave partials of the hulls and sums
+    double part[8][LIKE_THREADS / 64];  // wave partials of the hulls and sums
 };
+static_assert(NE_W < 65536 && NE_D < 65536, "fine cells index entries as 16-bit");
 
-// a thread's cursor into one sorted WD/disc table: the position x it stands
-// at, the first entry at or above x, and C(x) = sum of q over the entries
-// below x (exact int64).  Points that follow each other in phase move it by
-// the few entries between them; a jump to another cell starts over from the
-// cell's prefix (the same integer either way)
-struct LongCur {
-    double x;
-    int i;
-    long long C;
-};
-
-__device__ __forceinline__ void long_seek(const LongTabs& W, int t, LongCur& K, double x)
+// a value the whole block holds alike, into scalar registers
+__device__ __forceinline__ double uni(double x)
 {
-    const int base = t ? NE_W : 0, g = tcell(x, W.t0, W.ginv);
-    if (!(K.x == K.x && tcell(K.x, W.t0, W.ginv) == g)) {  // another cell (or no position yet): its prefix
-        K.C = W.cpre[t][g];
-        K.i = base + (g ? W.cend[t][g - 1] : 0);
-        const int ie = base + W.cend[t][g];
-        while (K.i < ie && W.epos[K.i] < x) K.C += W.ewq[K.i++];
-        K.x = x;
-        return;
+    const long long b = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_readfirstlane(static_cast<int>(b));
+    const int hi = __builtin_amdgcn_readfirstlane(static_cast<int>(b >> 32));
+    return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
+}
+
+// the point phase's per-pair constants, read once from LDS into scalar
+// registers: every lane's lookups and sub-bin terms use them, and the LDS
+// pipe -- which the lookups keep busy -- serves no broadcasts in the loop
+struct LongU {
+    double t0[2], g4[2], amin[2], bmax[2];  // WD/disc tables: fine cells (4 per build cell) and hulls
+    int n[2];                               // entries per table
+    double itb, ivs, dnorm, vsum, sa, sb;   // spot / donor norms, the spot hull
+    double nbs0, nbs1, nbc, fis, omf;       // the record's terms of the sub-bin sums (MODEL_SPEC 6), folded
+    double sg, cg, ibden, dsc;              // the sums' scales
+    double invS;                            // 1 / sub-bins
+    int nd, nsp;                            // donor / spot entries
+};
+
+__device__ __forceinline__ LongU long_uniforms(const LongTabs& W, const SubTables& T, int S)
+{
+    LongU K;
+    K.invS = uni(1.0 / S);
+    for (int t = 0; t < 2; ++t) {
+        K.t0[t] = uni(W.t0[t]);
+        K.g4[t] = uni(4.0 * W.ginv[t]);
+        K.amin[t] = uni(W.amin[t]);
+        K.bmax[t] = uni(W.bmax[t]);
+        K.n[t] = __builtin_amdgcn_readfirstlane(W.cend[t][TCELLS - 1]);
     }
-    const int ib = base, ie = base + W.cend[t][TCELLS - 1];
-    if (x >= K.x)
-        while (K.i < ie && W.epos[K.i] < x) K.C += W.ewq[K.i++];
-    else
-        while (K.i > ib && W.epos[K.i - 1] >= x) K.C -= W.ewq[--K.i];
-    K.x = x;
+    K.itb = uni(W.snorm[0]); K.ivs = uni(W.snorm[1]); K.dnorm = uni(W.snorm[2]); K.vsum = uni(W.snorm[3]);
+    K.sa = uni(W.shull[2]); K.sb = uni(W.shull[3]);
+    const double sg = W.sgeo[G_S], cg = W.sgeo[G_C], fis = W.sgeo[G_FIS], bden = W.sgeo[G_BDEN];
+    K.sg = uni(sg); K.cg = uni(cg); K.fis = uni(fis); K.omf = uni(1.0 - fis);
+    K.nbs0 = uni(W.sgeo[G_NB0] * sg); K.nbs1 = uni(-W.sgeo[G_NB1] * sg); K.nbc = uni(W.sgeo[G_NB2] * cg);
+    K.ibden = uni(bden > 0.0 ? 1.0 / bden : 0.0);
+    K.dsc = uni(FX_INV * W.snorm[3] / W.snorm[2]);
+    K.nd = __builtin_amdgcn_readfirstlane(T.dend[TCELLS - 1]);
+    K.nsp = __builtin_amdgcn_readfirstlane(T.send[TCELLS - 1]);
+    return K;
+}
+
+// the first entry of table t at or above x: the entries of the fine cells
+// below x's all lie below it, those of the cells above all above (the fine
+// index is monotone in position)
+#ifdef LFG_PROFILE_PAIR
+#define LONG_CNT(c, k) (c)[k]++
+#else
+#define LONG_CNT(c, k)
+#endif
+__device__ __forceinline__ int long_find(const LongTabs& W, const LongU& K, int t, double x, int* ctr = nullptr)
+{
+    const double u = (x - K.t0[t]) * K.g4[t];
+    const int f = u <= 0.0 ? 0 : (u >= double(LONG_FC - 1) ? LONG_FC - 1 : int(u));
+    const double* ep = W.epos + (t ? NE_W : 0);
+    int i = W.fcell[t][f];
+    const int ie = f < LONG_FC - 1 ? int(W.fcell[t][f + 1]) : K.n[t];
+    while (i < ie && ep[i] < x) {
+        ++i;
+        LONG_CNT(ctr, 0);
+    }
+    return i;
 }
 
 // eclipsed fraction of table t over window [lo, hi] (hi > lo): the integral
-// of the covering weight over the window / its width; the cursor ends at hi
-__device__ __forceinline__ double long_window(const LongTabs& W, int t, LongCur& K, double lo, double hi)
+// of the covering weight over the window / its width (iw = FX_INV / (hi - lo))
+__device__ __forceinline__ double long_window(const LongTabs& W, const LongU& K, int t, double lo, double hi,
+                                              double iw, int* ctr = nullptr)
 {
-    if (!(hi > W.amin && lo < W.bmax)) return 0.0;
-    long_seek(W, t, K, lo);
-    const long long C = K.C;
-    const int ie = (t ? NE_W : 0) + W.cend[t][TCELLS - 1];
+    if (!(hi > K.amin[t] && lo < K.bmax[t])) return 0.0;
+    LONG_CNT(ctr, 2);
+    const int base = t ? NE_W : 0, n = K.n[t];
+    int i = long_find(W, K, t, lo, ctr);
+    long long Cp = i ? W.ecb[base + i - 1] : 0;
+    const long long C = Cp;
     double corr = 0.0;
-    while (K.i < ie && W.epos[K.i] < hi) {
-        corr = fma(double(W.ewq[K.i]), hi - W.epos[K.i], corr);
-        K.C += W.ewq[K.i++];
+    for (; i < n && W.epos[base + i] < hi; ++i) {
+        const long long cb = W.ecb[base + i];
+        corr = fma(double(cb - Cp), hi - W.epos[base + i], corr);
+        Cp = cb;
+        LONG_CNT(ctr, 1);
     }
-    K.x = hi;
-    return fma(corr, FX_INV / (hi - lo), double(C) * FX_INV);
+    return fma(corr, iw, double(C) * FX_INV);
 }
 
 // table t at a point (zero-width window): the elements with a_k < ph < b_k
 // (the starts below ph, the ends at or below it)
-__device__ __forceinline__ double long_point(const LongTabs& W, int t, LongCur& K, double ph)
+__device__ __forceinline__ double long_point(const LongTabs& W, const LongU& K, int t, double ph)
 {
-    if (!(ph > W.amin && ph < W.bmax)) return 0.0;
-    long_seek(W, t, K, ph);
-    long long C = K.C;
-    const int ie = (t ? NE_W : 0) + W.cend[t][TCELLS - 1];
-    for (int i = K.i; i < ie && W.epos[i] == ph; ++i)
-        if (W.ewq[i] < 0) C += W.ewq[i];
+    if (!(ph > K.amin[t] && ph < K.bmax[t])) return 0.0;
+    const int base = t ? NE_W : 0, n = K.n[t];
+    int i = long_find(W, K, t, ph);
+    long long Cp = i ? W.ecb[base + i - 1] : 0, C = Cp;
+    for (; i < n && W.epos[base + i] == ph; ++i) {
+        const long long cb = W.ecb[base + i];
+        if (cb - Cp < 0) C += cb - Cp;
+        Cp = cb;
+    }
     return double(C) * FX_INV;
 }
 
 // WD and disc eclipsed fractions of a point's window (phase phc, half-width
 // wk >= 0): the unique elements over [lo, hi] and, for their mirrors, over
-// [-hi, -lo]; K: the thread's four cursors (WD, disc) x (window, mirror)
-__device__ __forceinline__ double2 long_wd_disc(const LongTabs& W, LongCur (&K)[4], double phc, double wk)
+// [-hi, -lo]
+__device__ __forceinline__ double2 long_wd_disc(const LongTabs& W, const LongU& K, double phc, double wk,
+                                               int* ctr = nullptr)
 {
     if (wk > 0.0) {
-        const double lo = phc - wk, hi = phc + wk;
-        return make_double2(long_window(W, 0, K[0], lo, hi) + long_window(W, 0, K[1], -hi, -lo),
-                            long_window(W, 1, K[2], lo, hi) + long_window(W, 1, K[3], -hi, -lo));
+        const double lo = phc - wk, hi = phc + wk, iw = FX_INV / (hi - lo);  // -lo - -hi = hi - lo exactly
+        return make_double2(long_window(W, K, 0, lo, hi, iw, ctr) + long_window(W, K, 0, -hi, -lo, iw, ctr),
+                            long_window(W, K, 1, lo, hi, iw, ctr) + long_window(W, K, 1, -hi, -lo, iw, ctr));
     }
-    return make_double2(long_point(W, 0, K[0], phc) + long_point(W, 0, K[1], -phc),
-                        long_point(W, 1, K[2], phc) + long_point(W, 1, K[3], -phc));
+    return make_double2(long_point(W, K, 0, phc) + long_point(W, K, 0, -phc),
+                        long_point(W, K, 1, phc) + long_point(W, K, 1, -phc));
 }
 
 // sub_point with its donor cursor carried from point to point (SubCur): a
 // point whose first sub-bin lies at or above the last one's phase walks on
 // from there instead of a fresh lookup (a thread's run of sorted points);
 // the line of sight is formed afresh at each point's first sub-bin
+// the donor cursor runs two entries ahead: the next entry's position, code
+// and tile vector (raw, LDS) and the one after's position and code are in
+// registers, their loads issued a crossing earlier -- a crossing applies the
+// vector and moves the pipe on without waiting on LDS
 struct SubCur {
-    double ph, npos;
+    double ph, npos, n2pos;
+    double nq[3];
     long long vx, vy, vz;
-    int cur, ncode;
+    int cur, ncode, n2code;
+#ifdef LFG_SPOT_CARRY
+    // the spot cursor, carried from sub-bin to sub-bin and point to point:
+    // every entry at or below shi counted into sC, scur the first above,
+    // snpos its position
+    double shi, snpos;
+    long long sC;
+    int scur;
+#endif
 };
 
-__device__ __forceinline__ double2 sub_point_c(const SubTables& T, const SubEntries& D, const double2* sab,
-                                               const double* sbw, const double* sdq, const double* snorm,
-                                               const double* shull, const double* SG, double ph0, double wk, int S,
-                                               SubCur& U)
+__device__ __forceinline__ void subcur_fill(const SubEntries& D, const double* sdq, int nd, SubCur& U)
 {
-    using lds_cvd = const volatile __attribute__((address_space(3))) double*;
-    const lds_cvd VG = (lds_cvd)SG;
-    const lds_cvd VN = (lds_cvd)snorm;
-    const int nd = T.dend[TCELLS - 1], nsp = T.send[TCELLS - 1];
-    const double h = wk / S, ih = 0.5 / h;
-    double sbs = 0.0, srs = 0.0, sn = 0.0, cs = 1.0, rs = 0.0, rc = 1.0;
+    U.npos = U.cur < nd ? D.dpos[U.cur] : INFINITY;
+    U.ncode = U.cur < nd ? D.dcode[U.cur] : 0;
+    U.n2pos = U.cur + 1 < nd ? D.dpos[U.cur + 1] : INFINITY;
+    U.n2code = U.cur + 1 < nd ? D.dcode[U.cur + 1] : 0;
+    const double* dq = sdq + ((U.ncode >> 1) >> 2) * DON_STRIDE;
+    U.nq[0] = dq[0]; U.nq[1] = dq[1]; U.nq[2] = dq[2];
+}
+
+// a point's estimated cost in the LONG point phase (the partition of the
+// points over the threads): windows in the WD/disc hulls walk the tables,
+// those in the spot hull the spot entries at every sub-bin
+__device__ __forceinline__ int long_weight(const LongU& K, double ph0, double w)
+{
+    const double phc = wrap_phase(ph0), wk = w < 0.0 ? 0.0 : w, lo = phc - wk, hi = phc + wk;
+    bool wd = false;
+    for (int t = 0; t < 2; ++t)
+        wd = wd || (hi >= K.amin[t] && lo <= K.bmax[t]) || (-lo >= K.amin[t] && -hi <= K.bmax[t]);
+    const bool sp = hi >= K.sa && lo <= K.sb;
+    return 5 + (wd ? 8 : 0) + (sp ? 2 : 0);  // from the per-wave times of equal runs (profiles/r05)
+}
+
+// a crossing of entry cur: its vector into V (donor_apply's arithmetic), then
+// the pipe one entry on
+__device__ __forceinline__ void subcur_cross(const SubEntries& D, const double* sdq, int nd, double ivs, SubCur& U)
+{
+    const int code = U.ncode, mr = (code >> 1) & 3;
+    const long long qx = to_fx(U.nq[0] * ivs);
+    const long long qy = to_fx(((mr & 1) ? -U.nq[1] : U.nq[1]) * ivs);
+    const long long qz = to_fx(((mr & 2) ? -U.nq[2] : U.nq[2]) * ivs);
+    if (code & 1) { U.vx -= qx; U.vy -= qy; U.vz -= qz; }
+    else { U.vx += qx; U.vy += qy; U.vz += qz; }
+    ++U.cur;
+    U.npos = U.n2pos;
+    U.ncode = U.n2code;
+    const double* dq = sdq + ((U.ncode >> 1) >> 2) * DON_STRIDE;
+    U.nq[0] = dq[0]; U.nq[1] = dq[1]; U.nq[2] = dq[2];
+    U.n2pos = U.cur + 1 < nd ? D.dpos[U.cur + 1] : INFINITY;
+    U.n2code = U.cur + 1 < nd ? D.dcode[U.cur + 1] : 0;
+}
+
+__device__ __forceinline__ double2 sub_point_c(const SubTables& T, const SubEntries& D, const double2* sab,
+                                               const double* sbw, const double* sdq, const LongU& K, double ph0,
+                                               double wk, int S, SubCur& U)
+{
+    const int nd = K.nd, nsp = K.nsp;
+    const double h = wk * K.invS, ih = 0.5 / h;
+    // the first sub-bin's line of sight and the turn per sub-bin (both paths)
+    const double phA = wrap_phase(ph0 - wk + h);
+    const double4 eA = sincospi2_ool(2.0 * phA, 4.0 * h);
+#ifdef LFG_QUIET_FAST
+    if (h > 0.0) {
+        // the quiet point -- most of them: no donor entry crossed within it,
+        // its sub-bins all off the spot's hull, no wrap -- takes the sums in
+        // closed form over the rotated line of sight: V is constant, the
+        // spot is uneclipsed, so sum_j V . e_j = V . sum_j e_j and the beaming
+        // term needs only max(nb . e_j, 0) per sub-bin
+        const double phZ = wrap_phase(ph0 - wk + (2 * S - 1) * h);
+        if (phA >= U.ph && phZ >= phA && !donor_counted(U.npos, U.ncode, phZ) &&
+            (phZ + h <= K.sa || phA - h >= K.sb)) {
+            double sn = eA.x, cs = eA.y, scs = 0.0, ssn = 0.0, smx = 0.0;
+            for (int j = 0; j < S; ++j) {
+                scs += cs;
+                ssn += sn;
+                smx += fmax(fma(K.nbs0, cs, fma(K.nbs1, sn, K.nbc)), 0.0);
+                const double c2 = fma(cs, eA.w, -sn * eA.z);
+                sn = fma(sn, eA.w, cs * eA.z);
+                cs = c2;
+            }
+            U.ph = phZ;
+            const double sbs = fma(K.omf, smx, S * K.fis);
+            const double srs1 = fma(double(U.vx), scs, -double(U.vy) * ssn), srs2 = S * double(U.vz);
+            return make_double2(sbs * K.ibden, fma(K.sg, srs1, K.cg * srs2) * K.dsc);
+        }
+    }
+#endif
+    double sbs = 0.0, srs1 = 0.0, srs2 = 0.0, sn = 0.0, cs = 1.0, rs = 0.0, rc = 1.0;
     long long Cs = 0;
     int scur = 0;
     bool sv = false;  // Cs / scur hold C at this sub-bin's lo
     for (int j = 0; j < S; ++j) {
         const double phn = wrap_phase(ph0 - wk + (2 * j + 1) * h);
         bool chg = false;
+#ifdef LFG_ABL_SC_DONOR
+        if (false) {
+#else
         if (!(phn >= U.ph)) {  // a fresh lookup (the first point, a step back in phase)
-            U.cur = sub_donor(T, D, sdq, VN[1], phn, U.vx, U.vy, U.vz);
-            U.npos = U.cur < nd ? D.dpos[U.cur] : INFINITY;
-            U.ncode = U.cur < nd ? D.dcode[U.cur] : 0;
+#endif
+            U.cur = sub_donor(T, D, sdq, K.ivs, phn, U.vx, U.vy, U.vz);
+            subcur_fill(D, sdq, nd, U);
             chg = true;
         } else {
+#ifndef LFG_ABL_SC_DONOR
             while (donor_counted(U.npos, U.ncode, phn)) {  // npos = inf past the last entry
-                donor_apply(sdq, U.ncode, VN[1], U.vx, U.vy, U.vz);
+#else
+            while (false) {
+#endif
+                subcur_cross(D, sdq, nd, K.ivs, U);
                 chg = true;
-                ++U.cur;
-                U.npos = U.cur < nd ? D.dpos[U.cur] : INFINITY;
-                U.ncode = U.cur < nd ? D.dcode[U.cur] : 0;
             }
         }
+#ifdef LFG_ABL_SC_TRIG
+        if (j == 0) {
+            const double4 e4 = make_double4(phn, 1.0 - phn * phn, h, 1.0 - h);
+#else
         if (j == 0 || !(phn >= U.ph)) {
-            const double4 e4 = sincospi2_ool(2.0 * phn, 4.0 * h);  // the turn per sub-bin: 2 pi (2 h)
+            const double4 e4 = j == 0 ? eA : sincospi2_ool(2.0 * phn, 4.0 * h);  // the turn per sub-bin: 2 pi (2 h)
+#endif
             sn = e4.x;
             cs = e4.y;
             rs = e4.z;
@@ -3051,9 +3192,51 @@ __device__ __forceinline__ double2 sub_point_c(const SubTables& T, const SubEntr
         double ebj = 0.0;
         const double lo = phn - h, hi = phn + h;
         if (!(h > 0.0)) {
-            ebj = sub_spot(T, sab, sbw, VN[0], lo, hi, shull[2], shull[3]);
-        } else if (hi > shull[2] && lo < shull[3]) {
-            const double itb = VN[0];
+            ebj = sub_spot(T, sab, sbw, K.itb, lo, hi, K.sa, K.sb);
+#ifdef LFG_ABL_SC_SPOT
+        } else if (false) {
+#else
+        } else if (hi > K.sa && lo < K.sb) {
+#endif
+            const double itb = K.itb;
+#ifdef LFG_SPOT_CARRY
+            if (!(lo >= U.shi)) {  // a fresh lookup (the first window, a step back)
+                U.sC = spot_C(T, sbw, itb, lo, U.scur);
+                U.snpos = U.scur < nsp ? T.spos[U.scur] : INFINITY;
+            } else {
+                while (U.snpos <= lo) {  // the entries since the last window's hi
+                    const int code = T.scode[U.scur];
+                    const long long Wq = to_fx(sbw[code >> 1] * itb);
+                    U.sC += (code & 1) ? -Wq : Wq;
+                    ++U.scur;
+                    U.snpos = U.scur < nsp ? T.spos[U.scur] : INFINITY;
+                }
+            }
+            long long Cn = U.sC;
+            double corr = 0.0;
+            while (U.snpos <= hi) {
+                const int code = T.scode[U.scur], k = code >> 1;
+                const double wn = sbw[k] * itb;
+                const double2 ab = sab[k];
+                const long long Wq = to_fx(wn);
+                if (!(code & 1)) {
+                    Cn += Wq;
+                    corr = fma(wn, fmin(ab.y, hi) - ab.x, corr);
+                } else {
+                    Cn -= Wq;
+                    if (ab.x <= lo) corr = fma(-wn, hi - ab.y, corr);
+                }
+                ++U.scur;
+                U.snpos = U.scur < nsp ? T.spos[U.scur] : INFINITY;
+            }
+            ebj = fma(corr, ih, double(U.sC) * FX_INV);
+            U.sC = Cn;
+            U.shi = hi;
+            (void)sv; (void)Cs; (void)scur;
+        } else {
+            sv = false;
+        }
+#else
             if (!sv) Cs = spot_C(T, sbw, itb, lo, scur);
             sv = true;
             long long Cn = Cs;
@@ -3076,14 +3259,14 @@ __device__ __forceinline__ double2 sub_point_c(const SubTables& T, const SubEntr
         } else {
             sv = false;
         }
-        const double sg = VG[G_S], cg = VG[G_C];
-        const double e0 = sg * cs, e1 = -sg * sn;
-        srs = fma(e0, double(U.vx), fma(e1, double(U.vy), fma(cg, double(U.vz), srs)));
-        const double fis = VG[G_FIS];
-        sbs = fma(fis + (1.0 - fis) * fmax(VG[G_NB0] * e0 + VG[G_NB1] * e1 + VG[G_NB2] * cg, 0.0), 1.0 - ebj, sbs);
+#endif
+        // e = (s cos, -s sin, c) at the sub-phase: the donor term V . e and
+        // the spot's beaming term fis + (1 - fis) max(nb . e, 0) (sg, cg folded in)
+        srs1 = fma(cs, double(U.vx), fma(-sn, double(U.vy), srs1));
+        srs2 += double(U.vz);
+        sbs = fma(fma(K.omf, fmax(fma(K.nbs0, cs, fma(K.nbs1, sn, K.nbc)), 0.0), K.fis), 1.0 - ebj, sbs);
     }
-    const double bden = VG[G_BDEN];
-    return make_double2(bden > 0.0 ? sbs / bden : 0.0, srs * (FX_INV * VN[3]) / VN[2]);
+    return make_double2(sbs * K.ibden, fma(K.sg, srs1, K.cg * srs2) * K.dsc);
 }
 
 // the LONG tables from the element phase's results in LDS (all threads of
@@ -3100,33 +3283,50 @@ __device__ __forceinline__ void long_tables(LongTabs& W, SubTables& T, SubEntrie
     constexpr int nt = LIKE_THREADS, nw = LIKE_THREADS / 64;
     const int lane = tid & 63, wv = tid >> 6;
     // (a) hulls of the WD/disc and spot intervals, the donor |v| sum
-    double amin = INFINITY, bmax = -INFINITY, sa = INFINITY, sb = -INFINITY, vs = 0.0;
+    double amin[2] = {INFINITY, INFINITY}, bmax[2] = {-INFINITY, -INFINITY}, sa = INFINITY, sb = -INFINITY, vs = 0.0;
     for (int g = tid; g < NU_WDD; g += nt) {
         const double2 ab = abw[g];
-        if (ab.x < ab.y) { amin = fmin(amin, ab.x); bmax = fmax(bmax, ab.y); }
+        const int t = uitem(g) < U_WD ? 0 : 1;
+        if (ab.x < ab.y) {
+            amin[t] = fmin(amin[t], ab.x);
+            bmax[t] = fmax(bmax[t], ab.y);
+        }
     }
     if (tid < NBS && sab[tid].x < sab[tid].y) { sa = sab[tid].x; sb = sab[tid].y; }
     if (tid < U_DON)  // the four mirror images of a tile have the same |vx| + |vy| + |vz|
         vs = 4.0 * (fabs(sdq[tid * DON_STRIDE]) + fabs(sdq[tid * DON_STRIDE + 1]) + fabs(sdq[tid * DON_STRIDE + 2]));
-    amin = wave_min(amin); bmax = wave_max(bmax); sa = wave_min(sa); sb = wave_max(sb); vs = wave_sum(vs);
-    if (lane == 0) { W.part[0][wv] = amin; W.part[1][wv] = bmax; W.part[2][wv] = sa; W.part[3][wv] = sb; W.part[4][wv] = vs; }
+    for (int t = 0; t < 2; ++t) {
+        amin[t] = wave_min(amin[t]);
+        bmax[t] = wave_max(bmax[t]);
+    }
+    sa = wave_min(sa); sb = wave_max(sb); vs = wave_sum(vs);
+    if (lane == 0) {
+        W.part[0][wv] = amin[0]; W.part[1][wv] = bmax[0]; W.part[2][wv] = sa; W.part[3][wv] = sb; W.part[4][wv] = vs;
+        W.part[5][wv] = amin[1]; W.part[6][wv] = bmax[1];
+    }
     __syncthreads();
-    amin = INFINITY; bmax = -INFINITY; sa = INFINITY; sb = -INFINITY; vs = 0.0;
+    amin[0] = amin[1] = INFINITY; bmax[0] = bmax[1] = -INFINITY; sa = INFINITY; sb = -INFINITY; vs = 0.0;
     for (int k = 0; k < nw; ++k) {  // every thread forms the block's values (no barrier for a broadcast)
-        amin = fmin(amin, W.part[0][k]); bmax = fmax(bmax, W.part[1][k]);
+        amin[0] = fmin(amin[0], W.part[0][k]); bmax[0] = fmax(bmax[0], W.part[1][k]);
+        amin[1] = fmin(amin[1], W.part[5][k]); bmax[1] = fmax(bmax[1], W.part[6][k]);
         sa = fmin(sa, W.part[2][k]); sb = fmax(sb, W.part[3][k]); vs += W.part[4][k];
     }
-    const double t0 = amin, ginv = (bmax > amin) ? TCELLS / (bmax - amin) : 0.0;
+    // the cells of table t over its own hull (the WD contacts crowd a narrower one)
+    double t0[2], ginv[2];
+    for (int t = 0; t < 2; ++t) {
+        t0[t] = amin[t];
+        ginv[t] = (bmax[t] > amin[t]) ? TCELLS / (bmax[t] - amin[t]) : 0.0;
+    }
     const double st0 = sa, sginv = (sb > sa) ? TCELLS / (sb - sa) : 0.0;
     constexpr double t0d = -0.5, t1d = 0.5, dginv = TCELLS;  // donor cells: the whole phase circle
     const double itb = 1.0 / (double(static_cast<long long>(stot[0])) * (FX_INV / PAIR_SPOT_S)), ivs = 1.0 / vs;
     if (tid == 0) {
-        W.t0 = t0; W.ginv = ginv; W.amin = amin; W.bmax = bmax;
+        for (int t = 0; t < 2; ++t) { W.t0[t] = t0[t]; W.ginv[t] = ginv[t]; W.amin[t] = amin[t]; W.bmax[t] = bmax[t]; }
         W.snorm[0] = itb;
         W.snorm[1] = ivs;
         W.snorm[2] = double(static_cast<long long>(stot[1])) * (FX_INV / PAIR_DON_S);
         W.snorm[3] = vs;
-        W.shull[0] = amin; W.shull[1] = bmax; W.shull[2] = sa; W.shull[3] = sb;
+        W.shull[0] = fmin(amin[0], amin[1]); W.shull[1] = fmax(bmax[0], bmax[1]); W.shull[2] = sa; W.shull[3] = sb;
         T.dt0 = t0d; T.dginv = dginv; T.st0 = st0; T.sginv = sginv;
     }
     // (b) counts and fixed-point sums per cell
@@ -3143,7 +3343,7 @@ __device__ __forceinline__ void long_tables(LongTabs& W, SubTables& T, SubEntrie
         int t;
         long long q;
         if (!wd_entry(g, ab, t, q)) continue;
-        const int ga = tcell(ab.x, t0, ginv), gb = tcell(ab.y, t0, ginv);
+        const int ga = tcell(ab.x, t0[t], ginv[t]), gb = tcell(ab.y, t0[t], ginv[t]);
         atomicAdd(&W.cend[t][ga], 1);
         atomicAdd(&W.cend[t][gb], 1);
         atomicAdd(reinterpret_cast<unsigned long long*>(&W.cpre[t][ga]), static_cast<unsigned long long>(q));
@@ -3204,12 +3404,12 @@ __device__ __forceinline__ void long_tables(LongTabs& W, SubTables& T, SubEntrie
         long long q;
         if (!wd_entry(g, ab, t, q)) continue;
         const int base = t ? NE_W : 0;
-        const int ia = atomicAdd(&W.cend[t][tcell(ab.x, t0, ginv)], 1);
+        const int ia = atomicAdd(&W.cend[t][tcell(ab.x, t0[t], ginv[t])], 1);
         W.epos[base + ia] = ab.x;
-        W.ewq[base + ia] = q;
-        const int ib = atomicAdd(&W.cend[t][tcell(ab.y, t0, ginv)], 1);
+        W.ecb[base + ia] = q;
+        const int ib = atomicAdd(&W.cend[t][tcell(ab.y, t0[t], ginv[t])], 1);
         W.epos[base + ib] = ab.y;
-        W.ewq[base + ib] = -q;
+        W.ecb[base + ib] = -q;
     }
     {
         double p0, p1;
@@ -3239,7 +3439,8 @@ __device__ __forceinline__ void long_tables(LongTabs& W, SubTables& T, SubEntrie
     // contacts crowd).  WD/disc by (position, weight), donor by position with
     // an end before a start (sub_point's cursor), spot by (position, code):
     // total orders, so the tables (and long_window's double sums) do not
-    // depend on the atomics' slot order
+    // depend on the atomics' slot order.  A WD/disc entry leaves C just after
+    // it: its cell's prefix, the weights of the entries before it, its own
     {
         constexpr int RW = (NE_W + NE_D + nt - 1) / nt, RD = (TD_MAX + nt - 1) / nt;
         double wp[RW], dp[RD], sp = 0.0;
@@ -3253,16 +3454,20 @@ __device__ __forceinline__ void long_tables(LongTabs& W, SubTables& T, SubEntrie
             const int i = tid + r * nt, t = i < NE_W ? 0 : 1, base = t ? NE_W : 0, li = i - base;
             if (i >= NE_W + NE_D || li >= W.cend[t][TCELLS - 1]) continue;
             const double p = W.epos[i];
-            const long long q = W.ewq[i];
-            const int g = tcell(p, t0, ginv), c0 = g ? W.cend[t][g - 1] : 0, c1 = W.cend[t][g];
+            const long long q = W.ecb[i];
+            const int g = tcell(p, t0[t], ginv[t]), c0 = g ? W.cend[t][g - 1] : 0, c1 = W.cend[t][g];
             int rank = 0;
+            long long cb = W.cpre[t][g] + q;
+#pragma unroll 4
             for (int k = c0; k < c1; ++k) {
                 const double pk = W.epos[base + k];
-                const long long qk = W.ewq[base + k];
-                rank += (pk < p || (pk == p && (qk < q || (qk == q && k < li)))) ? 1 : 0;
+                const long long qk = W.ecb[base + k];
+                const bool before = pk < p || (pk == p && (qk < q || (qk == q && k < li)));
+                rank += before ? 1 : 0;
+                cb += before ? qk : 0;
             }
             wp[r] = p;
-            wq[r] = q;
+            wq[r] = cb;
             wslot[r] = base + c0 + rank;
         }
         const int ndn = T.dend[TCELLS - 1], nsn = T.send[TCELLS - 1];
@@ -3276,6 +3481,7 @@ __device__ __forceinline__ void long_tables(LongTabs& W, SubTables& T, SubEntrie
             const double p = D.dpos[i];
             const int c = D.dcode[i], g = tcell(p, t0d, dginv), c0 = g ? T.dend[g - 1] : 0, c1 = T.dend[g];
             int rank = 0;
+#pragma unroll 4
             for (int k = c0; k < c1; ++k) {
                 const double pk = D.dpos[k];
                 const int ck = D.dcode[k];
@@ -3290,6 +3496,7 @@ __device__ __forceinline__ void long_tables(LongTabs& W, SubTables& T, SubEntrie
             const double p = T.spos[tid];
             const int c = T.scode[tid], g = tcell(p, st0, sginv), c0 = g ? T.send[g - 1] : 0, c1 = T.send[g];
             int rank = 0;
+#pragma unroll 4
             for (int k = c0; k < c1; ++k) {
                 const double pk = T.spos[k];
                 const int ck = T.scode[k];
@@ -3304,7 +3511,7 @@ __device__ __forceinline__ void long_tables(LongTabs& W, SubTables& T, SubEntrie
         for (int r = 0; r < RW; ++r)
             if (wslot[r] >= 0) {
                 W.epos[wslot[r]] = wp[r];
-                W.ewq[wslot[r]] = wq[r];
+                W.ecb[wslot[r]] = wq[r];
             }
 #pragma unroll
         for (int r = 0; r < RD; ++r)
@@ -3316,6 +3523,26 @@ __device__ __forceinline__ void long_tables(LongTabs& W, SubTables& T, SubEntrie
             T.spos[sslot] = sp;
             T.scode[sslot] = sc;
         }
+    }
+    __syncthreads();
+    // (f) the fine index (over cpre, now spent): a thread per build cell
+    // counts its sorted entries below each of its four fine cells
+    if (tid < 2 * TCELLS) {
+        const int t = tid / TCELLS, g = tid % TCELLS, base = t ? NE_W : 0;
+        const int c0 = g ? W.cend[t][g - 1] : 0, c1 = W.cend[t][g];
+        const double fg = 4.0 * ginv[t];
+        int k = c0;
+        unsigned short f4[4];
+        for (int j = 0; j < 4; ++j) {
+            const int f = 4 * g + j;
+            for (; k < c1; ++k) {  // entries of fine cell < f (the same clamped index as long_find)
+                const double u = (W.epos[base + k] - t0[t]) * fg;
+                const int fk = u <= 0.0 ? 0 : (u >= double(LONG_FC - 1) ? LONG_FC - 1 : int(u));
+                if (fk >= f) break;
+            }
+            f4[j] = static_cast<unsigned short>(k);
+        }
+        for (int j = 0; j < 4; ++j) W.fcell[t][4 * g + j] = f4[j];
     }
     __syncthreads();
 }
@@ -3487,6 +3714,7 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
             LST.dend[tid] = LST.send[tid] = 0;
         } else if (tid < TCELLS + 3) {
             LST.dv0[tid - TCELLS] = 0;
+
         } else if (tid >= nt - LFG_NGEO) {
             LT.sgeo[tid - (nt - LFG_NGEO)] = G[tid - (nt - LFG_NGEO)];
         }
@@ -3744,35 +3972,133 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
         long_tables(LT, LST, LSE, Lab, sab, sbw, sdq, swt, stot, ul, 1.0 / (TWO_PI * ((1.0 - ul) * 0.5 + ul / 3.0)),
                     lspart, tid);
         PAIR_STAMP(12, tid == 0);
-        const int S = L.nsub, R = (n + nt - 1) / nt, p0 = tid * R, p1 = min(p0 + R, n);
+        const int S = L.nsub;
         const double* xe = L.x + o0;
         const double* we = L.w ? L.w + o0 : nullptr;
         const double* ye = L.y + o0;
         const double* ee = L.ye + o0;
         const double fwd = Gc[G_WDF], fds = Gc[G_DF], fsp = Gc[G_SF], frs = Gc[G_RSF];
-        LongCur KC[4];
-        for (int k = 0; k < 4; ++k) KC[k] = LongCur{NAN, 0, 0};
-        SubCur SC{INFINITY, INFINITY, 0, 0, 0, 0, 0};
+#ifdef LFG_PROFILE_PAIR
+        unsigned long long tl_wd = 0, tl_sub = 0;
+        int lctr[3] = {0, 0, 0};
+#endif
+        SubCur SC{INFINITY, INFINITY, INFINITY, {0.0, 0.0, 0.0}, 0, 0, 0, 0, 0, 0
+#ifdef LFG_SPOT_CARRY
+                  , INFINITY, INFINITY, 0, 0
+#endif
+        };
+        const LongU KU = long_uniforms(LT, LST, S);
+        const double fspS = uni(fsp / S), frsS = uni(frs / S);
+        // a contiguous run of points per thread: its donor cursor walks on
+        // from point to point (a dynamic queue of 4-point chunks balanced the
+        // eclipse's points over the waves but doubled the total: every chunk
+        // starts with fresh lookups; and its chi^2 order was not fixed)
+        // The runs are cut where the running estimated cost (long_weight, in
+        // index order) passes equal shares: a thread in the eclipse takes
+        // fewer points, and the waves end together (the eclipse's waves took
+        // 2-3 times the others' time with equal counts)
+        int p0, p1;
+        {
+            const int R = (n + nt - 1) / nt, c0 = min(tid * R, n), c1 = min(c0 + R, n);
+            long long v[1] = {0};
+            for (int p = c0; p < c1; ++p) v[0] += long_weight(KU, xe[p] - phi0, we ? we[p] : 0.0);
+            const long long own = v[0];
+            cell_scan<1>(v, lspart, tid);  // exclusive prefix over the chunks (a barrier inside)
+            int* pre = reinterpret_cast<int*>(Lab);  // the WD/disc intervals are spent
+            pre[tid] = int(v[0]);
+            if (tid == nt - 1) pre[nt] = int(v[0] + own);
+            __syncthreads();
+            const long long T = pre[nt];
+            auto start = [&](int t) {  // the first point whose cost before it reaches t / nt of the total
+                if (t <= 0) return 0;
+                if (t >= nt) return n;
+                const long long tgt = (T * t) / nt;
+                if (tgt <= 0) return 0;
+                int a = 0, b = nt - 1;  // the last chunk with prefix < tgt
+                while (a < b) {
+                    const int mid = (a + b + 1) >> 1;
+                    if (pre[mid] < tgt) a = mid;
+                    else b = mid - 1;
+                }
+                long long cum = pre[a];
+                const int e = min(a * R + R, n);
+                for (int p = min(a * R, n); p < e; ++p) {
+                    if (cum >= tgt) return p;
+                    cum += long_weight(KU, xe[p] - phi0, we ? we[p] : 0.0);
+                }
+                return e;
+            };
+            p0 = start(tid);
+            p1 = start(tid + 1);
+        }
+        {
+            double xn = p0 < p1 ? xe[p0] : 0.0, wn = (p0 < p1 && we) ? we[p0] : 0.0;
         for (int p = p0; p < p1; ++p) {
-            const double xp = xe[p], wp = we ? we[p] : 0.0, yp = ye[p], ep = ee[p];
+#ifdef LFG_ABL_GLOAD  // (diagnostic builds) no global loads in the point loop: a synthetic grid
+            const double xp = -0.3 + p * 6.0006e-5, wp = 3.0003e-5, yp = 1.0, ep = 0.004;
+            (void)xn; (void)wn;
+#else
+            const double xp = xn, wp = wn, yp = ye[p], ep = ee[p];
+            if (p + 1 < p1) {  // the next point's phase and width, in flight during this one
+                xn = xe[p + 1];
+                wn = we ? we[p + 1] : 0.0;
+            }
+#endif
             const double wk = wp < 0.0 ? 0.0 : wp;  // MODEL_SPEC 3 (NaN stays NaN)
             const double ph0 = xp - phi0, phc = wrap_phase(ph0);
+#ifdef LFG_PROFILE_PAIR  // per-lane cycles of the two model parts (the wave's max lane: g_pair_w[1..2])
+            const unsigned long long tq0 = __builtin_amdgcn_s_memtime();
+#endif
 #ifdef LFG_ABL_LWD
             const double2 f2 = make_double2(phc * 1e-30, wk * 1e-30);
 #else
-            const double2 f2 = long_wd_disc(LT, KC, phc, wk);
+#ifdef LFG_PROFILE_PAIR
+            const double2 f2 = long_wd_disc(LT, KU, phc, wk, lctr);
+#else
+            const double2 f2 = long_wd_disc(LT, KU, phc, wk);
+#endif
+#endif
+#ifdef LFG_PROFILE_PAIR
+            __builtin_amdgcn_s_waitcnt(0);
+            const unsigned long long tq1 = __builtin_amdgcn_s_memtime();
+            tl_wd += (tq1 - tq0) + (f2.x == 12345.0 ? 1 : 0);
 #endif
 #ifdef LFG_ABL_LSUB
             const double2 r2 = make_double2(phc * 1e-30, wk * 1e-30);
 #else
-            const double2 r2 = sub_point_c(LST, LSE, sab, sbw, sdq, LT.snorm, LT.shull, LT.sgeo, ph0, wk, S, SC);
+            const double2 r2 = sub_point_c(LST, LSE, sab, sbw, sdq, KU, ph0, wk, S, SC);
+#endif
+#ifdef LFG_PROFILE_PAIR
+            __builtin_amdgcn_s_waitcnt(0);
+            tl_sub += (__builtin_amdgcn_s_memtime() - tq1) + (r2.x == 12345.0 ? 1 : 0);
 #endif
             // k_lnlike's sum, term for term (MODEL_SPEC 3: a NaN width, a NaN flux)
-            const double f = isnan(wk) ? NAN : fwd * (1.0 - f2.x) + fds * (1.0 - f2.y) + fsp * r2.x / S + frs * r2.y / S;
+            const double f = isnan(wk) ? NAN : fwd * (1.0 - f2.x) + fds * (1.0 - f2.y) + fspS * r2.x + frsS * r2.y;
             const double rr = (yp - f) / ep;
             chi += isnan(f) ? INFINITY : rr * rr;
         }
+        }
         PAIR_WSTAMP(0);  // (diagnostic builds) this wave's points done
+#ifdef LFG_PROFILE_PAIR
+        {
+            unsigned long long a = tl_wd, b = tl_sub;
+            for (int off = 32; off > 0; off >>= 1) {
+                a = max(a, (unsigned long long)__shfl_xor((long long)a, off));
+                b = max(b, (unsigned long long)__shfl_xor((long long)b, off));
+            }
+            if (lane == 0 && blockIdx.x < 4096) { g_pair_w[1][wv][blockIdx.x] = a; g_pair_w[2][wv][blockIdx.x] = b; }
+            // walk steps / window entries / windows in a hull: the wave's max lane (16 bits each)
+            int c0 = lctr[0], c1 = lctr[1], c2 = lctr[2];
+            for (int off = 32; off > 0; off >>= 1) {
+                c0 = max(c0, __shfl_xor(c0, off));
+                c1 = max(c1, __shfl_xor(c1, off));
+                c2 = max(c2, __shfl_xor(c2, off));
+            }
+            if (lane == 0 && blockIdx.x < 4096)
+                g_pair_w[3][wv][blockIdx.x] = (unsigned long long)(c0 & 0xffff) | ((unsigned long long)(c1 & 0xffff) << 16) |
+                                              ((unsigned long long)(c2 & 0xffff) << 32);
+        }
+#endif
     } else if (m > 0) {
         const double s = Gc[G_S], c = Gc[G_C], ul = Gc[G_ULIMB];
         const double twd = TWO_PI * ((1.0 - ul) * 0.5 + ul / 3.0);  // 2 pi [F(1) - F(0)]

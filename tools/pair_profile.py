@@ -91,5 +91,11 @@ if hasattr(L, "lfg_debug_pair_jobs") and L.lfg_debug_pair_jobs(ctypes.c_void_p(j
 if LONG and wv.any():
     d = (wv[0] - t[12][None, :]) / 100.0
     print("LONG point loop per wave after the tables (us, median over blocks): %s" % np.median(d, axis=1).round(2))
+    # s_memtime cycles (~100 MHz-equivalent ticks? printed raw) of the busiest lane per wave
+    print("LONG busiest lane's WD/disc cycles per wave (median): %s" % np.median(wv[1], axis=1).round(0))
+    print("LONG busiest lane's sub-bin cycles per wave (median): %s" % np.median(wv[2], axis=1).round(0))
+    c = wv[3].astype(np.uint64)
+    for k, nm in enumerate(("find-walk steps", "window entries", "windows in a hull")):
+        print("LONG max lane's %s per wave (median): %s" % (nm, np.median(((c >> np.uint64(16 * k)) & np.uint64(0xffff)).astype(np.float64), axis=1).round(0)))
 if len(sys.argv) > 4:  # raw stamps for offline analysis
     np.save(sys.argv[4], t)
