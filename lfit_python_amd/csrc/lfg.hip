@@ -3050,12 +3050,12 @@ __device__ __forceinline__ double2 long_wd_disc(const LongTabs& W, const LongU& 
 // from there instead of a fresh lookup (a thread's run of sorted points);
 // the line of sight is formed afresh at each point's first sub-bin
 // the donor cursor runs two entries ahead: the next entry's position, code
-// and tile vector (raw, LDS) and the one after's position and code are in
-// registers, their loads issued a crossing earlier -- a crossing applies the
-// vector and moves the pipe on without waiting on LDS
+// and tile vector (fixed point: long_tables' step (g)) and the one after's
+// position and code are in registers, their loads issued a crossing earlier
+// -- a crossing applies the vector and moves the pipe on without waiting on LDS
 struct SubCur {
     double ph, npos, n2pos;
-    double nq[3];
+    long long nq[3];  // the next entry's tile vector (fixed point, before the mirror's signs)
     long long vx, vy, vz;
     int cur, ncode, n2code;
 #ifdef LFG_SPOT_CARRY
@@ -3074,7 +3074,7 @@ __device__ __forceinline__ void subcur_fill(const SubEntries& D, const double* s
     U.ncode = U.cur < nd ? D.dcode[U.cur] : 0;
     U.n2pos = U.cur + 1 < nd ? D.dpos[U.cur + 1] : INFINITY;
     U.n2code = U.cur + 1 < nd ? D.dcode[U.cur + 1] : 0;
-    const double* dq = sdq + ((U.ncode >> 1) >> 2) * DON_STRIDE;
+    const long long* dq = reinterpret_cast<const long long*>(sdq + ((U.ncode >> 1) >> 2) * DON_STRIDE);
     U.nq[0] = dq[0]; U.nq[1] = dq[1]; U.nq[2] = dq[2];
 }
 
@@ -3088,23 +3088,24 @@ __device__ __forceinline__ int long_weight(const LongU& K, double ph0, double w)
     for (int t = 0; t < 2; ++t)
         wd = wd || (hi >= K.amin[t] && lo <= K.bmax[t]) || (-lo >= K.amin[t] && -hi <= K.bmax[t]);
     const bool sp = hi >= K.sa && lo <= K.sb;
-    return 5 + (wd ? 8 : 0) + (sp ? 2 : 0);  // from the per-wave times of equal runs (profiles/r05)
+    // weights from A/B runs at config 5 (wave ranges with interleaved lanes):
+    // 5/3/1 2.39 M evals/s, 5/8/2 2.34, 5/1/1 2.31, uniform 2.36
+    return 5 + (wd ? 3 : 0) + (sp ? 1 : 0);
 }
 
-// a crossing of entry cur: its vector into V (donor_apply's arithmetic), then
-// the pipe one entry on
-__device__ __forceinline__ void subcur_cross(const SubEntries& D, const double* sdq, int nd, double ivs, SubCur& U)
+// a crossing of entry cur: its vector into V (the mirror image's signs on the
+// unique tile's fixed-point vector: donor_apply's sums, exactly), then the
+// pipe one entry on
+__device__ __forceinline__ void subcur_cross(const SubEntries& D, const double* sdq, int nd, SubCur& U)
 {
     const int code = U.ncode, mr = (code >> 1) & 3;
-    const long long qx = to_fx(U.nq[0] * ivs);
-    const long long qy = to_fx(((mr & 1) ? -U.nq[1] : U.nq[1]) * ivs);
-    const long long qz = to_fx(((mr & 2) ? -U.nq[2] : U.nq[2]) * ivs);
+    const long long qx = U.nq[0], qy = (mr & 1) ? -U.nq[1] : U.nq[1], qz = (mr & 2) ? -U.nq[2] : U.nq[2];
     if (code & 1) { U.vx -= qx; U.vy -= qy; U.vz -= qz; }
     else { U.vx += qx; U.vy += qy; U.vz += qz; }
     ++U.cur;
     U.npos = U.n2pos;
     U.ncode = U.n2code;
-    const double* dq = sdq + ((U.ncode >> 1) >> 2) * DON_STRIDE;
+    const long long* dq = reinterpret_cast<const long long*>(sdq + ((U.ncode >> 1) >> 2) * DON_STRIDE);
     U.nq[0] = dq[0]; U.nq[1] = dq[1]; U.nq[2] = dq[2];
     U.n2pos = U.cur + 1 < nd ? D.dpos[U.cur + 1] : INFINITY;
     U.n2code = U.cur + 1 < nd ? D.dcode[U.cur + 1] : 0;
@@ -3157,7 +3158,23 @@ __device__ __forceinline__ double2 sub_point_c(const SubTables& T, const SubEntr
 #else
         if (!(phn >= U.ph)) {  // a fresh lookup (the first point, a step back in phase)
 #endif
-            U.cur = sub_donor(T, D, sdq, K.ivs, phn, U.vx, U.vy, U.vz);
+            {  // sub_donor with the tiles' fixed-point vectors
+                const int g = tcell(phn, T.dt0, T.dginv);
+                U.vx = T.dpre[g][0];
+                U.vy = T.dpre[g][1];
+                U.vz = T.dpre[g][2];
+                int i = g ? T.dend[g - 1] : 0;
+                for (const int ie = T.dend[g]; i < ie; ++i) {
+                    const int code = D.dcode[i];
+                    if (!donor_counted(D.dpos[i], code, phn)) break;
+                    const int mr = (code >> 1) & 3;
+                    const long long* dq = reinterpret_cast<const long long*>(sdq + ((code >> 1) >> 2) * DON_STRIDE);
+                    const long long qx = dq[0], qy = (mr & 1) ? -dq[1] : dq[1], qz = (mr & 2) ? -dq[2] : dq[2];
+                    if (code & 1) { U.vx -= qx; U.vy -= qy; U.vz -= qz; }
+                    else { U.vx += qx; U.vy += qy; U.vz += qz; }
+                }
+                U.cur = i;
+            }
             subcur_fill(D, sdq, nd, U);
             chg = true;
         } else {
@@ -3166,7 +3183,7 @@ __device__ __forceinline__ double2 sub_point_c(const SubTables& T, const SubEntr
 #else
             while (false) {
 #endif
-                subcur_cross(D, sdq, nd, K.ivs, U);
+                subcur_cross(D, sdq, nd, U);
                 chg = true;
             }
         }
@@ -3543,6 +3560,17 @@ __device__ __forceinline__ void long_tables(LongTabs& W, SubTables& T, SubEntrie
             f4[j] = static_cast<unsigned short>(k);
         }
         for (int j = 0; j < 4; ++j) W.fcell[t][4 * g + j] = f4[j];
+    }
+    // (g) each unique donor tile's vector in fixed point, in place of its raw
+    // components (the point phase adds them at its donor crossings; a mirror
+    // image's components differ in sign only, and to_fx is odd)
+    if (tid < U_DON) {
+        double* dq = const_cast<double*>(sdq) + tid * DON_STRIDE;
+        const long long q0 = to_fx(dq[0] * ivs), q1 = to_fx(dq[1] * ivs), q2 = to_fx(dq[2] * ivs);
+        long long* dl = reinterpret_cast<long long*>(dq);
+        dl[0] = q0;
+        dl[1] = q1;
+        dl[2] = q2;
     }
     __syncthreads();
 }
@@ -3982,17 +4010,19 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
         unsigned long long tl_wd = 0, tl_sub = 0;
         int lctr[3] = {0, 0, 0};
 #endif
-        SubCur SC{INFINITY, INFINITY, INFINITY, {0.0, 0.0, 0.0}, 0, 0, 0, 0, 0, 0
+        SubCur SC{INFINITY, INFINITY, INFINITY, {0, 0, 0}, 0, 0, 0, 0, 0, 0
 #ifdef LFG_SPOT_CARRY
                   , INFINITY, INFINITY, 0, 0
 #endif
         };
         const LongU KU = long_uniforms(LT, LST, S);
         const double fspS = uni(fsp / S), frsS = uni(frs / S);
-        // a contiguous run of points per thread: its donor cursor walks on
-        // from point to point (a dynamic queue of 4-point chunks balanced the
-        // eclipse's points over the waves but doubled the total: every chunk
-        // starts with fresh lookups; and its chi^2 order was not fixed)
+        // each wave a contiguous range of the points, its lanes interleaved
+        // (a thread's points follow one another 64 apart, and its donor
+        // cursor walks on from point to point).  A dynamic queue of 4-point
+        // chunks balanced the eclipse's points over the waves but doubled the
+        // total (every chunk starts with fresh lookups; and its chi^2 order
+        // was not fixed)
         // The runs are cut where the running estimated cost (long_weight, in
         // index order) passes equal shares: a thread in the eclipse takes
         // fewer points, and the waves end together (the eclipse's waves took
@@ -4028,20 +4058,33 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
                 }
                 return e;
             };
+#ifdef LFG_LONG_LANE_RUNS
             p0 = start(tid);
             p1 = start(tid + 1);
+#else
+            // a wave's range, its lanes interleaved: each step of the loop
+            // reads 64 consecutive points (coalesced), and the lanes of a wave
+            // stand at neighbouring phases (the same branches of the lookups)
+            p0 = __builtin_amdgcn_readfirstlane(start(wv * 64)) + lane;
+            p1 = __builtin_amdgcn_readfirstlane(start(wv * 64 + 64));
+#endif
         }
+#ifdef LFG_LONG_LANE_RUNS
+        constexpr int PSTEP = 1;
+#else
+        constexpr int PSTEP = 64;
+#endif
         {
             double xn = p0 < p1 ? xe[p0] : 0.0, wn = (p0 < p1 && we) ? we[p0] : 0.0;
-        for (int p = p0; p < p1; ++p) {
+        for (int p = p0; p < p1; p += PSTEP) {
 #ifdef LFG_ABL_GLOAD  // (diagnostic builds) no global loads in the point loop: a synthetic grid
             const double xp = -0.3 + p * 6.0006e-5, wp = 3.0003e-5, yp = 1.0, ep = 0.004;
             (void)xn; (void)wn;
 #else
             const double xp = xn, wp = wn, yp = ye[p], ep = ee[p];
-            if (p + 1 < p1) {  // the next point's phase and width, in flight during this one
-                xn = xe[p + 1];
-                wn = we ? we[p + 1] : 0.0;
+            if (p + PSTEP < p1) {  // the next point's phase and width, in flight during this one
+                xn = xe[p + PSTEP];
+                wn = we ? we[p + PSTEP] : 0.0;
             }
 #endif
             const double wk = wp < 0.0 ? 0.0 : wp;  // MODEL_SPEC 3 (NaN stays NaN)
