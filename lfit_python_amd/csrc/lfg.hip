@@ -4027,53 +4027,60 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
         // index order) passes equal shares: a thread in the eclipse takes
         // fewer points, and the waves end together (the eclipse's waves took
         // 2-3 times the others' time with equal counts)
+        // The points in blocks of 64 (one step of a wave's loop): each block's
+        // estimated cost (long_weight, one coalesced pass, a wave per block),
+        // their prefix, and each wave takes the blocks where the running cost
+        // passes its eighth of the total; its lanes interleaved, so every step
+        // reads 64 consecutive points and the lanes of a wave stand at
+        // neighbouring phases (the same branches of the lookups)
         int p0, p1;
         {
-            const int R = (n + nt - 1) / nt, c0 = min(tid * R, n), c1 = min(c0 + R, n);
-            long long v[1] = {0};
-            for (int p = c0; p < c1; ++p) v[0] += long_weight(KU, xe[p] - phi0, we ? we[p] : 0.0);
-            const long long own = v[0];
-            cell_scan<1>(v, lspart, tid);  // exclusive prefix over the chunks (a barrier inside)
-            int* pre = reinterpret_cast<int*>(Lab);  // the WD/disc intervals are spent
-            pre[tid] = int(v[0]);
-            if (tid == nt - 1) pre[nt] = int(v[0] + own);
-            __syncthreads();
-            const long long T = pre[nt];
-            auto start = [&](int t) {  // the first point whose cost before it reaches t / nt of the total
-                if (t <= 0) return 0;
-                if (t >= nt) return n;
-                const long long tgt = (T * t) / nt;
-                if (tgt <= 0) return 0;
-                int a = 0, b = nt - 1;  // the last chunk with prefix < tgt
-                while (a < b) {
-                    const int mid = (a + b + 1) >> 1;
-                    if (pre[mid] < tgt) a = mid;
-                    else b = mid - 1;
+            constexpr int nw = LIKE_THREADS / 64;
+            const int nch = (n + 63) >> 6;
+            int* cw = reinterpret_cast<int*>(Lab);  // the WD/disc intervals are spent
+            int b0, b1;
+            if (nch + 1 <= int(sizeof(Lab) / sizeof(int))) {
+                for (int c = wv; c < nch; c += nw) {
+                    const int p = c * 64 + lane;
+                    int wt = p < n ? long_weight(KU, xe[p] - phi0, we ? we[p] : 0.0) : 0;
+                    for (int off = 32; off > 0; off >>= 1) wt += __shfl_xor(wt, off);
+                    if (lane == 0) cw[c] = wt;
                 }
-                long long cum = pre[a];
-                const int e = min(a * R + R, n);
-                for (int p = min(a * R, n); p < e; ++p) {
-                    if (cum >= tgt) return p;
-                    cum += long_weight(KU, xe[p] - phi0, we ? we[p] : 0.0);
+                __syncthreads();
+                if (wv == 0) {  // exclusive prefix over the blocks, in place; the total at nch
+                    const int B = (nch + 63) >> 6, q0 = min(lane * B, nch), q1 = min(q0 + B, nch);
+                    long long own = 0;
+                    for (int c = q0; c < q1; ++c) own += cw[c];
+                    long long run = wave_scan_incl(own, lane) - own;
+                    for (int c = q0; c < q1; ++c) {
+                        const int v = cw[c];
+                        cw[c] = int(run);
+                        run += v;
+                    }
+                    if (lane == 63) cw[nch] = int(run);
                 }
-                return e;
-            };
-#ifdef LFG_LONG_LANE_RUNS
-            p0 = start(tid);
-            p1 = start(tid + 1);
-#else
-            // a wave's range, its lanes interleaved: each step of the loop
-            // reads 64 consecutive points (coalesced), and the lanes of a wave
-            // stand at neighbouring phases (the same branches of the lookups)
-            p0 = __builtin_amdgcn_readfirstlane(start(wv * 64)) + lane;
-            p1 = __builtin_amdgcn_readfirstlane(start(wv * 64 + 64));
-#endif
+                __syncthreads();
+                const long long T = cw[nch];
+                auto first = [&](int w) {  // the first block whose cost before it reaches w / nw of the total
+                    const long long tgt = (T * w) / nw;
+                    int a = 0, b = nch;
+                    while (a < b) {
+                        const int mid = (a + b) >> 1;
+                        if (cw[mid] >= tgt) b = mid;
+                        else a = mid + 1;
+                    }
+                    return a;
+                };
+                b0 = wv ? first(wv) : 0;
+                b1 = wv + 1 < nw ? first(wv + 1) : nch;
+            } else {  // more blocks than the spent LDS holds: equal shares
+                b0 = nch * wv / nw;
+                b1 = nch * (wv + 1) / nw;
+            }
+            p0 = __builtin_amdgcn_readfirstlane(b0) * 64 + lane;
+            p1 = min(__builtin_amdgcn_readfirstlane(b1) * 64, n);
         }
-#ifdef LFG_LONG_LANE_RUNS
-        constexpr int PSTEP = 1;
-#else
         constexpr int PSTEP = 64;
-#endif
         {
             double xn = p0 < p1 ? xe[p0] : 0.0, wn = (p0 < p1 && we) ? we[p0] : 0.0;
         for (int p = p0; p < p1; p += PSTEP) {
