@@ -3058,14 +3058,6 @@ struct SubCur {
     long long nq[3];  // the next entry's tile vector (fixed point, before the mirror's signs)
     long long vx, vy, vz;
     int cur, ncode, n2code;
-#ifdef LFG_SPOT_CARRY
-    // the spot cursor, carried from sub-bin to sub-bin and point to point:
-    // every entry at or below shi counted into sC, scur the first above,
-    // snpos its position
-    double shi, snpos;
-    long long sC;
-    int scur;
-#endif
 };
 
 __device__ __forceinline__ void subcur_fill(const SubEntries& D, const double* sdq, int nd, SubCur& U)
@@ -3117,47 +3109,16 @@ __device__ __forceinline__ double2 sub_point_c(const SubTables& T, const SubEntr
 {
     const int nd = K.nd, nsp = K.nsp;
     const double h = wk * K.invS, ih = 0.5 / h;
-    // the first sub-bin's line of sight and the turn per sub-bin (both paths)
+    // the first sub-bin's line of sight and the turn per sub-bin
     const double phA = wrap_phase(ph0 - wk + h);
     const double4 eA = sincospi2_ool(2.0 * phA, 4.0 * h);
-#ifdef LFG_QUIET_FAST
-    if (h > 0.0) {
-        // the quiet point -- most of them: no donor entry crossed within it,
-        // its sub-bins all off the spot's hull, no wrap -- takes the sums in
-        // closed form over the rotated line of sight: V is constant, the
-        // spot is uneclipsed, so sum_j V . e_j = V . sum_j e_j and the beaming
-        // term needs only max(nb . e_j, 0) per sub-bin
-        const double phZ = wrap_phase(ph0 - wk + (2 * S - 1) * h);
-        if (phA >= U.ph && phZ >= phA && !donor_counted(U.npos, U.ncode, phZ) &&
-            (phZ + h <= K.sa || phA - h >= K.sb)) {
-            double sn = eA.x, cs = eA.y, scs = 0.0, ssn = 0.0, smx = 0.0;
-            for (int j = 0; j < S; ++j) {
-                scs += cs;
-                ssn += sn;
-                smx += fmax(fma(K.nbs0, cs, fma(K.nbs1, sn, K.nbc)), 0.0);
-                const double c2 = fma(cs, eA.w, -sn * eA.z);
-                sn = fma(sn, eA.w, cs * eA.z);
-                cs = c2;
-            }
-            U.ph = phZ;
-            const double sbs = fma(K.omf, smx, S * K.fis);
-            const double srs1 = fma(double(U.vx), scs, -double(U.vy) * ssn), srs2 = S * double(U.vz);
-            return make_double2(sbs * K.ibden, fma(K.sg, srs1, K.cg * srs2) * K.dsc);
-        }
-    }
-#endif
     double sbs = 0.0, srs1 = 0.0, srs2 = 0.0, sn = 0.0, cs = 1.0, rs = 0.0, rc = 1.0;
     long long Cs = 0;
     int scur = 0;
     bool sv = false;  // Cs / scur hold C at this sub-bin's lo
     for (int j = 0; j < S; ++j) {
         const double phn = wrap_phase(ph0 - wk + (2 * j + 1) * h);
-        bool chg = false;
-#ifdef LFG_ABL_SC_DONOR
-        if (false) {
-#else
         if (!(phn >= U.ph)) {  // a fresh lookup (the first point, a step back in phase)
-#endif
             {  // sub_donor with the tiles' fixed-point vectors
                 const int g = tcell(phn, T.dt0, T.dginv);
                 U.vx = T.dpre[g][0];
@@ -3176,24 +3137,12 @@ __device__ __forceinline__ double2 sub_point_c(const SubTables& T, const SubEntr
                 U.cur = i;
             }
             subcur_fill(D, sdq, nd, U);
-            chg = true;
         } else {
-#ifndef LFG_ABL_SC_DONOR
-            while (donor_counted(U.npos, U.ncode, phn)) {  // npos = inf past the last entry
-#else
-            while (false) {
-#endif
+            while (donor_counted(U.npos, U.ncode, phn))  // npos = inf past the last entry
                 subcur_cross(D, sdq, nd, U);
-                chg = true;
-            }
         }
-#ifdef LFG_ABL_SC_TRIG
-        if (j == 0) {
-            const double4 e4 = make_double4(phn, 1.0 - phn * phn, h, 1.0 - h);
-#else
         if (j == 0 || !(phn >= U.ph)) {
             const double4 e4 = j == 0 ? eA : sincospi2_ool(2.0 * phn, 4.0 * h);  // the turn per sub-bin: 2 pi (2 h)
-#endif
             sn = e4.x;
             cs = e4.y;
             rs = e4.z;
@@ -3203,57 +3152,14 @@ __device__ __forceinline__ double2 sub_point_c(const SubTables& T, const SubEntr
             sn = fma(sn, rc, cs * rs);
             cs = c2;
         }
-        (void)chg;
         U.ph = phn;
         // spot: as sub_point (the windows of a point abut; each point starts afresh)
         double ebj = 0.0;
         const double lo = phn - h, hi = phn + h;
         if (!(h > 0.0)) {
             ebj = sub_spot(T, sab, sbw, K.itb, lo, hi, K.sa, K.sb);
-#ifdef LFG_ABL_SC_SPOT
-        } else if (false) {
-#else
         } else if (hi > K.sa && lo < K.sb) {
-#endif
             const double itb = K.itb;
-#ifdef LFG_SPOT_CARRY
-            if (!(lo >= U.shi)) {  // a fresh lookup (the first window, a step back)
-                U.sC = spot_C(T, sbw, itb, lo, U.scur);
-                U.snpos = U.scur < nsp ? T.spos[U.scur] : INFINITY;
-            } else {
-                while (U.snpos <= lo) {  // the entries since the last window's hi
-                    const int code = T.scode[U.scur];
-                    const long long Wq = to_fx(sbw[code >> 1] * itb);
-                    U.sC += (code & 1) ? -Wq : Wq;
-                    ++U.scur;
-                    U.snpos = U.scur < nsp ? T.spos[U.scur] : INFINITY;
-                }
-            }
-            long long Cn = U.sC;
-            double corr = 0.0;
-            while (U.snpos <= hi) {
-                const int code = T.scode[U.scur], k = code >> 1;
-                const double wn = sbw[k] * itb;
-                const double2 ab = sab[k];
-                const long long Wq = to_fx(wn);
-                if (!(code & 1)) {
-                    Cn += Wq;
-                    corr = fma(wn, fmin(ab.y, hi) - ab.x, corr);
-                } else {
-                    Cn -= Wq;
-                    if (ab.x <= lo) corr = fma(-wn, hi - ab.y, corr);
-                }
-                ++U.scur;
-                U.snpos = U.scur < nsp ? T.spos[U.scur] : INFINITY;
-            }
-            ebj = fma(corr, ih, double(U.sC) * FX_INV);
-            U.sC = Cn;
-            U.shi = hi;
-            (void)sv; (void)Cs; (void)scur;
-        } else {
-            sv = false;
-        }
-#else
             if (!sv) Cs = spot_C(T, sbw, itb, lo, scur);
             sv = true;
             long long Cn = Cs;
@@ -3276,7 +3182,6 @@ __device__ __forceinline__ double2 sub_point_c(const SubTables& T, const SubEntr
         } else {
             sv = false;
         }
-#endif
         // e = (s cos, -s sin, c) at the sub-phase: the donor term V . e and
         // the spot's beaming term fis + (1 - fis) max(nb . e, 0) (sg, cg folded in)
         srs1 = fma(cs, double(U.vx), fma(-sn, double(U.vy), srs1));
@@ -4011,9 +3916,6 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
         int lctr[3] = {0, 0, 0};
 #endif
         SubCur SC{INFINITY, INFINITY, INFINITY, {0, 0, 0}, 0, 0, 0, 0, 0, 0
-#ifdef LFG_SPOT_CARRY
-                  , INFINITY, INFINITY, 0, 0
-#endif
         };
         const LongU KU = long_uniforms(LT, LST, S);
         const double fspS = uni(fsp / S), frsS = uni(frs / S);
