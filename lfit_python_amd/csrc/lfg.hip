@@ -2677,6 +2677,11 @@ __device__ unsigned long long g_pair_t[20][4096];
         if ((cond) && blockIdx.x < 4096) g_pair_t[slot][blockIdx.x] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 __device__ unsigned long long g_pair_w[4][8][4096];
+__device__ unsigned long long g_long_t[8][4096];  // the LONG table build's steps (thread 0 after each barrier)
+#define LONG_TSTAMP(k)                                                                      \
+    do {                                                                                    \
+        if (tid == 0 && blockIdx.x < 4096) g_long_t[k][blockIdx.x] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
 __device__ unsigned long long g_pair_j[3][16][4096];  // per chunk: job start, sink entry, end
 #define PAIR_WSTAMP(k)                                                                                  \
     do {                                                                                                \
@@ -2684,6 +2689,7 @@ __device__ unsigned long long g_pair_j[3][16][4096];  // per chunk: job start, s
     } while (0)
 #else
 #define PAIR_STAMP(slot, cond)
+#define LONG_TSTAMP(k)
 #define PAIR_WSTAMP(k)
 #endif
 
@@ -3227,6 +3233,7 @@ __device__ __forceinline__ void long_tables(LongTabs& W, SubTables& T, SubEntrie
         W.part[5][wv] = amin[1]; W.part[6][wv] = bmax[1];
     }
     __syncthreads();
+    LONG_TSTAMP(0);
     amin[0] = amin[1] = INFINITY; bmax[0] = bmax[1] = -INFINITY; sa = INFINITY; sb = -INFINITY; vs = 0.0;
     for (int k = 0; k < nw; ++k) {  // every thread forms the block's values (no barrier for a broadcast)
         amin[0] = fmin(amin[0], W.part[0][k]); bmax[0] = fmax(bmax[0], W.part[1][k]);
@@ -3302,6 +3309,7 @@ __device__ __forceinline__ void long_tables(LongTabs& W, SubTables& T, SubEntrie
         }
     }
     __syncthreads();
+    LONG_TSTAMP(1);
     // (c) exclusive prefixes over the cells
     {
         long long v[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -3319,6 +3327,7 @@ __device__ __forceinline__ void long_tables(LongTabs& W, SubTables& T, SubEntrie
         }
     }
     __syncthreads();
+    LONG_TSTAMP(2);
     // (d) the entries into cell order; afterwards cend / dend / send hold the cell ends
     for (int g = tid; g < NU_WDD; g += nt) {
         double2 ab;
@@ -3355,6 +3364,7 @@ __device__ __forceinline__ void long_tables(LongTabs& W, SubTables& T, SubEntrie
         }
     }
     __syncthreads();
+    LONG_TSTAMP(3);
     // (e) every cell's entries in order: each entry counts the entries of its
     // cell that sort before it and moves to that rank (all entries at once;
     // an insertion sort per cell took O(n^2) steps in the cells where the WD
@@ -3429,6 +3439,7 @@ __device__ __forceinline__ void long_tables(LongTabs& W, SubTables& T, SubEntrie
             sslot = c0 + rank;
         }
         __syncthreads();
+    LONG_TSTAMP(4);
 #pragma unroll
         for (int r = 0; r < RW; ++r)
             if (wslot[r] >= 0) {
@@ -3447,6 +3458,7 @@ __device__ __forceinline__ void long_tables(LongTabs& W, SubTables& T, SubEntrie
         }
     }
     __syncthreads();
+    LONG_TSTAMP(5);
     // (f) the fine index (over cpre, now spent): a thread per build cell
     // counts its sorted entries below each of its four fine cells
     if (tid < 2 * TCELLS) {
@@ -3478,6 +3490,7 @@ __device__ __forceinline__ void long_tables(LongTabs& W, SubTables& T, SubEntrie
         dl[2] = q2;
     }
     __syncthreads();
+    LONG_TSTAMP(6);
 }
 
 // GP (GP trees, MODE 2 of k_lnlike): instead of chi^2 the residuals, each
@@ -5572,6 +5585,10 @@ int lfg_debug_pair_jobs(unsigned long long* host)
 int lfg_debug_pair_waves(unsigned long long* host)
 {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pair_w), sizeof(g_pair_w)) == hipSuccess ? 0 : -1;
+}
+int lfg_debug_long_tables(unsigned long long* host)
+{
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_long_t), sizeof(g_long_t)) == hipSuccess ? 0 : -1;
 }
 #endif
 

@@ -88,6 +88,20 @@ if hasattr(L, "lfg_debug_pair_jobs") and L.lfg_debug_pair_jobs(ctypes.c_void_p(j
             sv = (jb[1, c][ok] - jb[0, c][ok]) / 100.0
             sk = (jb[2, c][ok] - jb[1, c][ok]) / 100.0
             print("  chunk %2d  solve %6.2f  sink %6.2f  (n %d)" % (c, np.median(sv), np.median(sk), ok.sum()))
+if LONG:
+    lt = np.zeros((8, 4096), dtype=np.uint64)
+    try:
+        ok = L.lfg_debug_long_tables(ctypes.c_void_p(lt.ctypes.data)) == 0
+    except AttributeError:
+        ok = False
+    if ok and lt.any():
+        lt = lt[:, :nb].astype(np.float64)
+        prev = t[9]
+        for k, nm in enumerate(("(a) hulls", "(b) counts, sums", "(c) cell scan", "(d) scatter", "(e) ranks",
+                                "(e) placed", "(f) fine index, (g) donor fx")):
+            d = (lt[k] - prev) / 100.0
+            print("LONG table step %-28s median %6.2f  p90 %6.2f us" % (nm, np.median(d), np.percentile(d, 90)))
+            prev = lt[k]
 if LONG and wv.any():
     d = (wv[0] - t[12][None, :]) / 100.0
     print("LONG point loop per wave after the tables (us, median over blocks): %s" % np.median(d, axis=1).round(2))
