@@ -3954,7 +3954,8 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
             const int nch = (n + 63) >> 6;
             int* cw = reinterpret_cast<int*>(Lab);  // the WD/disc intervals are spent
             int b0, b1;
-            if (nch + 1 <= int(sizeof(Lab) / sizeof(int))) {
+            constexpr int LAB_INTS = int(NU_WDD * sizeof(double2) / sizeof(int));
+            if (nch + 1 <= LAB_INTS) {
                 for (int c = wv; c < nch; c += nw) {
                     const int p = c * 64 + lane;
                     int wt = p < n ? long_weight(KU, xe[p] - phi0, we ? we[p] : 0.0) : 0;
