@@ -2739,6 +2739,9 @@ struct PairSink {
     }
     __device__ __forceinline__ void wd_disc(int u, double a, double b)
     {
+#ifdef LFG_ABL_SINK_WD  // (diagnostic builds) the sink skipped: LDS counter attribution only
+        return;
+#endif
         if (dir) {
             ab[uslot(u)] = make_double2(a, b);
             return;
@@ -2760,7 +2763,11 @@ struct PairSink {
         sab[j] = make_double2(a, b);
         sbw[j] = w;
         tspot += to_fx(w * PAIR_SPOT_S);
+#ifdef LFG_ABL_SINK_SPOT  // (diagnostic builds) the runs skipped: LDS counter attribution only
+        if (false) {
+#else
         if (!dir && a < b) {
+#endif
             const Runs RR[1] = {element_runs(a, b, XW, hi)};
             const double aa[1] = {a}, bb[1] = {b};
             apply_runs_batched<1>(RR, aa, bb, w * PAIR_SPOT_S, XW, hi, iw, acc[2]);
@@ -2784,6 +2791,9 @@ struct PairSink {
             const double hw = (mr & 2) ? 0.5 - hw0 : hw0;
             tn += to_fx(fmax(-s * vy + c * vz, 0.0) * PAIR_DON_S);
             PA[mr][0] = QA[mr][0] = PA[mr][1] = QA[mr][1] = 0;
+#ifdef LFG_ABL_SINK_DON  // (diagnostic builds) the arcs skipped: LDS counter attribution only
+            continue;
+#endif
             if (dir || !(hw > 0.0)) continue;
             // visible for phases in (cen - hw, cen + hw) mod 1
             double x1 = -INFINITY, x2 = INFINITY, y1 = 0.0, y2 = 0.0;
