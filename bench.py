@@ -627,8 +627,8 @@ def run(args):
                                                                   "(DESIGN.md 3): an intermediate, not 8(d) work"}},
             },
             "acceptance_fraction": acc,
-            "kernel_layout": {1: "k_pair", 2: "k_pair (LONG: per-pair breakpoint tables in LDS, a run of points "
-                                                "per thread)"}.get(layout, "k_elements + k_lnlike"),
+            "kernel_layout": {1: "k_pair", 2: "k_pair (LONG: per-pair breakpoint tables in LDS, each wave a "
+                                                "cost-balanced range of the points)"}.get(layout, "k_elements + k_lnlike"),
             **({"ranks": ranks} if ranks else {}),
             **({"exchange_ms_per_half_step": xch_ms} if (xch_ms is not None and not ranks) else {}),
             **({"emulation": emu, "emulated_rank": True} if emu else {}),

@@ -2922,7 +2922,8 @@ __device__ __forceinline__ void pair_cells(int* cell, int p, int m, double vprev
 //    crowd); a zero-width window takes the elements with a_k < ph < b_k;
 //  * spot and donor at the sub-bins: the S > 1 breakpoint tables of k_lnlike
 //    (SubTables, SubEntries, sub_point), built here from LDS.
-// Each thread takes a contiguous run of points (MODEL_SPEC 3 for every
+// Each wave takes a range of blocks of 64 points, its lanes interleaved
+// (MODEL_SPEC 3 for every
 // width, order and wrap: no sortedness is assumed).
 constexpr int NE_W = 2 * U_WD, NE_D = 2 * U_DISC;  // WD / disc table entries (two per unique element)
 constexpr int LONG_FC = 4 * TCELLS;                 // fine cells per table (four per build cell)
@@ -3510,7 +3511,7 @@ __device__ __forceinline__ void long_tables(LongTabs& W, SubTables& T, SubEntrie
 // LONG: eclipses longer than a tile and sub-binned exposures (the LONG
 // tables above, long_tables / long_wd_disc / sub_point): the element phase
 // keeps the point-major sinks, and after the phase barrier the tables are
-// built and every thread evaluates a contiguous run of points
+// built and every wave evaluates a cost-balanced range of the points
 template <bool GP, bool FOLD = false, bool LONG = false>
 __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
 {
@@ -3923,7 +3924,7 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
     // ---- each point's flux and chi^2 (GP: residual, changepoint block)
     double chi = 0.0;
     if constexpr (LONG) {
-        // the pair's tables, then this thread's run of points [p0, p1)
+        // the pair's tables, then this wave's range of the points (lanes interleaved)
         const double ul = Gc[G_ULIMB];
         long_tables(LT, LST, LSE, Lab, sab, sbw, sdq, swt, stot, ul, 1.0 / (TWO_PI * ((1.0 - ul) * 0.5 + ul / 3.0)),
                     lspart, tid);
