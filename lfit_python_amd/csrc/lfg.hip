@@ -3294,12 +3294,11 @@ __device__ __forceinline__ void long_tables(LongTabs& W, SubTables& T, SubEntrie
         bool in0, in1;
         int v0;
         lane_breakpoints(tid, sdq, sab, t0d, t1d, p0, p1, in0, in1, v0);
+        long long c0[3] = {0, 0, 0};  // this lane's share of V0, summed per wave below
         if (tid >= nt - NDONOR) {
             long long q[3];
             donor_q(sdq, tid - (nt - NDONOR), ivs, q[0], q[1], q[2]);
-            if (v0)
-                for (int k = 0; k < 3; ++k)
-                    atomicAdd(reinterpret_cast<unsigned long long*>(&T.dv0[k]), static_cast<unsigned long long>(v0 * q[k]));
+            for (int k = 0; k < 3; ++k) c0[k] = v0 * q[k];
 #pragma unroll
             for (int b = 0; b < 2; ++b) {
                 if (!(b ? in1 : in0)) continue;
@@ -3317,6 +3316,13 @@ __device__ __forceinline__ void long_tables(LongTabs& W, SubTables& T, SubEntrie
                 atomicAdd(&T.send[g], 1);
                 atomicAdd(reinterpret_cast<unsigned long long*>(&T.spre[g]), static_cast<unsigned long long>(b ? -Wq : Wq));
             }
+        }
+        // V0: the wave's sum, one atomic per component (half the donor lanes
+        // add to these three words; per-lane atomics serialised on them)
+        for (int k = 0; k < 3; ++k) {
+            const long long w = wave_scan_incl(c0[k], lane);
+            if (lane == 63 && w != 0)
+                atomicAdd(reinterpret_cast<unsigned long long*>(&T.dv0[k]), static_cast<unsigned long long>(w));
         }
     }
     __syncthreads();
