@@ -3327,20 +3327,47 @@ __device__ __forceinline__ void long_tables(LongTabs& W, SubTables& T, SubEntrie
     }
     __syncthreads();
     LONG_TSTAMP(1);
-    // (c) exclusive prefixes over the cells
-    {
-        long long v[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        if (tid < TCELLS) {
-            v[0] = W.cend[0][tid]; v[1] = W.cend[1][tid]; v[2] = W.cpre[0][tid]; v[3] = W.cpre[1][tid];
-            v[4] = T.dend[tid]; v[5] = T.send[tid]; v[6] = T.dpre[tid][0]; v[7] = T.dpre[tid][1];
-            v[8] = T.dpre[tid][2]; v[9] = T.spre[tid];
-        }
-        cell_scan<10>(v, spart, tid);
-        if (tid < TCELLS) {
-            W.cend[0][tid] = int(v[0]); W.cend[1][tid] = int(v[1]); W.cpre[0][tid] = v[2]; W.cpre[1][tid] = v[3];
-            T.dend[tid] = int(v[4]); T.send[tid] = int(v[5]);
-            T.dpre[tid][0] = v[6] + T.dv0[0]; T.dpre[tid][1] = v[7] + T.dv0[1]; T.dpre[tid][2] = v[8] + T.dv0[2];
-            T.spre[tid] = v[9];
+    // (c) exclusive prefixes over the cells: each wave scans whole arrays
+    // (a lane four consecutive cells, then the wave's 64 sums), so no part
+    // sums cross waves and one barrier ends the step
+    static_assert(TCELLS == 4 * 64, "a wave's lanes hold four cells each");
+    (void)spart;
+    for (int a = wv; a < 10; a += nw) {  // uniform per wave
+        auto get = [&](int g) -> long long {
+            switch (a) {
+            case 0: return W.cend[0][g];
+            case 1: return W.cend[1][g];
+            case 2: return W.cpre[0][g];
+            case 3: return W.cpre[1][g];
+            case 4: return T.dend[g];
+            case 5: return T.send[g];
+            case 6: return T.dpre[g][0];
+            case 7: return T.dpre[g][1];
+            case 8: return T.dpre[g][2];
+            default: return T.spre[g];
+            }
+        };
+        auto set = [&](int g, long long x) {
+            switch (a) {
+            case 0: W.cend[0][g] = int(x); break;
+            case 1: W.cend[1][g] = int(x); break;
+            case 2: W.cpre[0][g] = x; break;
+            case 3: W.cpre[1][g] = x; break;
+            case 4: T.dend[g] = int(x); break;
+            case 5: T.send[g] = int(x); break;
+            case 6: T.dpre[g][0] = x + T.dv0[0]; break;
+            case 7: T.dpre[g][1] = x + T.dv0[1]; break;
+            case 8: T.dpre[g][2] = x + T.dv0[2]; break;
+            default: T.spre[g] = x; break;
+            }
+        };
+        long long c[4];
+        for (int j = 0; j < 4; ++j) c[j] = get(4 * lane + j);
+        const long long own = c[0] + c[1] + c[2] + c[3];
+        long long run = wave_scan_incl(own, lane) - own;
+        for (int j = 0; j < 4; ++j) {
+            set(4 * lane + j, run);
+            run += c[j];
         }
     }
     __syncthreads();
