@@ -2917,31 +2917,32 @@ __device__ __forceinline__ void pair_cells(int* cell, int p, int m, double vprev
 //      int_lo^hi C(t) dt = C(lo) (hi - lo) + sum_{lo <= pos < hi} q (hi - pos),
 //    with q = +w at a start a_k and -w at an end b_k; each sorted entry holds
 //    C just after it (int64 fixed point, exact), so C(lo) is one read once the
-//    first entry at or above lo is found -- in its fine cell (1 024 per table
-//    over the table's own hull, a few entries even where the WD contacts
-//    crowd); a zero-width window takes the elements with a_k < ph < b_k;
+//    first entry at or above lo is found -- in its cell (1 024 per table over
+//    the table's own hull, a few entries even where the WD contacts crowd);
+//    a zero-width window takes the elements with a_k < ph < b_k;
 //  * spot and donor at the sub-bins: the S > 1 breakpoint tables of k_lnlike
 //    (SubTables, SubEntries, sub_point), built here from LDS.
 // Each wave takes a range of blocks of 64 points, its lanes interleaved
-// (MODEL_SPEC 3 for every
-// width, order and wrap: no sortedness is assumed).
+// (MODEL_SPEC 3 for every width, order and wrap: no sortedness is assumed).
 constexpr int NE_W = 2 * U_WD, NE_D = 2 * U_DISC;  // WD / disc table entries (two per unique element)
-constexpr int LONG_FC = 4 * TCELLS;                 // fine cells per table (four per build cell)
+constexpr int LONG_FC = 4 * TCELLS;                 // cells per WD/disc table (the sub-bin tables: TCELLS)
 struct LongTabs {
-    union {
-        long long cpre[2][TCELLS];        // build: covering weight at each cell's start
-        unsigned short fcell[2][LONG_FC];  // lookup: the first entry of each fine cell
-    };
-    int cend[2][TCELLS];        // counts -> exclusive offsets -> (after the scatter) cell ends
+    int fend[2][LONG_FC];       // WD / disc cells: counts -> exclusive offsets -> (after the scatter) cell ends
     double epos[NE_W + NE_D];   // entries: WD [0, NE_W), disc after
-    long long ecb[NE_W + NE_D];  // build: q; after the sort: C just after the entry
-    double t0[2], ginv[2], amin[2], bmax[2];  // per table: cells over its hull
+    long long ecb[NE_W + NE_D];  // build: q; after the sort and scan: C just after the entry
+    double t0[2], ginv[2], amin[2], bmax[2];  // per table: LONG_FC cells over its hull
     double snorm[4];            // sub_point's: 1 / spot total, 1 / donor |v| sum, donor norm, |v| sum
     double shull[4];            // [2], [3]: the spot hull (sub_point)
     double sgeo[LFG_NGEO];      // the record, for sub_point's LDS reads
     double part[8][LIKE_THREADS / 64];  // wave partials of the hulls and sums
 };
-static_assert(NE_W < 65536 && NE_D < 65536, "fine cells index entries as 16-bit");
+
+// the WD/disc cell of x in table t (clamped to the table's cells)
+__device__ __forceinline__ int long_cell(double x, double t0, double ginv)
+{
+    const double u = (x - t0) * ginv;
+    return u <= 0.0 ? 0 : (u >= double(LONG_FC - 1) ? LONG_FC - 1 : int(u));
+}
 
 // a value the whole block holds alike, into scalar registers
 __device__ __forceinline__ double uni(double x)
@@ -2956,7 +2957,7 @@ __device__ __forceinline__ double uni(double x)
 // registers: every lane's lookups and sub-bin terms use them, and the LDS
 // pipe -- which the lookups keep busy -- serves no broadcasts in the loop
 struct LongU {
-    double t0[2], g4[2], amin[2], bmax[2];  // WD/disc tables: fine cells (4 per build cell) and hulls
+    double t0[2], gf[2], amin[2], bmax[2];  // WD/disc tables: cells and hulls
     int n[2];                               // entries per table
     double itb, ivs, dnorm, vsum, sa, sb;   // spot / donor norms, the spot hull
     double nbs0, nbs1, nbc, fis, omf;       // the record's terms of the sub-bin sums (MODEL_SPEC 6), folded
@@ -2971,10 +2972,10 @@ __device__ __forceinline__ LongU long_uniforms(const LongTabs& W, const SubTable
     K.invS = uni(1.0 / S);
     for (int t = 0; t < 2; ++t) {
         K.t0[t] = uni(W.t0[t]);
-        K.g4[t] = uni(4.0 * W.ginv[t]);
+        K.gf[t] = uni(W.ginv[t]);
         K.amin[t] = uni(W.amin[t]);
         K.bmax[t] = uni(W.bmax[t]);
-        K.n[t] = __builtin_amdgcn_readfirstlane(W.cend[t][TCELLS - 1]);
+        K.n[t] = __builtin_amdgcn_readfirstlane(W.fend[t][LONG_FC - 1]);
     }
     K.itb = uni(W.snorm[0]); K.ivs = uni(W.snorm[1]); K.dnorm = uni(W.snorm[2]); K.vsum = uni(W.snorm[3]);
     K.sa = uni(W.shull[2]); K.sb = uni(W.shull[3]);
@@ -2988,9 +2989,9 @@ __device__ __forceinline__ LongU long_uniforms(const LongTabs& W, const SubTable
     return K;
 }
 
-// the first entry of table t at or above x: the entries of the fine cells
-// below x's all lie below it, those of the cells above all above (the fine
-// index is monotone in position)
+// the first entry of table t at or above x: the entries of the cells below
+// x's all lie below it, those of the cells above all above (the cell index
+// is monotone in position)
 #ifdef LFG_PROFILE_PAIR
 #define LONG_CNT(c, k) (c)[k]++
 #else
@@ -2998,11 +2999,10 @@ __device__ __forceinline__ LongU long_uniforms(const LongTabs& W, const SubTable
 #endif
 __device__ __forceinline__ int long_find(const LongTabs& W, const LongU& K, int t, double x, int* ctr = nullptr)
 {
-    const double u = (x - K.t0[t]) * K.g4[t];
-    const int f = u <= 0.0 ? 0 : (u >= double(LONG_FC - 1) ? LONG_FC - 1 : int(u));
+    const int f = long_cell(x, K.t0[t], K.gf[t]);
     const double* ep = W.epos + (t ? NE_W : 0);
-    int i = W.fcell[t][f];
-    const int ie = f < LONG_FC - 1 ? int(W.fcell[t][f + 1]) : K.n[t];
+    int i = f ? W.fend[t][f - 1] : 0;
+    const int ie = W.fend[t][f];
     while (i < ie && ep[i] < x) {
         ++i;
         LONG_CNT(ctr, 0);
@@ -3255,7 +3255,7 @@ __device__ __forceinline__ void long_tables(LongTabs& W, SubTables& T, SubEntrie
     double t0[2], ginv[2];
     for (int t = 0; t < 2; ++t) {
         t0[t] = amin[t];
-        ginv[t] = (bmax[t] > amin[t]) ? TCELLS / (bmax[t] - amin[t]) : 0.0;
+        ginv[t] = (bmax[t] > amin[t]) ? LONG_FC / (bmax[t] - amin[t]) : 0.0;
     }
     const double st0 = sa, sginv = (sb > sa) ? TCELLS / (sb - sa) : 0.0;
     constexpr double t0d = -0.5, t1d = 0.5, dginv = TCELLS;  // donor cells: the whole phase circle
@@ -3283,11 +3283,9 @@ __device__ __forceinline__ void long_tables(LongTabs& W, SubTables& T, SubEntrie
         int t;
         long long q;
         if (!wd_entry(g, ab, t, q)) continue;
-        const int ga = tcell(ab.x, t0[t], ginv[t]), gb = tcell(ab.y, t0[t], ginv[t]);
-        atomicAdd(&W.cend[t][ga], 1);
-        atomicAdd(&W.cend[t][gb], 1);
-        atomicAdd(reinterpret_cast<unsigned long long*>(&W.cpre[t][ga]), static_cast<unsigned long long>(q));
-        atomicAdd(reinterpret_cast<unsigned long long*>(&W.cpre[t][gb]), static_cast<unsigned long long>(-q));
+        (void)q;
+        atomicAdd(&W.fend[t][long_cell(ab.x, t0[t], ginv[t])], 1);
+        atomicAdd(&W.fend[t][long_cell(ab.y, t0[t], ginv[t])], 1);
     }
     {
         double p0, p1;
@@ -3327,47 +3325,69 @@ __device__ __forceinline__ void long_tables(LongTabs& W, SubTables& T, SubEntrie
     }
     __syncthreads();
     LONG_TSTAMP(1);
-    // (c) exclusive prefixes over the cells: each wave scans whole arrays
-    // (a lane four consecutive cells, then the wave's 64 sums), so no part
-    // sums cross waves and one barrier ends the step
-    static_assert(TCELLS == 4 * 64, "a wave's lanes hold four cells each");
+    // (c) exclusive prefixes over the cells: each wave scans one whole array
+    // (a lane its run of consecutive cells, then the wave's 64 sums), so no
+    // part sums cross waves and one barrier ends the step
+    static_assert(TCELLS == 4 * 64 && LONG_FC == 16 * 64 && nw == 8, "eight arrays, one per wave");
     (void)spart;
-    for (int a = wv; a < 10; a += nw) {  // uniform per wave
+    {
+        const int a = wv;  // 0, 1: the WD/disc cells; 2..7: the sub-bin tables' cells
         auto get = [&](int g) -> long long {
             switch (a) {
-            case 0: return W.cend[0][g];
-            case 1: return W.cend[1][g];
-            case 2: return W.cpre[0][g];
-            case 3: return W.cpre[1][g];
-            case 4: return T.dend[g];
-            case 5: return T.send[g];
-            case 6: return T.dpre[g][0];
-            case 7: return T.dpre[g][1];
-            case 8: return T.dpre[g][2];
+            case 0: return W.fend[0][g];
+            case 1: return W.fend[1][g];
+            case 2: return T.dend[g];
+            case 3: return T.send[g];
+            case 4: return T.dpre[g][0];
+            case 5: return T.dpre[g][1];
+            case 6: return T.dpre[g][2];
             default: return T.spre[g];
             }
         };
         auto set = [&](int g, long long x) {
             switch (a) {
-            case 0: W.cend[0][g] = int(x); break;
-            case 1: W.cend[1][g] = int(x); break;
-            case 2: W.cpre[0][g] = x; break;
-            case 3: W.cpre[1][g] = x; break;
-            case 4: T.dend[g] = int(x); break;
-            case 5: T.send[g] = int(x); break;
-            case 6: T.dpre[g][0] = x + T.dv0[0]; break;
-            case 7: T.dpre[g][1] = x + T.dv0[1]; break;
-            case 8: T.dpre[g][2] = x + T.dv0[2]; break;
+            case 0: W.fend[0][g] = int(x); break;
+            case 1: W.fend[1][g] = int(x); break;
+            case 2: T.dend[g] = int(x); break;
+            case 3: T.send[g] = int(x); break;
+            case 4: T.dpre[g][0] = x + T.dv0[0]; break;
+            case 5: T.dpre[g][1] = x + T.dv0[1]; break;
+            case 6: T.dpre[g][2] = x + T.dv0[2]; break;
             default: T.spre[g] = x; break;
             }
         };
-        long long c[4];
-        for (int j = 0; j < 4; ++j) c[j] = get(4 * lane + j);
-        const long long own = c[0] + c[1] + c[2] + c[3];
-        long long run = wave_scan_incl(own, lane) - own;
-        for (int j = 0; j < 4; ++j) {
-            set(4 * lane + j, run);
-            run += c[j];
+        if (a < 2) {  // 16 cells per lane, int counts: loaded once, in one round trip
+            constexpr int PER = LONG_FC / 64;
+            int* f = W.fend[a] + PER * lane;
+            int c[PER];
+            int own = 0;
+#pragma unroll
+            for (int j = 0; j < PER; ++j) {
+                c[j] = f[j];
+                own += c[j];
+            }
+            int run = int(wave_scan_incl(own, lane)) - own;
+#pragma unroll
+            for (int j = 0; j < PER; ++j) {
+                f[j] = run;
+                run += c[j];
+            }
+        } else {
+            constexpr int PER = TCELLS / 64;
+            const int g0 = PER * lane;
+            long long c[PER];
+            long long own = 0;
+#pragma unroll
+            for (int j = 0; j < PER; ++j) {
+                c[j] = get(g0 + j);
+                own += c[j];
+            }
+            long long run = wave_scan_incl(own, lane) - own;
+#pragma unroll
+            for (int j = 0; j < PER; ++j) {
+                set(g0 + j, run);
+                run += c[j];
+            }
         }
     }
     __syncthreads();
@@ -3379,10 +3399,10 @@ __device__ __forceinline__ void long_tables(LongTabs& W, SubTables& T, SubEntrie
         long long q;
         if (!wd_entry(g, ab, t, q)) continue;
         const int base = t ? NE_W : 0;
-        const int ia = atomicAdd(&W.cend[t][tcell(ab.x, t0[t], ginv[t])], 1);
+        const int ia = atomicAdd(&W.fend[t][long_cell(ab.x, t0[t], ginv[t])], 1);
         W.epos[base + ia] = ab.x;
         W.ecb[base + ia] = q;
-        const int ib = atomicAdd(&W.cend[t][tcell(ab.y, t0[t], ginv[t])], 1);
+        const int ib = atomicAdd(&W.fend[t][long_cell(ab.y, t0[t], ginv[t])], 1);
         W.epos[base + ib] = ab.y;
         W.ecb[base + ib] = -q;
     }
@@ -3415,8 +3435,7 @@ __device__ __forceinline__ void long_tables(LongTabs& W, SubTables& T, SubEntrie
     // contacts crowd).  WD/disc by (position, weight), donor by position with
     // an end before a start (sub_point's cursor), spot by (position, code):
     // total orders, so the tables (and long_window's double sums) do not
-    // depend on the atomics' slot order.  A WD/disc entry leaves C just after
-    // it: its cell's prefix, the weights of the entries before it, its own
+    // depend on the atomics' slot order
     {
         constexpr int RW = (NE_W + NE_D + nt - 1) / nt, RD = (TD_MAX + nt - 1) / nt;
         double wp[RW], dp[RD], sp = 0.0;
@@ -3428,22 +3447,19 @@ __device__ __forceinline__ void long_tables(LongTabs& W, SubTables& T, SubEntrie
             wp[r] = 0.0;
             wq[r] = 0;
             const int i = tid + r * nt, t = i < NE_W ? 0 : 1, base = t ? NE_W : 0, li = i - base;
-            if (i >= NE_W + NE_D || li >= W.cend[t][TCELLS - 1]) continue;
+            if (i >= NE_W + NE_D || li >= W.fend[t][LONG_FC - 1]) continue;
             const double p = W.epos[i];
             const long long q = W.ecb[i];
-            const int g = tcell(p, t0[t], ginv[t]), c0 = g ? W.cend[t][g - 1] : 0, c1 = W.cend[t][g];
+            const int g = long_cell(p, t0[t], ginv[t]), c0 = g ? W.fend[t][g - 1] : 0, c1 = W.fend[t][g];
             int rank = 0;
-            long long cb = W.cpre[t][g] + q;
 #pragma unroll 4
             for (int k = c0; k < c1; ++k) {
                 const double pk = W.epos[base + k];
                 const long long qk = W.ecb[base + k];
-                const bool before = pk < p || (pk == p && (qk < q || (qk == q && k < li)));
-                rank += before ? 1 : 0;
-                cb += before ? qk : 0;
+                rank += (pk < p || (pk == p && (qk < q || (qk == q && k < li)))) ? 1 : 0;
             }
             wp[r] = p;
-            wq[r] = cb;
+            wq[r] = q;
             wslot[r] = base + c0 + rank;
         }
         const int ndn = T.dend[TCELLS - 1], nsn = T.send[TCELLS - 1];
@@ -3503,30 +3519,24 @@ __device__ __forceinline__ void long_tables(LongTabs& W, SubTables& T, SubEntrie
     }
     __syncthreads();
     LONG_TSTAMP(5);
-    // (f) the fine index (over cpre, now spent): a thread per build cell
-    // counts its sorted entries below each of its four fine cells
-    if (tid < 2 * TCELLS) {
-        const int t = tid / TCELLS, g = tid % TCELLS, base = t ? NE_W : 0;
-        const int c0 = g ? W.cend[t][g - 1] : 0, c1 = W.cend[t][g];
-        const double fg = 4.0 * ginv[t];
-        int k = c0;
-        unsigned short f4[4];
-        for (int j = 0; j < 4; ++j) {
-            const int f = 4 * g + j;
-            for (; k < c1; ++k) {  // entries of fine cell < f (the same clamped index as long_find)
-                const double u = (W.epos[base + k] - t0[t]) * fg;
-                const int fk = u <= 0.0 ? 0 : (u >= double(LONG_FC - 1) ? LONG_FC - 1 : int(u));
-                if (fk >= f) break;
-            }
-            f4[j] = static_cast<unsigned short>(k);
+    // (f) C just after each sorted WD/disc entry: the running sum of the
+    // weights in table order (exact int64), a wave per table, a lane a run
+    if (wv < 2) {
+        const int t = wv, n = W.fend[t][LONG_FC - 1], B = (n + 63) >> 6, k0 = min(lane * B, n), k1 = min(k0 + B, n);
+        long long* q = W.ecb + (t ? NE_W : 0);
+        long long own = 0;
+        for (int k = k0; k < k1; ++k) own += q[k];
+        long long run = wave_scan_incl(own, lane) - own;
+        for (int k = k0; k < k1; ++k) {
+            run += q[k];
+            q[k] = run;
         }
-        for (int j = 0; j < 4; ++j) W.fcell[t][4 * g + j] = f4[j];
     }
     // (g) each unique donor tile's vector in fixed point, in place of its raw
     // components (the point phase adds them at its donor crossings; a mirror
     // image's components differ in sign only, and to_fx is odd)
-    if (tid < U_DON) {
-        double* dq = const_cast<double*>(sdq) + tid * DON_STRIDE;
+    if (tid >= 128 && tid < 128 + U_DON) {  // waves 2.. (0 and 1 run (f))
+        double* dq = const_cast<double*>(sdq) + (tid - 128) * DON_STRIDE;
         const long long q0 = to_fx(dq[0] * ivs), q1 = to_fx(dq[1] * ivs), q2 = to_fx(dq[2] * ivs);
         long long* dl = reinterpret_cast<long long*>(dq);
         dl[0] = q0;
@@ -3696,15 +3706,13 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
         if (lane == 0) sflagw[wv] = wf;
     }
     if constexpr (LONG) {  // the tables' counters and sums; the record for sub_point's LDS reads
+        for (int i = tid; i < 2 * LONG_FC; i += nt) (&LT.fend[0][0])[i] = 0;
         if (tid < TCELLS) {
-            LT.cpre[0][tid] = LT.cpre[1][tid] = 0;
-            LT.cend[0][tid] = LT.cend[1][tid] = 0;
             LST.dpre[tid][0] = LST.dpre[tid][1] = LST.dpre[tid][2] = 0;
             LST.spre[tid] = 0;
             LST.dend[tid] = LST.send[tid] = 0;
         } else if (tid < TCELLS + 3) {
             LST.dv0[tid - TCELLS] = 0;
-
         } else if (tid >= nt - LFG_NGEO) {
             LT.sgeo[tid - (nt - LFG_NGEO)] = G[tid - (nt - LFG_NGEO)];
         }

@@ -97,8 +97,8 @@ if LONG:
     if ok and lt.any():
         lt = lt[:, :nb].astype(np.float64)
         prev = t[9]
-        for k, nm in enumerate(("(a) hulls", "(b) counts, sums", "(c) cell scan", "(d) scatter", "(e) ranks",
-                                "(e) placed", "(f) fine index, (g) donor fx")):
+        for k, nm in enumerate(("(a) hulls", "(b) counts", "(c) cell scans", "(d) scatter", "(e) ranks",
+                                "(e) placed", "(f) C per entry, (g) donor fx")):
             d = (lt[k] - prev) / 100.0
             print("LONG table step %-28s median %6.2f  p90 %6.2f us" % (nm, np.median(d), np.percentile(d, 90)))
             prev = lt[k]
