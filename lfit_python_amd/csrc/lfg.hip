@@ -3209,13 +3209,14 @@ __device__ __forceinline__ double2 sub_point_c(const SubTables& T, const SubEntr
 }
 
 // the LONG tables from the element phase's results in LDS (all threads of
-// the block, after the phase barrier; five barriers).  abw: the WD/disc
+// the block, after the phase barrier; seven barriers).  abw: the WD/disc
 // intervals by sweep slot; the spot (sab, sbw), the donor tiles (sdq), the
 // disc ring weights (swt) and the spot / donor fixed-point totals (stot) as
 // k_pair's point-major sinks leave them.  The tables must be zero (k_pair's
-// prologue clears them)
+// prologue clears them).  Step (g) rewrites each unique donor tile's first
+// three sdq words as its fixed-point vector (the point phase's form)
 __device__ __forceinline__ void long_tables(LongTabs& W, SubTables& T, SubEntries& D, const double2* abw,
-                                            const double2* sab, const double* sbw, const double* sdq,
+                                            const double2* sab, const double* sbw, double* sdq,
                                             const double* swt, const unsigned long long* stot, double ul, double itwd,
                                             long long (*spart)[LIKE_THREADS / 64], int tid)
 {
@@ -3536,7 +3537,7 @@ __device__ __forceinline__ void long_tables(LongTabs& W, SubTables& T, SubEntrie
     // components (the point phase adds them at its donor crossings; a mirror
     // image's components differ in sign only, and to_fx is odd)
     if (tid >= 128 && tid < 128 + U_DON) {  // waves 2.. (0 and 1 run (f))
-        double* dq = const_cast<double*>(sdq) + (tid - 128) * DON_STRIDE;
+        double* dq = sdq + (tid - 128) * DON_STRIDE;
         const long long q0 = to_fx(dq[0] * ivs), q1 = to_fx(dq[1] * ivs), q2 = to_fx(dq[2] * ivs);
         long long* dl = reinterpret_cast<long long*>(dq);
         dl[0] = q0;

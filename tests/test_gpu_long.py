@@ -158,3 +158,24 @@ def test_long_spec_chain_equals_plain_chain():
     for a, b in zip(got, out[0]):
         np.testing.assert_array_equal(a, b)
     assert torch.isfinite(torch.as_tensor(out[0][1])).all()
+
+
+def test_long_equal_shares_beyond_block_table(oracle):
+    """180 000 points: more blocks of 64 than the spent LDS holds for the
+    cost partition (2 800 ints), so the waves take equal shares of the blocks
+    (k_pair LONG's fallback); S = 1, against the oracle"""
+    import torch
+    from lfit_python_amd import _native, batch
+    npts = 180000
+    assert (npts + 63) // 64 + 1 > 2800
+    m = _model(oracle, npts, 1, "sorted")
+    t = batch.compile_tree(m, nsub=1)
+    ev = batch.LnProbEvaluator(t)
+    assert _native.lib().lfg_layout(ctypes.byref(ev.ctree)) == 2
+    W = 8
+    walk = _walkers(m, W, 5)
+    got = ev(torch.as_tensor(walk, device="cuda")).cpu().numpy()
+    ref, _, _ = oracle.lnprob_batch(walk, t, nsub=1)
+    assert np.isfinite(ref).sum() >= W // 2
+    _same(got, ref, LNP_RTOL)
+
