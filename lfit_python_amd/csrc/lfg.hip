@@ -3067,13 +3067,19 @@ __device__ __forceinline__ double2 long_wd_disc(const LongTabs& W, const LongU& 
 // from there instead of a fresh lookup (a thread's run of sorted points);
 // the line of sight is formed afresh at each point's first sub-bin
 // the donor cursor runs two entries ahead: the next entry's position, code
-// and tile vector (fixed point: long_tables' step (g)) and the one after's
+// and tile vector (fixed point as a double: long_tables' step (g)) and the one after's
 // position and code are in registers, their loads issued a crossing earlier
 // -- a crossing applies the vector and moves the pipe on without waiting on LDS
+// the donor sum V of the point phase, in fixed-point units but held as a
+// double: the sub-bin sums take it without an int64 -> double conversion per
+// sub-bin (12 instructions; 2.72 -> 2.91 M evals/s at config 5).  The sum
+// over a thread's crossings rounds, ~1e-15 of V's scale, against exact int64
+// (the tables' cell prefixes and the tiles' vectors stay exact)
+using LongV = double;
 struct SubCur {
     double ph, npos, n2pos;
-    long long nq[3];  // the next entry's tile vector (fixed point, before the mirror's signs)
-    long long vx, vy, vz;
+    LongV nq[3];  // the next entry's tile vector (fixed point, before the mirror's signs)
+    LongV vx, vy, vz;
     int cur, ncode, n2code;
 };
 
@@ -3083,7 +3089,7 @@ __device__ __forceinline__ void subcur_fill(const SubEntries& D, const double* s
     U.ncode = U.cur < nd ? D.dcode[U.cur] : 0;
     U.n2pos = U.cur + 1 < nd ? D.dpos[U.cur + 1] : INFINITY;
     U.n2code = U.cur + 1 < nd ? D.dcode[U.cur + 1] : 0;
-    const long long* dq = reinterpret_cast<const long long*>(sdq + ((U.ncode >> 1) >> 2) * DON_STRIDE);
+    const LongV* dq = reinterpret_cast<const LongV*>(sdq + ((U.ncode >> 1) >> 2) * DON_STRIDE);
     U.nq[0] = dq[0]; U.nq[1] = dq[1]; U.nq[2] = dq[2];
 }
 
@@ -3103,18 +3109,17 @@ __device__ __forceinline__ int long_weight(const LongU& K, double ph0, double w)
 }
 
 // a crossing of entry cur: its vector into V (the mirror image's signs on the
-// unique tile's fixed-point vector: donor_apply's sums, exactly), then the
-// pipe one entry on
+// unique tile's fixed-point vector), then the pipe one entry on
 __device__ __forceinline__ void subcur_cross(const SubEntries& D, const double* sdq, int nd, SubCur& U)
 {
     const int code = U.ncode, mr = (code >> 1) & 3;
-    const long long qx = U.nq[0], qy = (mr & 1) ? -U.nq[1] : U.nq[1], qz = (mr & 2) ? -U.nq[2] : U.nq[2];
+    const LongV qx = U.nq[0], qy = (mr & 1) ? -U.nq[1] : U.nq[1], qz = (mr & 2) ? -U.nq[2] : U.nq[2];
     if (code & 1) { U.vx -= qx; U.vy -= qy; U.vz -= qz; }
     else { U.vx += qx; U.vy += qy; U.vz += qz; }
     ++U.cur;
     U.npos = U.n2pos;
     U.ncode = U.n2code;
-    const long long* dq = reinterpret_cast<const long long*>(sdq + ((U.ncode >> 1) >> 2) * DON_STRIDE);
+    const LongV* dq = reinterpret_cast<const LongV*>(sdq + ((U.ncode >> 1) >> 2) * DON_STRIDE);
     U.nq[0] = dq[0]; U.nq[1] = dq[1]; U.nq[2] = dq[2];
     U.n2pos = U.cur + 1 < nd ? D.dpos[U.cur + 1] : INFINITY;
     U.n2code = U.cur + 1 < nd ? D.dcode[U.cur + 1] : 0;
@@ -3138,16 +3143,16 @@ __device__ __forceinline__ double2 sub_point_c(const SubTables& T, const SubEntr
         if (!(phn >= U.ph)) {  // a fresh lookup (the first point, a step back in phase)
             {  // sub_donor with the tiles' fixed-point vectors
                 const int g = tcell(phn, T.dt0, T.dginv);
-                U.vx = T.dpre[g][0];
-                U.vy = T.dpre[g][1];
-                U.vz = T.dpre[g][2];
+                U.vx = LongV(T.dpre[g][0]);
+                U.vy = LongV(T.dpre[g][1]);
+                U.vz = LongV(T.dpre[g][2]);
                 int i = g ? T.dend[g - 1] : 0;
                 for (const int ie = T.dend[g]; i < ie; ++i) {
                     const int code = D.dcode[i];
                     if (!donor_counted(D.dpos[i], code, phn)) break;
                     const int mr = (code >> 1) & 3;
-                    const long long* dq = reinterpret_cast<const long long*>(sdq + ((code >> 1) >> 2) * DON_STRIDE);
-                    const long long qx = dq[0], qy = (mr & 1) ? -dq[1] : dq[1], qz = (mr & 2) ? -dq[2] : dq[2];
+                    const LongV* dq = reinterpret_cast<const LongV*>(sdq + ((code >> 1) >> 2) * DON_STRIDE);
+                    const LongV qx = dq[0], qy = (mr & 1) ? -dq[1] : dq[1], qz = (mr & 2) ? -dq[2] : dq[2];
                     if (code & 1) { U.vx -= qx; U.vy -= qy; U.vz -= qz; }
                     else { U.vx += qx; U.vy += qy; U.vz += qz; }
                 }
@@ -3214,7 +3219,7 @@ __device__ __forceinline__ double2 sub_point_c(const SubTables& T, const SubEntr
 // disc ring weights (swt) and the spot / donor fixed-point totals (stot) as
 // k_pair's point-major sinks leave them.  The tables must be zero (k_pair's
 // prologue clears them).  Step (g) rewrites each unique donor tile's first
-// three sdq words as its fixed-point vector (the point phase's form)
+// three sdq words as its fixed-point vector in doubles (the point phase's form)
 __device__ __forceinline__ void long_tables(LongTabs& W, SubTables& T, SubEntries& D, const double2* abw,
                                             const double2* sab, const double* sbw, double* sdq,
                                             const double* swt, const unsigned long long* stot, double ul, double itwd,
@@ -3533,13 +3538,14 @@ __device__ __forceinline__ void long_tables(LongTabs& W, SubTables& T, SubEntrie
             q[k] = run;
         }
     }
-    // (g) each unique donor tile's vector in fixed point, in place of its raw
-    // components (the point phase adds them at its donor crossings; a mirror
-    // image's components differ in sign only, and to_fx is odd)
+    // (g) each unique donor tile's vector in fixed point (held as doubles),
+    // in place of its raw components (the point phase adds them at its donor
+    // crossings; a mirror image's components differ in sign only, and to_fx
+    // is odd)
     if (tid >= 128 && tid < 128 + U_DON) {  // waves 2.. (0 and 1 run (f))
         double* dq = sdq + (tid - 128) * DON_STRIDE;
         const long long q0 = to_fx(dq[0] * ivs), q1 = to_fx(dq[1] * ivs), q2 = to_fx(dq[2] * ivs);
-        long long* dl = reinterpret_cast<long long*>(dq);
+        LongV* dl = reinterpret_cast<LongV*>(dq);
         dl[0] = q0;
         dl[1] = q1;
         dl[2] = q2;
@@ -3981,7 +3987,7 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
         unsigned long long tl_wd = 0, tl_sub = 0;
         int lctr[3] = {0, 0, 0};
 #endif
-        SubCur SC{INFINITY, INFINITY, INFINITY, {0, 0, 0}, 0, 0, 0, 0, 0, 0
+        SubCur SC{INFINITY, INFINITY, INFINITY, {0, 0, 0}, LongV(0), LongV(0), LongV(0), 0, 0, 0
         };
         const LongU KU = long_uniforms(LT, LST, S);
         const double fspS = uni(fsp / S), frsS = uni(frs / S);
