@@ -5315,6 +5315,17 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
                            rows * sizeof(double), hipMemcpyDeviceToDevice, st) != hipSuccess)
             return LFG_E_LAUNCH;
     }
+    if (sp && sp->out && fold && T->E == 1 && pair_eligible(T->gp, T->nsub, T->max_n, T->ndim)) {
+        // the deferred acceptance on the two-kernel layout: a fold k_pair
+        // launch snapshots its own half's rows (final until its verdicts are
+        // applied) for the next launch's speculative lanes; leave the same
+        // snapshot, so that a layout switch before the next half reads it valid
+        const int h = prop->half;
+        const size_t rows = size_t(prop->ns) * T->ndim;
+        if (hipMemcpyAsync(ws.snap + size_t(h) * ws.accstride * T->ndim, prop->pos + size_t(h) * rows,
+                           rows * sizeof(double), hipMemcpyDeviceToDevice, st) != hipSuccess)
+            return LFG_E_LAUNCH;
+    }
     if (T->gp) {
         L.res = ws.res;
         L.gpx = ws.gpx;
@@ -5676,7 +5687,16 @@ int lfg_debug_setup_cycles(unsigned long long* host)
 #endif
 __attribute__((used)) const char lfg_src_hash_tag[] = "lfg-src-hash:" LFG_SRC_HASH;
 
-const char* lfg_version(void) { return "lfg 0.4.0 gfx950 fp64 layout=pair src=" LFG_SRC_HASH; }
+const char* lfg_version(void)
+{
+    // the layout named is the one lfg_set_layout / LFG_PAIR currently select
+    // for eligible trees (pair: k_pair and k_pair LONG; two_kernel: k_elements
+    // + k_lnlike); lfg_layout(T) gives a given tree's kernels
+    int m = g_pair_layout.load(std::memory_order_relaxed);
+    if (m == -2) m = pair_env() ? 1 : 0;
+    return m == 1 ? "lfg 0.5.0 gfx950 fp64 layout=pair src=" LFG_SRC_HASH
+                  : "lfg 0.5.0 gfx950 fp64 layout=two_kernel src=" LFG_SRC_HASH;
+}
 
 #ifdef LFG_COUNT_ITERS
 // diagnostic builds only: read and clear the iteration counters of k_elements

@@ -132,6 +132,7 @@ class EnsembleSampler:
         self._chunks = []
         self._cat = None
         self._last = None  # the most recent run's chunk (None: it stored nothing)
+        self._active = None  # the chunk of a run in progress (sample() generator, run_mcmc)
         self.offload = True
         self.timer = None  # optional callable(walkers) -> lnp used instead of self.ev
         # one process, HIP moves, an evaluator with the fused entry: proposal,
@@ -324,7 +325,14 @@ class EnsembleSampler:
         self.replay(self._graph)
 
     def step(self):
-        """One emcee iteration: both halves, in place."""
+        """One emcee iteration: both halves, in place.
+
+        On the sharded fold path (lfg_stretch_step_shard_fold) the last
+        half-step's acceptance stays pending after step() returns: it is
+        applied by the next step's first launch.  The ensemble is current
+        through the pos / lnp / naccept / naccepted / acceptance_fraction
+        properties, or after sync() or close(); the raw _pos / _lnp tensors
+        lag one half-step until then."""
         if self._pending is not None and not (
                 (self.world > 1 or self.force_shard) and self.fuse_shard and self.timer is None and self._fold_ok()):
             self.sync()  # a path without the deferred acceptance follows
@@ -435,7 +443,8 @@ class EnsembleSampler:
 
     def close(self):
         """Release the direct RCCL communicator (every rank, before the
-        process group is destroyed)."""
+        process group is destroyed); pending verdicts are applied first."""
+        self.sync()
         if self._rccl:
             self._rccl.close()
         self._rccl = None
@@ -461,6 +470,7 @@ class EnsembleSampler:
                torch.empty((n, self.W), dtype=torch.float64, device=self.dev))
         self._chunks.append(buf)
         self._last = buf
+        self._active = buf   # written step by step until _end()
         self._cat = None
         return buf, thin
 
@@ -468,6 +478,8 @@ class EnsembleSampler:
         """end of a stored run: its device chunk moves to host memory
         (offload); rows: the chunk's rows actually written (a sample()
         generator left early), the rest is dropped"""
+        if buf is not None and self._active is buf:
+            self._active = None
         if buf is not None and rows is not None and rows < buf[0].shape[0]:
             cut = (buf[0][:rows], buf[1][:rows])
             self._chunks = [cut if c is buf else c for c in self._chunks]
@@ -494,6 +506,7 @@ class EnsembleSampler:
         if buf is not None and i % thin == 0:
             buf[0][i // thin].copy_(self._pos)
             buf[1][i // thin].copy_(self._lnp)
+            self._cat = None   # a concatenation taken mid-run is a copy: re-take it
 
     def sample(self, p0=None, lnprob0=None, rstate0=None, blobs0=None, iterations=1, thin=1,
                storechain=True, store=None, skip_initial_state_check=False, **kwargs):
@@ -549,7 +562,10 @@ class EnsembleSampler:
             elif len(self._chunks) == 1:
                 self._cat = self._chunks[0]
             else:
-                on_host = all(c.device.type == "cpu" for c, _ in self._chunks)
+                # a run still in progress keeps writing its chunk: only a
+                # chain of finished host chunks collapses into one
+                on_host = (all(c.device.type == "cpu" for c, _ in self._chunks) and
+                           not any(c is self._active for c in self._chunks))
                 last = self._chunks[-1]
                 self._cat = (torch.cat([c.cpu() for c, _ in self._chunks]),
                              torch.cat([l.cpu() for _, l in self._chunks]))
@@ -603,10 +619,12 @@ class EnsembleSampler:
 
     @property
     def naccepted(self):
+        self.sync()   # the last half-step's verdicts may still be pending
         return self._naccept.cpu().numpy()
 
     @property
     def acceptance_fraction(self):
+        self.sync()
         return (self._naccept.double() / max(self.iteration, 1)).cpu().numpy()
 
     def reset(self):
@@ -618,6 +636,7 @@ class EnsembleSampler:
         self._chunks = []
         self._cat = None
         self._last = None
+        self._active = None
 
     @property
     def random_state(self):

@@ -16,6 +16,10 @@ def pytest_configure(config):
 
 
 def pytest_collection_modifyitems(config, items):
+    # wall-clock (perf) tests run after every parity test, so that under -x a
+    # timing wobble on a shared host cannot hide the parity suite (stable
+    # sort: both groups keep their collection order)
+    items.sort(key=lambda item: "perf" in item.keywords)
     try:
         import torch
         has_gpu = torch.cuda.is_available()

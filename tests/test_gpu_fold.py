@@ -27,14 +27,15 @@ def _fused_chain(t, ev, init, seed, iters):
     return (S.chain_dev.cpu().numpy(), S.lnprob_dev.cpu().numpy(), S.naccept.cpu().numpy()), lnp0
 
 
-def _rank_chains(t, init, lnp0, seed, iters, R, evs=None, check_verdicts=True):
+def _rank_chains(t, init, lnp0, seed, iters, R, evs=None, check_verdicts=True, layouts=None):
     """R evaluators (R ranks' workspaces), each holding the whole ensemble and
     running lfg_stretch_step_shard_fold on walkers k n .. (k+1) n - 1 of every
     half; the verdict shards concatenated as the all_gather hands them over.
     A step's state is recorded once its last verdicts are applied: right
-    after the next step's half-0 launches (or after the final flush)."""
+    after the next step's half-0 launches (or after the final flush).
+    layouts: optional lfg_set_layout value per half-step (2 it + half)."""
     import torch
-    from lfit_python_amd import batch
+    from lfit_python_amd import _native, batch
     W = init.shape[0]
     n = W // 2 // R
     f64 = dict(dtype=torch.float64, device="cuda")
@@ -58,6 +59,8 @@ def _rank_chains(t, init, lnp0, seed, iters, R, evs=None, check_verdicts=True):
     for it in range(iters):
         for half in (0, 1):
             vprev = V[1 - half]
+            if layouts is not None:
+                _native.lib().lfg_set_layout(int(layouts[2 * it + half]))
             for k in range(R):
                 key = evs[k]._spec_key
                 spec_used += int(key is not None and key[-2:] == (half, it) and vprev is not None)
@@ -107,6 +110,31 @@ def test_fold_config2_matches_fused(R, layout):
     assert spec_used == R * (2 * 4 - 1)
     for a, b in zip(got, ref):
         np.testing.assert_array_equal(a, b)
+
+
+def test_fold_layout_switch_between_halves_matches_fused():
+    """lfg_set_layout between the halves of a deferred-acceptance chain (the
+    contract include/lfg.h states): a two-kernel half-step followed by a fold
+    k_pair half-step whose speculative lanes read the snapshot of the rows
+    through the pending verdicts.  The two-kernel fallback leaves the same
+    snapshot a fold k_pair launch leaves, so the chain follows the fused one
+    whatever the switch pattern: positions and acceptance counts bit-identical,
+    ln_prob to 1e-12 (the two layouts' sums differ in the last bits; a stale
+    snapshot gives wrong candidates, i.e. different positions)."""
+    from lfit_python_amd import _native
+    m, t, ev0, init = _ensemble("c2", seed=3)
+    init = init[:256]
+    ref, lnp0 = _fused_chain(t, ev0, init, 19, 5)
+    pattern = [1, 0, 1, 0, 0, 1, 1, 0, 1, 1]   # pair / two-kernel per half-step
+    prev = _native.lib().lfg_set_layout(1)
+    try:
+        for R in (1, 2):
+            got, _, _ = _rank_chains(t, init, lnp0, 19, 5, R, layouts=pattern)
+            np.testing.assert_array_equal(got[0], ref[0])
+            np.testing.assert_array_equal(got[2], ref[2])
+            np.testing.assert_allclose(got[1], ref[1], rtol=1e-12, atol=0)
+    finally:
+        _native.lib().lfg_set_layout(prev)
 
 
 def test_fold_e6_tree_fallback_matches_fused():

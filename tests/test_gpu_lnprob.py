@@ -134,13 +134,16 @@ def test_prior_rejected_walkers_stay_fast(cfg):
     ev = batch.LnProbEvaluator(t)
     x = torch.as_tensor(walk, device="cuda")
     ev(x)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(5):
+    times = []
+    for _ in range(5):   # the fastest of five calls: a host stall cannot decide it
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
         ev(x)
-    torch.cuda.synchronize()
-    per = (time.perf_counter() - t0) / 5
-    assert per < 2e-3, "ln_prob of %d walkers took %.2f ms" % (len(walk), per * 1e3)
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    per = min(times)
+    assert per < 2e-3, "ln_prob of %d walkers took %.2f ms (calls: %s)" % (
+        len(walk), per * 1e3, np.round(np.array(times) * 1e3, 3))
 
 
 @pytest.mark.parametrize("cfg", ["c2_complex", "c3_tree", "gp"])
@@ -177,8 +180,19 @@ def test_long_chain_keeps_its_pace():
     """A config-2 chain (1024 walkers) must not slow down as it leaves the
     starting ball: proposals outside the prior box once ran the nested
     solver on non-finite geometry for milliseconds (tools/chain_drift.py).
+
     Blocks of 30 steps after the first 60 (the failure set in from step
-    ~150): no block may take twice the fastest (the failure was 2.5-6x)."""
+    ~150; it was a sustained 2.5-6x slowdown of every later step).  Each
+    step is bracketed by HIP events on the evaluator's stream, so a step's
+    DEVICE time excludes host stalls between steps; the assertion is on the
+    median step of each block (one slow step cannot decide it, a slow path
+    that sets in does), with host and device times both in the message.
+    The chain is deterministic (seed 7, Philox, exact fixed-point sums), so
+    its device work is the same on every box; round 5's driver run saw one
+    block of 15.4 ms host time against 2.3-2.5 ms for the other seven, which
+    the same library did not repeat on another box: a host-side stall, not
+    the kernels.  The timed blocks also run with the Python GC off."""
+    import gc
     import time
     import torch
     from lfit_python_amd import batch, sampler, synthetic
@@ -193,16 +207,32 @@ def test_long_chain_keeps_its_pace():
     S.set_state(init)
     for _ in range(60):
         S.step()
-    blocks = []
-    for _ in range(8):
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(30):
-            S.step()
-        torch.cuda.synchronize()
-        blocks.append(time.perf_counter() - t0)
+    nb, ns = 8, 30
+    ev_s = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(nb * ns)]
+    host = []
+    gc_was = gc.isenabled()
+    gc.disable()
+    try:
+        for b in range(nb):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for s in range(ns):
+                e0, e1 = ev_s[b * ns + s]
+                e0.record()
+                S.step()
+                e1.record()
+            torch.cuda.synchronize()
+            host.append(time.perf_counter() - t0)
+    finally:
+        if gc_was:
+            gc.enable()
     S.close()
-    assert max(blocks) < 2.0 * min(blocks), "30-step blocks (ms): %s" % np.round(np.array(blocks) * 1e3, 2)
+    dev = np.array([e0.elapsed_time(e1) for e0, e1 in ev_s]).reshape(nb, ns)   # ms per step
+    med = np.median(dev, axis=1)
+    msg = ("per-step device median by block (us): %s; device block sums (ms): %s; host blocks (ms): %s"
+           % (np.round(med * 1e3, 1), np.round(dev.sum(1), 2), np.round(np.array(host) * 1e3, 2)))
+    print(msg)
+    assert med.max() < 2.0 * med.min(), msg
     assert np.all(np.isfinite(S.lnp.cpu().numpy()))
 
 

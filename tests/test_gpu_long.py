@@ -2,8 +2,9 @@
 sub-binned exposures (the reference's lc.w exposure path with sub-samples,
 /root/reference/CVModel.py:29-30, :64; BASELINE config 5) in one launch per
 half-step: the element phase keeps its results in LDS, per-pair breakpoint
-tables replace the two-kernel hand-off, and each thread evaluates a run of
-points on its own.  Every case against the oracle (oracle.lnprob_batch, the
+tables replace the two-kernel hand-off, and the points are dealt in blocks
+of 64 to waves by estimated cost, each wave taking a range of blocks with its
+lanes interleaved (a step of a wave reads 64 consecutive points).  Every case against the oracle (oracle.lnprob_batch, the
 flux -> chi^2 restatement of MODEL_SPEC 3, 5) at LNP_RTOL, through lfg_lnprob
 (compiled trees) and lfg_lnlike."""
 import ctypes

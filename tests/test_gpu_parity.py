@@ -209,11 +209,14 @@ def test_absurd_geometry_stays_fast():
     pars[1::4, 14] = 1e-3
     x, w = phase_grid(300)
     flux_batch(pars, x, w)        # warm
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    flux_batch(pars, x, w)
-    torch.cuda.synchronize()
-    assert time.perf_counter() - t0 < 0.05
+    times = []
+    for _ in range(3):   # the fastest of three: a host stall cannot decide it
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        flux_batch(pars, x, w)
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    assert min(times) < 0.05, "flux_batch calls (s): %s" % np.round(times, 4)
 
 
 def test_cv_object_api(oracle):

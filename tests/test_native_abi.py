@@ -108,9 +108,11 @@ def test_layout_switch_without_gpu():
         assert L.lfg_layout(tree(5, 300)) == 2     # sub-binned: k_pair LONG
         assert L.lfg_layout(tree(1, 10000)) == 2   # more points than a tile: LONG
         assert L.lfg_layout(tree(1, 10000, gp=1)) == 0   # a long GP eclipse: two kernels
+        assert b" layout=pair " in L.lfg_version()
         assert L.lfg_set_layout(0) == 1
         assert L.lfg_layout(tree(1, 300)) == 0
         assert L.lfg_layout(tree(5, 10000)) == 0
+        assert b" layout=two_kernel " in L.lfg_version()   # the version names the layout in force
     finally:
         L.lfg_set_layout(prev)
 
