@@ -2661,6 +2661,35 @@ struct PairArgs {
     double fa = 2.0;               // the stretch scale a
 };
 
+// The kernel-argument segment as a typed constant pointer whose value the
+// compiler cannot see through.  k_pair's arguments are ~1 KB; the compiler
+// loaded the speculative lanes' two SetupArgs (560 B, used by wave 0 of a few
+// blocks) at every wave's entry and spilled them into VGPR lanes, a chain of
+// ~15 dependent scalar-load waits (~3 us) ahead of the candidate chain.
+// Fields read through this pointer are loaded where they are used.
+template <typename T>
+__device__ __forceinline__ const __attribute__((address_space(4))) T* opaque_kernargs()
+{
+    auto p = (const __attribute__((address_space(4))) T*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return p;
+}
+
+// a by-value copy of a kernel-argument struct read through such a pointer
+// (word by word: the struct's copy constructor takes a generic reference)
+template <typename T>
+__device__ __forceinline__ T kernarg_copy(const __attribute__((address_space(4))) T* p)
+{
+    static_assert(sizeof(T) % 8 == 0, "whole words");
+    const auto* src = reinterpret_cast<const __attribute__((address_space(4))) unsigned long long*>(p);
+    unsigned long long w[sizeof(T) / 8];
+#pragma unroll
+    for (int i = 0; i < int(sizeof(T) / 8); ++i) w[i] = src[i];
+    T out;
+    __builtin_memcpy(&out, w, sizeof(T));
+    return out;
+}
+
 // the chunks of k_pair's element jobs 1..15, longest first (spot, outer
 // disc, donor, inner disc, WD: the Newton steps per region)
 __constant__ int kJobChunk[15] = {11, 12, 10, 9, 8, 13, 14, 7, 6, 5, 4, 3, 2, 1, 0};
@@ -2671,7 +2700,7 @@ __constant__ int kJobChunk[15] = {11, 12, 10, 9, 8, 13, 14, 7, 6, 5, 4, 3, 2, 1,
 constexpr double PAIR_SPOT_S = 1.0 / 128.0, PAIR_DON_S = 1.0 / 8.0;
 
 #ifdef LFG_PROFILE_PAIR  // diagnostic build only: s_memrealtime (100 MHz) stamps of each block's phases
-__device__ unsigned long long g_pair_t[20][4096];
+__device__ unsigned long long g_pair_t[24][4096];
 #define PAIR_STAMP(slot, cond)                                                     \
     do {                                                                           \
         if ((cond) && blockIdx.x < 4096) g_pair_t[slot][blockIdx.x] = __builtin_amdgcn_s_memrealtime(); \
@@ -3603,6 +3632,9 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
     constexpr int nt = LIKE_THREADS, nw = LIKE_THREADS / 64;
     const int pair = blockIdx.x, npairs = L.npairs;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+#ifdef LFG_ABL_EMPTY  // (diagnostic builds) the launch alone: traffic and instructions of an empty k_pair
+    if (pair >= 0) return;
+#endif
     PAIR_STAMP(0, tid == 0);
 #ifdef LFG_PROFILE_PAIR
     if (tid == 0 && blockIdx.x < 4096) {
@@ -3634,6 +3666,7 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
         xw_0 = xe[0];
         xw_1 = xe[n - 1];
     }
+    PAIR_STAMP(20, tid == 0 && n != -7);
     if (!LONG && L.w && n > 0) {
         const double* we = L.w + o0;
         ww_own = we[pl];
@@ -3659,6 +3692,7 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
         const double rp0 = G0[G_RPRIOR] + G0[G_RPRIOR_BS], rp1 = G1[G_RPRIOR] + G1[G_RPRIOR_BS];
         const double ph0 = G0[G_PHI0], ph1 = G1[G_PHI0];
         const int jw = int(__umulhi(draw(A.jseed, A.jstep, A.jhalf, 0, A.jlo + w).z, unsigned(A.jns)));
+        PAIR_STAMP(21, tid == 0 && jw != -7);
         if (FOLD)  // the partner's pending verdict: accepted unless NaN
             cand = __builtin_amdgcn_readfirstlane(int(!isnan(A.fv[__builtin_amdgcn_readfirstlane(jw)])));
         else
@@ -3846,7 +3880,10 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
             // candidate uniform per block: X.S[c] stays in scalar registers
             const int c = pair < A.nbc ? 0 : 1;
             const int t = (pair - c * A.nbc) * A.spl + lane;
-            if (t < X.nspec) setup_any<FOLD>(X.S[__builtin_amdgcn_readfirstlane(c)], t);
+            if (t < X.nspec) {  // the SetupArgs loaded here, not at the kernel's entry (opaque_kernargs)
+                const SetupArgs Sc = kernarg_copy(&opaque_kernargs<PairArgs>()->X.S[__builtin_amdgcn_readfirstlane(c)]);
+                setup_any<FOLD>(Sc, t);
+            }
 #ifdef LFG_PROFILE_PAIR
             if (lane == 0 && blockIdx.x < 4096) {
                 const int np = X.S[0].W * X.S[0].E;
@@ -3936,6 +3973,7 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
         // wave priority falls with each job a wave starts, so that the two
         // workgroups of a CU advance together (the issue arbiter otherwise
         // favours the older workgroup's waves)
+#ifndef LFG_ABL_ELEM  // (diagnostic builds) no element jobs: the prologue, setup lanes and likelihood alone
         PAIR_PRIO(3);
         if (!specblk) chunk(wv + 1);
         else if (wv > 0) chunk(wv);
@@ -3946,6 +3984,10 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
         PAIR_PRIO(1);
         if (j < 16) chunk(j);
         PAIR_PRIO(0);
+#else
+        (void)chunk;
+        (void)grab;
+#endif
         K.flush();
     }
     static_assert(11 * 64 >= U_WD + U_DISC && 10 * 64 < U_WD + U_DISC, "11 chunks of WD/disc");
@@ -3971,6 +4013,10 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
     }
     // ---- each point's flux and chi^2 (GP: residual, changepoint block)
     double chi = 0.0;
+#ifdef LFG_ABL_LIKE  // (diagnostic builds) no likelihood phase: chi^2 = 0
+    if (false) {
+    } else
+#endif
     if constexpr (LONG) {
         // the pair's tables, then this wave's range of the points (lanes interleaved)
         const double ul = Gc[G_ULIMB];

@@ -61,7 +61,7 @@ print("W %d: ln_prob call median %.2f us (p10 %.2f, p90 %.2f); finite %d" % (
     W, np.median(ts), np.percentile(ts, 10), np.percentile(ts, 90), int(torch.isfinite(lp).sum())))
 nb = W
 if hasattr(L, "lfg_debug_pair_jobs"):
-    t = np.zeros((20, 4096), dtype=np.uint64)
+    t = np.zeros((24, 4096), dtype=np.uint64)
     L.lfg_debug_pair(ctypes.c_void_p(t.ctypes.data))
     t = t[:, :nb].astype(np.float64)
     t0 = t[0]

@@ -40,7 +40,7 @@ S.set_state(init)
 for _ in range(10):
     S.step()
 torch.cuda.synchronize()
-t = np.zeros((20, 4096), dtype=np.uint64)
+t = np.zeros((24, 4096), dtype=np.uint64)
 assert L.lfg_debug_pair(ctypes.c_void_p(t.ctypes.data)) == 0
 nb = W // 2
 t = t[:, :nb].astype(np.float64)
@@ -48,7 +48,7 @@ t0 = t[0]
 span = (t[15].max() - t0.min()) / 100.0
 print("blocks %d, launch span %.2f us (first start -> last finish)" % (nb, span))
 print("block start spread: %s us" % np.percentile((t0 - t0.min()) / 100.0, [0, 50, 90, 100]).round(2))
-rows = [("candidate known", 10), ("own window (phi0)", 11), ("prologue before B0", 19), ("B0 (prologue)", 16)] + [("wave %d elements" % k, 1 + k) for k in range(8)] + [
+rows = [("kernargs, n known", 20), ("partner drawn", 21), ("candidate known", 10), ("own window (phi0)", 11), ("prologue before B0", 19), ("B0 (prologue)", 16)] + [("wave %d elements" % k, 1 + k) for k in range(8)] + [
     ("B1 (phase barrier)", 9)] + ([("LONG tables built", 12), ("LONG points, chi^2", 13), ("finish", 15)] if LONG else [
     ("B2 (items, norms)", 10), ("B3 (cells)", 11), ("scan", 12), ("chi^2", 13), ("finish", 15)])
 for name, k in rows:
