@@ -28,9 +28,12 @@ must equal --gpus.
 Kernel timing: the last warmup step records HIP events around every kernel
 (include/lfg.h LFG_NEV, on the caller stream all kernels run on) and picks
 the dominant kernel; in the timed region every --time-every-th ln_prob call
-records a start/stop event pair around that kernel only.  (A timing event is
-a queue barrier: events around all kernels cost ~20 % of the step, so they
-stay out of the timed region.)
+records a start/stop event pair around that kernel only (default every 20th:
+two samples at the driver's 20 steps, ten at 100).  A timing event is a queue
+barrier: events around all kernels cost ~20 % of the step, so they stay out
+of the timed region; a pair on every 8th call cost 1.2 % of the config-2 line
+against none (12.08 vs 12.23 M evals/s, one box, three rounds), every 40th
+nothing measurable.
 
 Roofline (MODEL_SPEC.md section 11; the path is FP64-VALU or latency bound,
 neither HBM- nor MFMA-bound):
@@ -141,7 +144,7 @@ def parse(argv=None):
                          "W/2/N walkers evaluated per half, a one-rank RCCL exchange of the shard, the acceptance "
                          "over the whole half); also times the fused one-GPU step and reports the implied 1->N ratio")
     ap.add_argument("--seed", type=int, default=20261015)
-    ap.add_argument("--time-every", type=int, default=8,
+    ap.add_argument("--time-every", type=int, default=20,
                     help="record the dominant kernel's event pair on every k-th ln_prob call of the timed region")
     args = ap.parse_args(argv)
     cfg = CONFIGS[args.config]
