@@ -926,7 +926,11 @@ __device__ inline int bspot(const Roche& R, double rad, double out[4], const QPa
     for (int k = 1; k < LFG_ST_NS; ++k)
         if (js == k) { lo = kStSb[k]; w = kStSb[k + 1] - kStSb[k]; }
     const double xs = 2.0 * (s - lo) / w - 1.0;
+#ifdef LFG_ABL_STTAB  // (diagnostic builds) every lane reads patch 0: the table's share of the traffic
+    const double* c = kStCoef + 0 * size_t(iq * LFG_ST_NS + js);
+#else
     const double* c = kStCoef + size_t(iq * LFG_ST_NS + js) * 3 * ST_PATCH;
+#endif
     double sp, cp;
     sincos(st_patch(c, xq, xs), &sp, &cp);
     out[0] = rad * cp;
