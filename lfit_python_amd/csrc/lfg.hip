@@ -3122,6 +3122,15 @@ __device__ __forceinline__ void subcur_fill(const SubEntries& D, const double* s
     U.nq[0] = dq[0]; U.nq[1] = dq[1]; U.nq[2] = dq[2];
 }
 
+#ifndef LFG_LW_BASE
+#define LFG_LW_BASE 3
+#endif
+#ifndef LFG_LW_WD
+#define LFG_LW_WD 2
+#endif
+#ifndef LFG_LW_SPOT
+#define LFG_LW_SPOT 3
+#endif
 // a point's estimated cost in the LONG point phase (the partition of the
 // points over the threads): windows in the WD/disc hulls walk the tables,
 // those in the spot hull the spot entries at every sub-bin
@@ -3133,8 +3142,10 @@ __device__ __forceinline__ int long_weight(const LongU& K, double ph0, double w)
         wd = wd || (hi >= K.amin[t] && lo <= K.bmax[t]) || (-lo >= K.amin[t] && -hi <= K.bmax[t]);
     const bool sp = hi >= K.sa && lo <= K.sb;
     // weights from A/B runs at config 5 (wave ranges with interleaved lanes):
-    // 5/3/1 2.39 M evals/s, 5/8/2 2.34, 5/1/1 2.31, uniform 2.36
-    return 5 + (wd ? 3 : 0) + (sp ? 1 : 0);
+    // 5/3/1 2.39 M evals/s, 5/8/2 2.34, 5/1/1 2.31, uniform 2.36 (round 5);
+    // round 6, with the quiet points in closed form: the spot hull's points
+    // all take the sub-bin loop (LFG_LW_* to retune)
+    return LFG_LW_BASE + (wd ? LFG_LW_WD : 0) + (sp ? LFG_LW_SPOT : 0);
 }
 
 // a crossing of entry cur: its vector into V (the mirror image's signs on the
@@ -3240,6 +3251,136 @@ __device__ __forceinline__ double2 sub_point_c(const SubTables& T, const SubEntr
         sbs = fma(fma(K.omf, fmax(fma(K.nbs0, cs, fma(K.nbs1, sn, K.nbc)), 0.0), K.fis), 1.0 - ebj, sbs);
     }
     return make_double2(sbs * K.ibden, fma(K.sg, srs1, K.cg * srs2) * K.dsc);
+}
+
+// ---- LONG quiet points: sub_point_c's sums in closed form ----
+// A point is quiet when, over its window [ph - w, ph + w] (S sub-bins):
+//  * no donor entry is counted between its first and its last sub-bin (the
+//    donor vector V is the same at every sub-bin),
+//  * the window is off the spot's hull (no sub-bin sees the spot eclipsed),
+//  * the beaming term b(phi) = nbs0 cos 2 pi phi + nbs1 sin 2 pi phi + nbc
+//    keeps one sign (neither of its two zero crossings lies in the window),
+//  * the window neither wraps at +-0.5 nor has a zero or NaN width.
+// The sub-bins' lines of sight then sum to D (cos, sin)(2 pi ph) with the
+// Dirichlet kernel D = sin(2 pi w) / sin(2 pi w / S) (the sub-bin centres lie
+// symmetrically about ph, 2 h apart), every sum of sub_point_c is linear in
+// them, and the point costs one sincospi instead of S sub-bin steps.
+// (Config 5: ~80 % of the points; the sub-bin sums were 57 % of the point
+// phase's VALU instructions.)  The others run sub_point_c.
+struct LongB {          // the beaming term's zero crossings, per pair (uniform)
+    double z0, z1;      // phases in [-0.5, 0.5)
+    int any;            // 0: b keeps one sign over the orbit
+};
+
+__device__ __forceinline__ LongB long_beam_zeros(const LongU& K)
+{
+    LongB B{0.0, 0.0, 0};
+    const double R = sqrt(K.nbs0 * K.nbs0 + K.nbs1 * K.nbs1);
+    if (R > fabs(K.nbc)) {  // b = R cos(2 pi phi - t) + nbc crosses zero twice
+        const double t = atan2(K.nbs1, K.nbs0), a = acos(-K.nbc / R);
+        B.z0 = uni(wrap_phase((t - a) * (1.0 / TWO_PI)));
+        B.z1 = uni(wrap_phase((t + a) * (1.0 / TWO_PI)));
+        B.any = 1;
+    }
+    return B;
+}
+
+// sin(x) / x, |x| < 0.1: the series to x^10 (error < 2e-22)
+__device__ __forceinline__ double sinc_small(double x)
+{
+    const double x2 = x * x;
+    return fma(x2, fma(x2, fma(x2, fma(x2, fma(x2, -1.0 / 39916800.0, 1.0 / 362880.0), -1.0 / 5040.0),
+                               1.0 / 120.0), -1.0 / 6.0), 1.0);
+}
+
+// true and the sums (as sub_point_c returns them) for a quiet point; false
+// for the others.  Either way U is left at the point's first sub-bin, as
+// sub_point_c's first step leaves it (the cursor walks on from there)
+__device__ __forceinline__ bool sub_point_quiet(const SubTables& T, const SubEntries& D, const double* sbw,
+                                                const double* sdq, const LongU& K, const LongB& B, double ph0,
+                                                double wk, int S, SubCur& U, double2& out)
+{
+    const double h = wk * K.invS;
+#ifdef LFG_COUNT_QUIET  // (diagnostic builds, with LFG_COUNT_ITERS: lfg_diag_iters) why points are not quiet
+#define QCNT(k) atomicAdd(g_iter_dbg + 56 + (k), 1ull)
+    QCNT(0);
+#else
+#define QCNT(k)
+#endif
+#ifdef LFG_ABL_QNONE  // (diagnostic builds) every point through the queue and sub_point_c
+    return false;
+#endif
+    if (!(h > 0.0)) { QCNT(1); return false; }  // zero or NaN widths
+    const double phc = wrap_phase(ph0), lo = phc - wk, hi = phc + wk;
+    constexpr double EPS = 1e-9;   // margins on the phase tests (the sub-bin loop's own phases round)
+#ifndef LFG_ABL_QALL  // (diagnostic builds: every point in closed form, a timing floor; wrong sums)
+    if (!(lo > -0.5 + EPS && hi < 0.5 - EPS)) { QCNT(2); return false; }
+    // the spot: the window off its hull, or inside it (then no spot entry may lie in the window)
+    const bool inspot = hi + EPS > K.sa && lo - EPS < K.sb;
+    if (inspot && !(lo - EPS > K.sa && hi + EPS < K.sb)) { QCNT(3); return false; }
+    if (B.any && ((B.z0 > lo - EPS && B.z0 < hi + EPS) || (B.z1 > lo - EPS && B.z1 < hi + EPS))) { QCNT(4); return false; }
+#endif
+    // the donor vector at the first sub-bin, as sub_point_c finds it
+    const int nd = K.nd;
+    const double ph1 = wrap_phase(ph0 - wk + h);
+    if (!(ph1 >= U.ph)) {
+        const int g = tcell(ph1, T.dt0, T.dginv);
+        U.vx = LongV(T.dpre[g][0]);
+        U.vy = LongV(T.dpre[g][1]);
+        U.vz = LongV(T.dpre[g][2]);
+        int i = g ? T.dend[g - 1] : 0;
+        for (const int ie = T.dend[g]; i < ie; ++i) {
+            const int code = D.dcode[i];
+            if (!donor_counted(D.dpos[i], code, ph1)) break;
+            const int mr = (code >> 1) & 3;
+            const LongV* dq = reinterpret_cast<const LongV*>(sdq + ((code >> 1) >> 2) * DON_STRIDE);
+            const LongV qx = dq[0], qy = (mr & 1) ? -dq[1] : dq[1], qz = (mr & 2) ? -dq[2] : dq[2];
+            if (code & 1) { U.vx -= qx; U.vy -= qy; U.vz -= qz; }
+            else { U.vx += qx; U.vy += qy; U.vz += qz; }
+        }
+        U.cur = i;
+        subcur_fill(D, sdq, nd, U);
+    } else {
+        while (donor_counted(U.npos, U.ncode, ph1)) subcur_cross(D, sdq, nd, U);
+    }
+    U.ph = ph1;
+    const double phS = wrap_phase(ph0 - wk + (2 * S - 1) * h);  // the last sub-bin
+#ifndef LFG_ABL_QALL
+    // an entry counted by a later sub-bin moves V inside the window: the
+    // sub-bin loop (a closed form per crossing, Dirichlet kernels of the
+    // sub-bins after it, held more registers than the loop has: 25-42
+    // spilled VGPRs, slower than the loop on 4 % of the points)
+    if (donor_counted(U.npos, U.ncode, phS)) { QCNT(5); return false; }
+#endif
+    // the spot's covering weight at the first sub-bin's lo, as sub_point_c
+    // takes it (spot_C); with no entry up to the last sub-bin's hi it is the
+    // eclipsed fraction of every sub-bin
+    double E = 0.0;
+    if (inspot) {
+        int cur;
+        const long long C = spot_C(T, sbw, K.itb, ph1 - h, cur);
+        if (cur < K.nsp && T.spos[cur] <= phS + h + EPS) { QCNT(3); return false; }
+        E = double(C) * FX_INV;
+    }
+    // the Dirichlet kernel of the sub-bins' turn (2 pi 2 h per sub-bin)
+    const double x = TWO_PI * wk, xs = TWO_PI * h;
+    double Dk;
+    if (x < 0.1) {
+        Dk = S * (sinc_small(x) / sinc_small(xs));
+    } else {
+        const double2 a = sincospi_ool(2.0 * wk), b = sincospi_ool(2.0 * h);
+        Dk = a.x / b.x;
+    }
+    const double2 e = sincospi_ool(2.0 * phc);  // (sin, cos) at the window's centre
+    const double Scs = Dk * e.y, Ssn = Dk * e.x;
+    const double srs1 = fma(Scs, double(U.vx), -Ssn * double(U.vy)), srs2 = S * double(U.vz);
+    const double bc = fma(K.nbs0, e.y, fma(K.nbs1, e.x, K.nbc));  // b at the centre: its sign in the window
+    const double sbs = (1.0 - E) * (bc > 0.0 ? fma(K.omf, fma(K.nbs0, Scs, fma(K.nbs1, Ssn, S * K.nbc)), S * K.fis)
+                                             : S * K.fis);
+    out = make_double2(sbs * K.ibden, fma(K.sg, srs1, K.cg * srs2) * K.dsc);
+    QCNT(6);
+    return true;
+#undef QCNT
 }
 
 // the LONG tables from the element phase's results in LDS (all threads of
@@ -4053,14 +4194,14 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
         // passes its eighth of the total; its lanes interleaved, so every step
         // reads 64 consecutive points and the lanes of a wave stand at
         // neighbouring phases (the same branches of the lookups)
+        constexpr int LAB_INTS = int(NU_WDD * sizeof(double2) / sizeof(int));  // the spent interval table, as ints
         int p0, p1;
         {
             constexpr int nw = LIKE_THREADS / 64;
             const int nch = (n + 63) >> 6;
             int* cw = reinterpret_cast<int*>(Lab);  // the WD/disc intervals are spent
             int b0, b1;
-            constexpr int LAB_INTS = int(NU_WDD * sizeof(double2) / sizeof(int));
-            if (nch + 1 <= LAB_INTS) {
+            if (nch + 1 <= LAB_INTS - 8 * 128) {  // (the point phase's queues take the last 8 x 128 ints)
                 for (int c = wv; c < nch; c += nw) {
                     const int p = c * 64 + lane;
                     int wt = p < n ? long_weight(KU, xe[p] - phi0, we ? we[p] : 0.0) : 0;
@@ -4101,54 +4242,90 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
             p0 = __builtin_amdgcn_readfirstlane(b0) * 64 + lane;
             p1 = min(__builtin_amdgcn_readfirstlane(b1) * 64, n);
         }
-        constexpr int PSTEP = 64;
-        {
-            double xn = p0 < p1 ? xe[p0] : 0.0, wn = (p0 < p1 && we) ? we[p0] : 0.0;
-        for (int p = p0; p < p1; p += PSTEP) {
-#ifdef LFG_ABL_GLOAD  // (diagnostic builds) no global loads in the point loop: a synthetic grid
-            const double xp = -0.3 + p * 6.0006e-5, wp = 3.0003e-5, yp = 1.0, ep = 0.004;
-            (void)xn; (void)wn;
-#else
-            const double xp = xn, wp = wn, yp = ye[p], ep = ee[p];
-            if (p + PSTEP < p1) {  // the next point's phase and width, in flight during this one
-                xn = xe[p + PSTEP];
-                wn = we ? we[p + PSTEP] : 0.0;
-            }
-#endif
+        // Pass 1 over the wave's points (steps of 64, lanes interleaved): the
+        // WD/disc windows, and the sub-bin sums in closed form where the point
+        // is quiet (sub_point_quiet).  The other points go to the wave's queue
+        // (a ring of LQ_CAP indices in the spent interval table, in index
+        // order); each time it holds 64 they run sub_point_c with every lane
+        // busy (pass 2), and the rest after the last step.  Every point's
+        // chi^2 term is added once, by the lane that finishes it.
+        constexpr int LQ_CAP = 128;
+        int* const lq = reinterpret_cast<int*>(Lab) + (LAB_INTS - 8 * LQ_CAP) + wv * LQ_CAP;
+        const LongB KB = long_beam_zeros(KU);
+        int qhead = 0, qtail = 0;  // uniform over the wave
+        auto full_point = [&](int p) {  // sub_point_c's path for point p
+            const double xp = xe[p], wp = we ? we[p] : 0.0, yp = ye[p], ep = ee[p];
             const double wk = wp < 0.0 ? 0.0 : wp;  // MODEL_SPEC 3 (NaN stays NaN)
             const double ph0 = xp - phi0, phc = wrap_phase(ph0);
-#ifdef LFG_PROFILE_PAIR  // per-lane cycles of the two model parts (the wave's max lane: g_pair_w[1..2])
-            const unsigned long long tq0 = __builtin_amdgcn_s_memtime();
-#endif
-#ifdef LFG_ABL_LWD
-            const double2 f2 = make_double2(phc * 1e-30, wk * 1e-30);
-#else
-#ifdef LFG_PROFILE_PAIR
-            const double2 f2 = long_wd_disc(LT, KU, phc, wk, lctr);
-#else
             const double2 f2 = long_wd_disc(LT, KU, phc, wk);
-#endif
-#endif
-#ifdef LFG_PROFILE_PAIR
-            __builtin_amdgcn_s_waitcnt(0);
-            const unsigned long long tq1 = __builtin_amdgcn_s_memtime();
-            tl_wd += (tq1 - tq0) + (f2.x == 12345.0 ? 1 : 0);
-#endif
-#ifdef LFG_ABL_LSUB
-            const double2 r2 = make_double2(phc * 1e-30, wk * 1e-30);
-#else
             const double2 r2 = sub_point_c(LST, LSE, sab, sbw, sdq, KU, ph0, wk, S, SC);
-#endif
-#ifdef LFG_PROFILE_PAIR
-            __builtin_amdgcn_s_waitcnt(0);
-            tl_sub += (__builtin_amdgcn_s_memtime() - tq1) + (r2.x == 12345.0 ? 1 : 0);
-#endif
-            // k_lnlike's sum, term for term (MODEL_SPEC 3: a NaN width, a NaN flux)
             const double f = isnan(wk) ? NAN : fwd * (1.0 - f2.x) + fds * (1.0 - f2.y) + fspS * r2.x + frsS * r2.y;
             const double rr = (yp - f) / ep;
             chi += isnan(f) ? INFINITY : rr * rr;
+        };
+        auto run_queue = [&](int cnt) {  // pass 2: cnt <= 64 queued points, one per lane
+            if (lane < cnt) full_point(lq[(qhead + lane) & (LQ_CAP - 1)]);
+            qhead += cnt;
+            // the queued points lie behind pass 1 (the cursor's fresh lookup
+            // took them), and walking the cursor back up from there re-crossed
+            // every entry in between: pass 1's next point looks afresh (one cell)
+            SC.ph = INFINITY;
+        };
+        const int pw0 = p0 - lane;  // the wave's first point (uniform)
+        // the next step's phase and width, in flight during this one
+        double xn = p0 < p1 ? xe[p0] : 0.0, wn = (p0 < p1 && we) ? we[p0] : 0.0;
+        for (int base = pw0; base < p1; base += 64) {
+            const int p = base + lane;
+            bool defer = false;
+            if (p < p1) {
+#ifdef LFG_ABL_GLOAD  // (diagnostic builds) no global loads in the point loop: a synthetic grid
+                const double xp = -0.3 + p * 6.0006e-5, wp = 3.0003e-5, yp = 1.0, ep = 0.004;
+                (void)xn; (void)wn;
+#else
+                const double xp = xn, wp = wn, yp = ye[p], ep = ee[p];
+                if (p + 64 < p1) {
+                    xn = xe[p + 64];
+                    wn = we ? we[p + 64] : 0.0;
+                }
+#endif
+                const double wk = wp < 0.0 ? 0.0 : wp;  // MODEL_SPEC 3 (NaN stays NaN)
+                const double ph0 = xp - phi0, phc = wrap_phase(ph0);
+                double2 r2;
+#ifdef LFG_ABL_LSUB
+                r2 = make_double2(phc * 1e-30, wk * 1e-30);
+                const bool quiet = true;
+#else
+                const bool quiet = sub_point_quiet(LST, LSE, sbw, sdq, KU, KB, ph0, wk, S, SC, r2);
+#endif
+                if (quiet) {
+#ifdef LFG_ABL_LWD
+                    const double2 f2 = make_double2(phc * 1e-30, wk * 1e-30);
+#else
+                    const double2 f2 = long_wd_disc(LT, KU, phc, wk);
+#endif
+                    // k_lnlike's sum, term for term (MODEL_SPEC 3: a NaN width, a NaN flux)
+                    const double f = fwd * (1.0 - f2.x) + fds * (1.0 - f2.y) + fspS * r2.x + frsS * r2.y;
+                    const double rr = (yp - f) / ep;
+                    chi += isnan(f) ? INFINITY : rr * rr;
+                } else {
+                    defer = true;
+                }
+            }
+            const unsigned long long m = __ballot(defer);
+            if (defer)
+                lq[(qtail + __builtin_amdgcn_mbcnt_hi(unsigned(m >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(m), 0u))) &
+                   (LQ_CAP - 1)] = p;
+            qtail += __popcll(m);
+#ifdef LFG_PROFILE_PAIR  // (diagnostic builds) the block's quiet and queued points
+            const unsigned long long mact = __ballot(p < p1);
+            if (lane == 0 && blockIdx.x < 4096) {
+                atomicAdd(&g_pair_t[22][blockIdx.x], (unsigned long long)__popcll(mact & ~m));
+                atomicAdd(&g_pair_t[23][blockIdx.x], (unsigned long long)__popcll(m));
+            }
+#endif
+            if (qtail - qhead >= 64) run_queue(64);
         }
-        }
+        if (qtail > qhead) run_queue(qtail - qhead);
         PAIR_WSTAMP(0);  // (diagnostic builds) this wave's points done
 #ifdef LFG_PROFILE_PAIR
         {

@@ -102,6 +102,9 @@ if LONG:
             d = (lt[k] - prev) / 100.0
             print("LONG table step %-28s median %6.2f  p90 %6.2f us" % (nm, np.median(d), np.percentile(d, 90)))
             prev = lt[k]
+if LONG and t[22].any():  # the quiet-point pass (round 6): points in closed form / queued for the sub-bin loop
+    qq, qd = t[22].sum(), t[23].sum()
+    print("LONG points in closed form %d, queued %d (%.1f %% quiet)" % (qq, qd, 100.0 * qq / max(qq + qd, 1)))
 if LONG and wv.any():
     d = (wv[0] - t[12][None, :]) / 100.0
     print("LONG point loop per wave after the tables (us, median over blocks): %s" % np.median(d, axis=1).round(2))
