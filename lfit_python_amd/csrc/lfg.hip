@@ -2631,6 +2631,35 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_lnlike(LikeArgs L)
 typedef const __attribute__((address_space(4))) double* CGeo;
 constexpr int DCP_LANES = 16, DCP_NTHETA = 10;  // k_gp_dcp / k_pair<true>: limb points of wdphases
 
+// The arguments of k_pair's prologue chains, contiguous, read at the entry in
+// one batch of scalar loads (kernarg_copy): the compiler otherwise issued them
+// in ~10 rounds, each behind an s_waitcnt for every outstanding load, ahead of
+// the candidate chain.  Copies of the LikeArgs / ElemSpec / PairArgs fields
+// of the same names (fill_hot, on the host, before each launch), typed by
+// address space: the uniform read-only words constant (scalar loads), the
+// points global (a copied generic pointer would make flat loads)
+typedef const __attribute__((address_space(4))) int* KInt;
+typedef const __attribute__((address_space(4))) double* KDbl;
+typedef const __attribute__((address_space(1))) double* GDbl;
+struct PairHot {
+    KInt accflag;   // X.accflag (the partner half's flags: this launch writes the other half's)
+    KDbl fv;        // fv (FOLD)
+    KInt jk;        // X.jk
+    KInt statusC;   // X.statusC, X.bstatusC, X.priorC, X.geoC (this half's candidates; the
+    KInt bstatusC;  //   speculative lanes write the next half's)
+    KDbl priorC;
+    KDbl geoC;
+    KDbl geo;       // L.geo, L.status, L.bstatus, L.prior (read before B0; wave 7 writes
+    KInt status;    //   the standard slots after it)
+    KInt bstatus;
+    KDbl prior;
+    KInt off;       // L.off, L.x, L.w
+    GDbl x;
+    GDbl w;
+    unsigned long long jseed, jstep;
+    int jhalf, jlo, jns, E, N, npairs;
+};
+
 struct PairArgs {
     LikeArgs L;
     ElemSpec X;                // candidate selection (X.jk) and speculative lanes (X.nspec, X.S)
@@ -2659,7 +2688,36 @@ struct PairArgs {
     double* fsnap = nullptr;  // [jns][ndim]: this half's rows, for the next launch's speculative lanes
     unsigned long long fstep = 0;  // the step of the pending moves' proposals
     double fa = 2.0;               // the stretch scale a
+    PairHot hot{};                 // fill_hot
 };
+
+// PairArgs.hot from the fields it copies (every k_pair launch, last)
+static void fill_hot(PairArgs& A)
+{
+    PairHot& H = A.hot;
+    H.accflag = (KInt)A.X.accflag;
+    H.fv = (KDbl)A.fv;
+    H.jk = (KInt)A.X.jk;
+    H.statusC = (KInt)A.X.statusC;
+    H.bstatusC = (KInt)A.X.bstatusC;
+    H.priorC = (KDbl)A.X.priorC;
+    H.geoC = (KDbl)A.X.geoC;
+    H.geo = (KDbl)A.L.geo;
+    H.status = (KInt)A.L.status;
+    H.bstatus = (KInt)A.L.bstatus;
+    H.prior = (KDbl)A.L.prior;
+    H.off = (KInt)A.L.off;
+    H.x = (GDbl)A.L.x;
+    H.w = (GDbl)A.L.w;
+    H.jseed = A.jseed;
+    H.jstep = A.jstep;
+    H.jhalf = A.jhalf;
+    H.jlo = A.jlo;
+    H.jns = A.jns;
+    H.E = A.L.E;
+    H.N = A.L.N;
+    H.npairs = A.L.npairs;
+}
 
 // The kernel-argument segment as a typed constant pointer whose value the
 // compiler cannot see through.  k_pair's arguments are ~1 KB; the compiler
@@ -3771,7 +3829,9 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
     __shared__ long long lspart[10][LIKE_THREADS / 64];
 
     constexpr int nt = LIKE_THREADS, nw = LIKE_THREADS / 64;
-    const int pair = blockIdx.x, npairs = L.npairs;
+    // the prologue's arguments in one batch of scalar loads (PairHot)
+    const PairHot H = kernarg_copy(&opaque_kernargs<PairArgs>()->hot);
+    const int pair = blockIdx.x, npairs = H.npairs;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
 #ifdef LFG_ABL_EMPTY  // (diagnostic builds) the launch alone: traffic and instructions of an empty k_pair
     if (pair >= 0) return;
@@ -3786,19 +3846,19 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
         g_pair_t[18][blockIdx.x] = xcc;
     }
 #endif
-    const int E = L.E;
+    const int E = H.E;
     const int w = (E == 1) ? pair : pair / E, e = (E == 1) ? 0 : pair - w * E;
     const int nwk = npairs / E;  // walkers of the batch
-    const bool offs = L.off && E > 1;
-    const int o0 = offs ? L.off[e] : 0;
-    const int n = offs ? L.off[e + 1] - o0 : L.N;
+    const bool offs = H.off && E > 1;
+    const int o0 = offs ? H.off[e] : 0;
+    const int n = offs ? H.off[e + 1] - o0 : H.N;
 
     // the point loads the windows need, issued first: they overlap the
     // candidate chain below (own point, predecessor, first and last)
     const bool own = !LONG && tid < n;
     const int m = n;
     const int pl = own ? tid : 0;
-    const double* xe = L.x + o0;
+    const GDbl xe = H.x + o0;
     double xw_own = 0.0, xw_prv = 0.0, xw_0 = 0.0, xw_1 = 0.0;
     double ww_own = 0.0, ww_prv = 0.0, ww_0 = 0.0, ww_1 = 0.0;
     if (!LONG && n > 0) {
@@ -3808,8 +3868,8 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
         xw_1 = xe[n - 1];
     }
     PAIR_STAMP(20, tid == 0 && n != -7);
-    if (!LONG && L.w && n > 0) {
-        const double* we = L.w + o0;
+    if (!LONG && H.w && n > 0) {
+        const GDbl we = H.w + o0;
         ww_own = we[pl];
         ww_prv = we[pl > 0 ? pl - 1 : 0];
         ww_0 = we[0];
@@ -3824,32 +3884,32 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
     const double* G;
     int st0, bst, cand = 0;
     double lpr = 0.0, zf = 0.0, rpr, phi0;
-    if (X.jk) {
+    if (H.jk) {
         const size_t c0 = size_t(pair), c1 = size_t(npairs) + pair;
-        const int sa0 = X.statusC[c0], sa1 = X.statusC[c1], sb0 = X.bstatusC[c0], sb1 = X.bstatusC[c1];
-        const double lp0 = X.priorC[w], lp1 = X.priorC[size_t(nwk) + w];
-        const double* G0 = X.geoC + c0 * LFG_NGEO;
-        const double* G1 = X.geoC + c1 * LFG_NGEO;
+        const int sa0 = H.statusC[c0], sa1 = H.statusC[c1], sb0 = H.bstatusC[c0], sb1 = H.bstatusC[c1];
+        const double lp0 = H.priorC[w], lp1 = H.priorC[size_t(nwk) + w];
+        const KDbl G0 = H.geoC + c0 * LFG_NGEO;
+        const KDbl G1 = H.geoC + c1 * LFG_NGEO;
         const double rp0 = G0[G_RPRIOR] + G0[G_RPRIOR_BS], rp1 = G1[G_RPRIOR] + G1[G_RPRIOR_BS];
         const double ph0 = G0[G_PHI0], ph1 = G1[G_PHI0];
-        const int jw = int(__umulhi(draw(A.jseed, A.jstep, A.jhalf, 0, A.jlo + w).z, unsigned(A.jns)));
+        const int jw = int(__umulhi(draw(H.jseed, H.jstep, H.jhalf, 0, H.jlo + w).z, unsigned(H.jns)));
         PAIR_STAMP(21, tid == 0 && jw != -7);
         if (FOLD)  // the partner's pending verdict: accepted unless NaN
-            cand = __builtin_amdgcn_readfirstlane(int(!isnan(A.fv[__builtin_amdgcn_readfirstlane(jw)])));
+            cand = __builtin_amdgcn_readfirstlane(int(!isnan(H.fv[__builtin_amdgcn_readfirstlane(jw)])));
         else
-            cand = __builtin_amdgcn_readfirstlane(X.accflag[__builtin_amdgcn_readfirstlane(jw)]);
+            cand = __builtin_amdgcn_readfirstlane(H.accflag[__builtin_amdgcn_readfirstlane(jw)]);
         PAIR_STAMP(10, tid == 0 && cand >= 0);
-        G = cand ? G1 : G0;
+        G = (const double*)(cand ? G1 : G0);
         st0 = cand ? sa1 : sa0;
         bst = cand ? sb1 : sb0;
         lpr = cand ? lp1 : lp0;
         rpr = cand ? rp1 : rp0;
         phi0 = cand ? ph1 : ph0;
     } else {
-        G = L.geo + size_t(pair) * LFG_NGEO;
-        st0 = L.status[pair];
-        bst = L.bstatus[pair];
-        if (L.prior) lpr = L.prior[w];
+        G = (const double*)(H.geo + size_t(pair) * LFG_NGEO);
+        st0 = H.status[pair];
+        bst = H.bstatus[pair];
+        if (H.prior) lpr = H.prior[w];
         rpr = G[G_RPRIOR] + G[G_RPRIOR_BS];
         phi0 = G[G_PHI0];
     }
@@ -3858,7 +3918,7 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
     // reads: the standard slot it copies into is not G when X.jk is set)
     const CGeo Gc = (CGeo)(G);
     const int stp = (st0 != ST_OK) ? st0 : bst;  // MODEL_SPEC 6 order: setup failures first
-    const bool prej = L.prior && !(lpr + rpr > -INFINITY);  // prior_rejects
+    const bool prej = H.prior && !(lpr + rpr > -INFINITY);  // prior_rejects
     const int st = (stp == ST_OK && prej) ? -1 : stp;  // -1: prior-rejected, straight to the -inf finish
     const bool acc1 = L.pos && E == 1;
     // this thread's point (one tile: m = n points): window and phase into LDS,
@@ -5287,7 +5347,8 @@ int lfg_lnlike(const double* pars, int W, int P, const double* x, const double* 
                nsub, nullptr, nullptr, lnlike, W, nullptr, nullptr, nullptr, false, nullptr,
                nullptr, nullptr, nullptr, 0, 0, 0ull, 0ull, nullptr};
     L.bstatus = ws.bstatus;
-    const PairArgs A{L, ElemSpec{}, nullptr, nullptr, 64, 0, 0ull, 0ull, 0, 0, 0, pair_prio(W)};
+    PairArgs A{L, ElemSpec{}, nullptr, nullptr, 64, 0, 0ull, 0ull, 0, 0, 0, pair_prio(W)};
+    fill_hot(A);
     if (kind == 2) hipLaunchKernelGGL((k_pair<false, false, true>), dim3(W), dim3(LIKE_THREADS), 0, st, A);
     else if (pair) hipLaunchKernelGGL(k_pair<false>, dim3(W), dim3(LIKE_THREADS), 0, st, A);
     else if (nsub > 1) hipLaunchKernelGGL((k_lnlike<1, true>), dim3(W), dim3(LIKE_THREADS), 0, st, L);
@@ -5488,6 +5549,7 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
             A.L.step = prop->step;
             A.L.half = h;
             A.L.zfac = prop->zfac;
+            fill_hot(A);
             if (kind == 2) hipLaunchKernelGGL((k_pair<false, true, true>), dim3(npairs), dim3(LIKE_THREADS), 0, st, A);
             else hipLaunchKernelGGL((k_pair<false, true>), dim3(npairs), dim3(LIKE_THREADS), 0, st, A);
             if ((rc = launch_ok())) return rc;
@@ -5513,12 +5575,15 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
             L.gpx = ws.gpx;
             L.gpb = ws.gpb;
             A.L = L;
+            fill_hot(A);
             hipLaunchKernelGGL(k_pair<true>, dim3(npairs), dim3(LIKE_THREADS), 0, st, A);
             if ((rc = launch_ok())) return rc;
             hipLaunchKernelGGL(k_gp_like, dim3(T->E * ((W + GP_PAIRS - 1) / GP_PAIRS)), dim3(GP_BLOCK), 0, st, L);
         } else if (kind == 2) {
+            fill_hot(A);
             hipLaunchKernelGGL((k_pair<false, false, true>), dim3(npairs), dim3(LIKE_THREADS), 0, st, A);
         } else {
+            fill_hot(A);
             hipLaunchKernelGGL(k_pair<false>, dim3(npairs), dim3(LIKE_THREADS), 0, st, A);
         }
         if ((rc = launch_ok())) return rc;
