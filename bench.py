@@ -71,7 +71,7 @@ sys.path.insert(0, ROOT)
 # MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md; FP64 vector = spec)
 HBM_PEAK_GBS = 8000.0
 FP64_PEAK_TFLOPS = 78.6
-PMC_DIR = os.path.join(ROOT, "profiles", "r05")   # pmc_traffic_<config>.json (tools/pmc_traffic.py)
+PMC_DIR = os.path.join(ROOT, "profiles", "r06")   # pmc_traffic_<config>.json (tools/pmc_traffic.py)
 
 NEV = 4  # LFG_NEV (include/lfg.h)
 # (name as rocprofv3 prints it, start event, end event) per kernel layout

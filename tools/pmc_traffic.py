@@ -1,7 +1,7 @@
 """HBM traffic per launch from the FETCH_SIZE / WRITE_SIZE passes of
 tools/pmc_profile.sh, for bench.py's roofline.traffic.
 
-  python tools/pmc_traffic.py gpurun_out/pmc_<tag> profiles/r03/pmc_traffic_c2.json [pairs [npts nsub]]
+  python tools/pmc_traffic.py gpurun_out/pmc_<tag> profiles/r03/pmc_traffic_c2.json [pairs [npts nsub [grid]]]
 
 pairs = (walker, eclipse) pairs per launch of the profiled run (bench.py
 defaults: 512 = 1024 walkers / 2 halves x 1 eclipse); bench.py scales by it.
@@ -47,7 +47,7 @@ def per_dispatch(d, counter):
     return out
 
 
-def summarise(d):
+def summarise(d, grid=None):
     fetch = per_dispatch(d, "FETCH_SIZE")
     write = per_dispatch(d, "WRITE_SIZE")
     flops = per_dispatch(d, "SQ_INSTS_VALU_FLOPS_FP64")  # per wave instruction: x64 lanes
@@ -61,7 +61,8 @@ def summarise(d):
             vals = src.get(kn, [])
             if not vals:
                 continue
-            g = collections.Counter(gs for gs, _ in vals).most_common(1)[0][0]
+            g = grid if grid and any(gs == grid for gs, _ in vals) else \
+                collections.Counter(gs for gs, _ in vals).most_common(1)[0][0]
             sel = sorted(v for gs, v in vals if gs == g)
             row[name] = sel[len(sel) // 2] * KIB * corr
             row["grid"] = g
@@ -75,7 +76,9 @@ def summarise(d):
 if __name__ == "__main__":
     src, dst = sys.argv[1], sys.argv[2]
     pairs = int(sys.argv[3]) if len(sys.argv) > 3 else 512
-    res = summarise(src)
+    # optional 6th argument: the grid size of the timed launches (when as many
+    # other launches of the kernel ran, e.g. initialise_walkers' larger batch)
+    res = summarise(src, int(sys.argv[6]) if len(sys.argv) > 6 else None)
     meta = {"source": os.path.basename(os.path.normpath(src)), "pairs_per_launch": pairs,
             "npts": int(sys.argv[4]) if len(sys.argv) > 4 else 300,
             "nsub": int(sys.argv[5]) if len(sys.argv) > 5 else 1,
