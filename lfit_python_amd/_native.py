@@ -25,6 +25,10 @@ if os.environ.get("LFG_LIB"):
                            "request (unset LFG_LIB to load %s)" % (os.environ["LFG_LIB"], LIB_PATH))
     LOAD_PATH = os.environ["LFG_LIB"]
 SOURCES = [os.path.join(_HERE, "csrc", "lfg.hip"), os.path.join(_HERE, "csrc", "lfg_components.hip")]
+# k_pair's fold and LONG instantiations: lfg.hip again, compiled on its own
+# without machine LICM (the reason: lfg.hip, lfg_pair_launch_split)
+SPLIT_SOURCE = os.path.join(_HERE, "csrc", "lfg_pair_split.hip")
+SPLIT_FLAGS = ["-mllvm", "-disable-machine-licm"]
 HEADERS = [os.path.join(_HERE, "csrc", "lfg_device.hpp"),
            os.path.join(_HERE, "csrc", "lfg_tables.hpp"),
            os.path.join(_HERE, "csrc", "lfg_stream_table.h"),
@@ -87,11 +91,11 @@ def source_hash():
     build() reads back), so a stale or foreign binary is told apart from
     the one this tree builds."""
     h = hashlib.sha256()
-    for p in SOURCES + HEADERS:
+    for p in SOURCES + [SPLIT_SOURCE] + HEADERS:
         h.update(os.path.relpath(p, REPO).encode())
         with open(p, "rb") as fh:
             h.update(fh.read())
-    h.update(" ".join(FLAGS).encode())
+    h.update(" ".join(FLAGS + SPLIT_FLAGS).encode())
     return h.hexdigest()[:16]
 
 
@@ -119,10 +123,18 @@ def build(force=False, verbose=False):
     if not force and file_hash(LIB_PATH) == want:
         return LIB_PATH
     tmp = LIB_PATH + ".tmp"
-    cmd = ["hipcc"] + FLAGS + ['-DLFG_SRC_HASH="%s"' % want, "-I", INCLUDE, "-o", tmp] + SOURCES
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
+    obj = LIB_PATH + ".split.tmp.o"
+    cmds = [["hipcc"] + [f for f in FLAGS if f != "-shared"] + SPLIT_FLAGS + ["-I", INCLUDE, "-c", "-o", obj,
+                                                                            SPLIT_SOURCE],
+            ["hipcc"] + FLAGS + ['-DLFG_SRC_HASH="%s"' % want, "-I", INCLUDE, "-o", tmp] + SOURCES + ["-x", "none", obj]]
+    try:
+        for cmd in cmds:
+            if verbose:
+                print(" ".join(cmd))
+            subprocess.run(cmd, check=True)
+    finally:
+        if os.path.exists(obj):
+            os.remove(obj)
     os.replace(tmp, LIB_PATH)
     return LIB_PATH
 

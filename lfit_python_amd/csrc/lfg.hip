@@ -27,6 +27,12 @@
 
 using namespace lfg;
 
+// Diagnostic builds that read device counters back (lfg_debug_*) keep every
+// kernel in this translation unit (see lfg_pair_launch_split below)
+#if defined(LFG_PROFILE_PAIR) || defined(LFG_COUNT_ITERS) || defined(LFG_COUNT_QUIET)
+#define LFG_ONE_TU 1
+#endif
+
 namespace {
 
 constexpr int SETUP_BLOCK = 64;
@@ -579,10 +585,12 @@ __device__ __forceinline__ void setup_any(const SetupArgs& A, int t)
     LFG_CY(3, t, tl);
 }
 
+#ifndef LFG_NOLICM_TU  // (lfg_pair_split.hip compiles k_pair only)
 __global__ __launch_bounds__(SETUP_BLOCK) void k_setup(SetupArgs A)
 {
     setup_any(A, blockIdx.x * SETUP_BLOCK + threadIdx.x);
 }
+#endif
 
 // ------------------------------------------------------------- k_elements
 // One lane per symmetry-unique element.  The WD/disc grids are mirror
@@ -887,6 +895,7 @@ __device__ __forceinline__ void elem_stamp(unsigned long long t0, int kind)
 }
 #endif
 
+#ifndef LFG_NOLICM_TU  // (lfg_pair_split.hip compiles k_pair only)
 __global__ __launch_bounds__(ELEM_BLOCK) __attribute__((amdgpu_waves_per_eu(ELEM_MINW))) void k_elements(const double* __restrict__ geo, int* status, int npairs,
                                                          double2* __restrict__ AB, double* __restrict__ DON,
                                                          double* __restrict__ WT, const int* __restrict__ bstatus,
@@ -960,6 +969,7 @@ __global__ __launch_bounds__(ELEM_BLOCK) __attribute__((amdgpu_waves_per_eu(ELEM
     elem_stamp(pt0, 1 + ck);  // 1 + chunk of the pair's items
 #endif
 }
+#endif
 
 // interval of element k (MODEL_SPEC 5 numbering) from a pair's table: the
 // unique item of k's mirror pair, mirrored when k is the partner
@@ -989,6 +999,7 @@ __device__ inline double2 elem_ab(const double2* __restrict__ AB, int k)
 }
 
 // test/inspection only: per-element weights and the full 400-tile donor
+#ifndef LFG_NOLICM_TU  // (lfg_pair_split.hip compiles k_pair only)
 __global__ void k_expand(const double* __restrict__ geo, const int* __restrict__ status, int npairs,
                          const double2* __restrict__ AB, const double* __restrict__ DON, double* __restrict__ A,
                          double* __restrict__ B, double* __restrict__ WG, double* __restrict__ DFULL)
@@ -1027,6 +1038,7 @@ __global__ void k_expand(const double* __restrict__ geo, const int* __restrict__
         }
     }
 }
+#endif
 
 // --------------------------------------------------------------- k_lnlike
 // Cross-lane sums and scans by DPP (no LDS round trips; __shfl_xor /
@@ -4516,6 +4528,7 @@ __global__ __launch_bounds__(LIKE_THREADS, LIKE_MINW) void k_pair(PairArgs A)
 // (the nested eclipse solver), min / max by shuffles; other pairs return at
 // once.  Runs after k_elements (the pair's record is in the standard slot)
 // and before k_lnlike<2>, which reads G_GP_DCP.
+#ifndef LFG_NOLICM_TU  // (lfg_pair_split.hip compiles k_pair only)
 __global__ __launch_bounds__(64) void k_gp_dcp(double* __restrict__ geo, const int* __restrict__ status, int npairs)
 {
     const int pair = int(blockIdx.x) * (64 / DCP_LANES) + int(threadIdx.x) / DCP_LANES;
@@ -4549,6 +4562,7 @@ __global__ __launch_bounds__(64) void k_gp_dcp(double* __restrict__ geo, const i
         G[G_GP_OK] = ok ? 1.0 : 0.0;
     }
 }
+#endif
 
 // -------------------------------------------------------------- k_gp_like
 // GP trees (MODEL_SPEC 10.4): the Kalman filter over each pair's residuals
@@ -4611,6 +4625,7 @@ __device__ __forceinline__ double gp_pinf(int i, int j, double ain, double aout,
     return k == 0 ? a : (k == 1 ? a * lam : 2.0 * a * lam * lam);
 }
 
+#ifndef LFG_NOLICM_TU  // (lfg_pair_split.hip compiles k_pair only)
 __global__ __launch_bounds__(GP_BLOCK) __attribute__((amdgpu_waves_per_eu(2))) void k_gp_like(LikeArgs L)
 {
     __shared__ double sel[GP_PAIRS][GP_SEG][4][GP_EL];
@@ -4887,6 +4902,7 @@ __global__ __launch_bounds__(GP_BLOCK) __attribute__((amdgpu_waves_per_eu(2))) v
     L.lle[pair] = lle;
     combine_after(L, pair);
 }
+#endif
 
 // -------------------------------------------------------------- k_combine
 // E > 1: ln_prob (and the fused acceptance) of every walker once all its
@@ -4898,6 +4914,7 @@ __global__ __launch_bounds__(GP_BLOCK) __attribute__((amdgpu_waves_per_eu(2))) v
 // once (the walker's chain of 2E dependent-latency loads in one lane was 43 us
 // per config-3 launch), lane 0 adds them in combine_walker's order (the
 // same sums, bit for bit), and the lanes copy an accepted proposal.
+#ifndef LFG_NOLICM_TU  // (lfg_pair_split.hip compiles k_pair only)
 __global__ __launch_bounds__(256) void k_combine_walkers(LikeArgs L)
 {
     const int w = int(blockIdx.x) * 4 + int(threadIdx.x >> 6), lane = int(threadIdx.x & 63);
@@ -4942,7 +4959,9 @@ __global__ __launch_bounds__(256) void k_combine_walkers(LikeArgs L)
     if (__shfl(acc ? 1 : 0, 0, 64))
         for (int d = lane; d < L.ndim; d += 64) L.pos[size_t(wg) * L.ndim + d] = L.qprop[size_t(w) * L.ndim + d];
 }
+#endif
 
+#ifndef LFG_NOLICM_TU  // (lfg_pair_split.hip compiles k_pair only)
 __global__ void k_combine(int W, int E, const double* __restrict__ prior, const double* __restrict__ geo,
                           double* __restrict__ lle, double* __restrict__ lnp)
 {
@@ -4966,6 +4985,7 @@ __global__ void k_combine(int W, int E, const double* __restrict__ prior, const 
     for (int e = 0; e < E; ++e) ll += lle[size_t(w) * E + e];
     lnp[w] = lp + ll;
 }
+#endif
 
 // ------------------------------------------------------- stretch-move sampler
 // Philox4x32-10 (Salmon et al. 2011), counter = (walker, step lo, step hi,
@@ -4997,6 +5017,7 @@ __device__ inline uint4 draw(unsigned long long seed, unsigned long long step, i
 // q = c_j - (c_j - s) z = c_j + z (s - c_j), factor = (ndim - 1) ln z
 // step counter: by value, or (stepp != nullptr) from device memory so that
 // a captured HIP graph replays with the current step
+#ifndef LFG_NOLICM_TU  // (lfg_pair_split.hip compiles k_pair only)
 __global__ void k_propose(const double* __restrict__ pos, int W, int ndim, int half, double a,
                           unsigned long long seed, unsigned long long step,
                           const unsigned long long* __restrict__ stepp, double* __restrict__ q,
@@ -5017,8 +5038,10 @@ __global__ void k_propose(const double* __restrict__ pos, int W, int ndim, int h
     for (int d = 0; d < ndim; ++d) out[d] = fma(s[d] - cj[d], z, cj[d]);  // c_j + z (s - c_j), as make_prop
     zfac[i] = (ndim - 1.0) * log(z);
 }
+#endif
 
 // Metropolis acceptance: accept if ln u < factor + lnp_new - lnp_old
+#ifndef LFG_NOLICM_TU  // (lfg_pair_split.hip compiles k_pair only)
 __global__ void k_accept(double* __restrict__ pos, double* __restrict__ lnp, int W, int ndim, int half,
                          const double* __restrict__ q, const double* __restrict__ zfac,
                          const double* __restrict__ lnp_new, unsigned long long seed, unsigned long long step,
@@ -5040,6 +5063,7 @@ __global__ void k_accept(double* __restrict__ pos, double* __restrict__ lnp, int
         if (naccept) naccept[w] += 1;
     }
 }
+#endif
 
 // k_accept with the proposal re-formed from the same draws (k_propose's
 // arithmetic): the sharded half-step keeps only its own shard of q, and the
@@ -5049,6 +5073,7 @@ __global__ void k_accept(double* __restrict__ pos, double* __restrict__ lnp, int
 // accepted walker's row moves with one load round over the lanes (lane d:
 // dimension d) instead of one lane's serial chunks of 8
 constexpr int REGEN_WAVES = 4;
+#ifndef LFG_NOLICM_TU  // (lfg_pair_split.hip compiles k_pair only)
 __global__ __launch_bounds__(64 * REGEN_WAVES) void k_accept_regen(double* __restrict__ pos, double* __restrict__ lnp, int W, int ndim, int half,
                                double a, const double* __restrict__ lnp_new, unsigned long long seed,
                                unsigned long long step, int* __restrict__ naccept, int* __restrict__ accflag)
@@ -5077,6 +5102,7 @@ __global__ __launch_bounds__(64 * REGEN_WAVES) void k_accept_regen(double* __res
     }
     if (accflag && lane == 0) accflag[i] = acc ? 1 : 0;  // the speculative setup's candidate choice
 }
+#endif
 
 // the deferred acceptance's two halves outside k_pair<_, true>:
 //  k_apply_verdicts: half `half`'s gathered verdicts (ln_prob where the move
@@ -5084,6 +5110,7 @@ __global__ __launch_bounds__(64 * REGEN_WAVES) void k_accept_regen(double* __res
 //  re-formed from its draws as k_accept_regen does (the flush at a chain's
 //  end, and the fold's fallback); one wave per walker
 //  k_verdict: a shard's verdicts from its ln_prob (k_accept_regen's test)
+#ifndef LFG_NOLICM_TU  // (lfg_pair_split.hip compiles k_pair only)
 __global__ __launch_bounds__(64 * REGEN_WAVES) void k_apply_verdicts(double* __restrict__ pos, double* __restrict__ lnp,
                                                                       int W, int ndim, int half, double a,
                                                                       const double* __restrict__ verdict,
@@ -5112,7 +5139,9 @@ __global__ __launch_bounds__(64 * REGEN_WAVES) void k_apply_verdicts(double* __r
     }
     if (accflag && lane == 0) accflag[i] = acc ? 1 : 0;
 }
+#endif
 
+#ifndef LFG_NOLICM_TU  // (lfg_pair_split.hip compiles k_pair only)
 __global__ void k_verdict(const double* __restrict__ lnp_new, const double* __restrict__ lnp,
                           const double* __restrict__ zfac, int n, int lo, int ns, int half, unsigned long long seed,
                           unsigned long long step, double* __restrict__ vout)
@@ -5123,6 +5152,7 @@ __global__ void k_verdict(const double* __restrict__ lnp_new, const double* __re
     const double v = lnp_new[k];
     vout[k] = (log(u53(r.x, r.y)) < zfac[k] + v - lnp[size_t(half) * ns + lo + k]) ? v : NAN;
 }
+#endif
 
 // ------------------------------------------------------ k_gp, k_wdphases
 __device__ __forceinline__ double readlane_f64(double v, int j)
@@ -5134,6 +5164,7 @@ __device__ __forceinline__ double readlane_f64(double v, int j)
 
 // one wave per residual vector: lanes load 64 points at a time, every lane
 // runs the (wave-uniform) filter over them through readlane broadcasts
+#ifndef LFG_NOLICM_TU  // (lfg_pair_split.hip compiles k_pair only)
 __global__ __launch_bounds__(64) void k_gp(const double* __restrict__ x, const double* __restrict__ ye,
                                            const double* __restrict__ res, int N, const double* __restrict__ hyp,
                                            const double* __restrict__ blocks, int nb, double* __restrict__ lnlike)
@@ -5160,7 +5191,9 @@ __global__ __launch_bounds__(64) void k_gp(const double* __restrict__ x, const d
     }
     if (lane == 0) lnlike[w] = F.lnlike();
 }
+#endif
 
+#ifndef LFG_NOLICM_TU  // (lfg_pair_split.hip compiles k_pair only)
 __global__ void k_wdphases(const double* __restrict__ q, const double* __restrict__ inc,
                            const double* __restrict__ r1, int n, int ntheta, double* __restrict__ ph3,
                            double* __restrict__ ph4, int* __restrict__ status)
@@ -5175,8 +5208,10 @@ __global__ void k_wdphases(const double* __restrict__ q, const double* __restric
     ph4[i] = (st == ST_OK) ? b : NAN;
     status[i] = st;
 }
+#endif
 
 // ---------------------------------------------------------------- k_roche
+#ifndef LFG_NOLICM_TU  // (lfg_pair_split.hip compiles k_pair only)
 __global__ void k_roche(int op, const double* __restrict__ a, const double* __restrict__ b, int n,
                         double* __restrict__ out, int* __restrict__ status)
 {
@@ -5202,9 +5237,11 @@ __global__ void k_roche(int op, const double* __restrict__ a, const double* __re
     }
     status[i] = st;
 }
+#endif
 
 inline int launch_ok() { return hipGetLastError() == hipSuccess ? LFG_OK : LFG_E_LAUNCH; }
 
+#ifndef LFG_NOLICM_TU
 // k_setup (setup, prior and stream lanes) then k_elements, on the caller's
 // stream.  ev (nullable, LFG_NEV events): 0 before k_setup, 1 after k_setup,
 // 2 after k_elements
@@ -5234,7 +5271,38 @@ int run_front(const SetupArgs& S, const Ws& ws, hipStream_t st, void* const* ev,
     mark(2);
     return LFG_OK;
 }
+#endif  // LFG_NOLICM_TU
 
+}  // namespace
+
+// k_pair's fold and LONG instantiations are compiled in lfg_pair_split.hip:
+// this source again, without machine LICM (-mllvm -disable-machine-licm).
+// At the 128-VGPR ceiling the pass hoisted literal constants and cheap loop
+// invariants into VGPRs and the register allocator then spilled: LONG's
+// point loop reloaded five doubles from scratch per point (48 B per lane,
+// 41.6 MB of PMC traffic per config-5 launch), the fold variant 32 B.
+// Without it LONG spills 16 B and the fold variant none: config 5
+// 3.39 -> 3.52 M evals/s; config 4's one-of-eight fold shard 12.71 -> 12.76
+// and 12.36 -> 12.77 M on two boxes (profiles/r06/ab_split_nolicm.txt).  The
+// speculative one-tile k_pair (config 2) measured no different and GP trees
+// 5 % slower, so they stay here, compiled with the pass.
+enum { PAIR_SPLIT_LONG = 0, PAIR_SPLIT_FOLD = 1, PAIR_SPLIT_FOLD_LONG = 2 };
+__attribute__((visibility("hidden"))) void lfg_pair_launch_split(int variant, unsigned grid, hipStream_t st,
+                                                                   const void* args);
+
+#ifndef LFG_NOLICM_TU
+namespace {
+// launch k_pair<false, FOLD, LONG> (not both false) with the arguments A
+void launch_pair_split(int variant, unsigned grid, hipStream_t st, const PairArgs& A)
+{
+#ifdef LFG_ONE_TU
+    if (variant == PAIR_SPLIT_LONG) hipLaunchKernelGGL((k_pair<false, false, true>), dim3(grid), dim3(LIKE_THREADS), 0, st, A);
+    else if (variant == PAIR_SPLIT_FOLD) hipLaunchKernelGGL((k_pair<false, true>), dim3(grid), dim3(LIKE_THREADS), 0, st, A);
+    else hipLaunchKernelGGL((k_pair<false, true, true>), dim3(grid), dim3(LIKE_THREADS), 0, st, A);
+#else
+    lfg_pair_launch_split(variant, grid, st, &A);
+#endif
+}
 }  // namespace
 
 extern "C" {
@@ -5358,7 +5426,7 @@ int lfg_lnlike(const double* pars, int W, int P, const double* x, const double* 
     L.bstatus = ws.bstatus;
     PairArgs A{L, ElemSpec{}, nullptr, nullptr, 64, 0, 0ull, 0ull, 0, 0, 0, pair_prio(W)};
     fill_hot(A);
-    if (kind == 2) hipLaunchKernelGGL((k_pair<false, false, true>), dim3(W), dim3(LIKE_THREADS), 0, st, A);
+    if (kind == 2) launch_pair_split(PAIR_SPLIT_LONG, unsigned(W), st, A);
     else if (pair) hipLaunchKernelGGL(k_pair<false>, dim3(W), dim3(LIKE_THREADS), 0, st, A);
     else if (nsub > 1) hipLaunchKernelGGL((k_lnlike<1, true>), dim3(W), dim3(LIKE_THREADS), 0, st, L);
     else hipLaunchKernelGGL((k_lnlike<1, false>), dim3(W), dim3(LIKE_THREADS), 0, st, L);
@@ -5559,8 +5627,7 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
             A.L.half = h;
             A.L.zfac = prop->zfac;
             fill_hot(A);
-            if (kind == 2) hipLaunchKernelGGL((k_pair<false, true, true>), dim3(npairs), dim3(LIKE_THREADS), 0, st, A);
-            else hipLaunchKernelGGL((k_pair<false, true>), dim3(npairs), dim3(LIKE_THREADS), 0, st, A);
+            launch_pair_split(kind == 2 ? PAIR_SPLIT_FOLD_LONG : PAIR_SPLIT_FOLD, unsigned(npairs), st, A);
             if ((rc = launch_ok())) return rc;
             mark(3);
             return LFG_OK;
@@ -5590,7 +5657,7 @@ static int lnprob_impl(const double* walkers, int W, const lfg_tree* T, double* 
             hipLaunchKernelGGL(k_gp_like, dim3(T->E * ((W + GP_PAIRS - 1) / GP_PAIRS)), dim3(GP_BLOCK), 0, st, L);
         } else if (kind == 2) {
             fill_hot(A);
-            hipLaunchKernelGGL((k_pair<false, false, true>), dim3(npairs), dim3(LIKE_THREADS), 0, st, A);
+            launch_pair_split(PAIR_SPLIT_LONG, unsigned(npairs), st, A);
         } else {
             fill_hot(A);
             hipLaunchKernelGGL(k_pair<false>, dim3(npairs), dim3(LIKE_THREADS), 0, st, A);
@@ -6007,3 +6074,4 @@ int lfg_diag_iters(unsigned long long* out)
 #endif
 
 }  // extern "C"
+#endif  // LFG_NOLICM_TU

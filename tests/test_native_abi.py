@@ -157,10 +157,14 @@ def test_stale_library_is_rebuilt(tmp_path, monkeypatch):
         _native.LIB_PATH + ".orig", cmd[cmd.index("-o") + 1]))[0])
     (tmp_path / "liblfg_hip.so.orig").write_bytes(data)
     _native.build()
-    assert len(calls) == 1 and ('-DLFG_SRC_HASH="%s"' % want) in calls[0]
+    # two hipcc runs: the split unit (k_pair's fold and LONG instantiations,
+    # without machine LICM), then the library linked with it
+    assert len(calls) == 2 and calls[0][-1] == _native.SPLIT_SOURCE and "-disable-machine-licm" in calls[0]
+    assert ('-DLFG_SRC_HASH="%s"' % want) in calls[1] and "-disable-machine-licm" not in calls[1]
     assert _native.file_hash(str(lib)) == want
+    assert not any(p.name.endswith(".tmp.o") for p in tmp_path.iterdir())
     _native.build()                      # now current: nothing rebuilt
-    assert len(calls) == 1
+    assert len(calls) == 2
 
 
 def test_foreign_library_refused(tmp_path):

@@ -6,5 +6,14 @@ set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 name=$1; shift
 mkdir -p $R/build/exp
+# k_pair's fold and LONG instantiations: lfg_pair_split.hip without machine
+# LICM (LFG_SRC builds of older sources have no split unit: LFG_SPLIT=0)
+split=
+if [ "${LFG_SPLIT:-1}" = 1 ]; then
+  hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -mllvm -disable-machine-licm -I $R/include "$@" \
+    -c -o $R/build/exp/split_$name.o $R/lfit_python_amd/csrc/lfg_pair_split.hip
+  split="-x none $R/build/exp/split_$name.o"
+fi
 hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -I $R/include "$@" \
-  -o $R/build/exp/liblfg_$name.so ${LFG_SRC:-$R/lfit_python_amd/csrc/lfg.hip} $R/lfit_python_amd/csrc/lfg_components.hip
+  -o $R/build/exp/liblfg_$name.so ${LFG_SRC:-$R/lfit_python_amd/csrc/lfg.hip} $R/lfit_python_amd/csrc/lfg_components.hip $split
+rm -f $R/build/exp/split_$name.o
