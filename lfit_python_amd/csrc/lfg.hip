@@ -3448,9 +3448,13 @@ __device__ __forceinline__ bool sub_point_quiet(const SubTables& T, const SubEnt
         U.dkw = wk;
         U.dk = Dk;
     }
-    // (sin, cos) at the window's centre; out of line: inlined here it cost
-    // config 5 13 % (its constants and temporaries against the 128 VGPRs)
-    const double2 e = sincospi_ool(2.0 * phc);
+    // (sin, cos) at the window's centre, inlined: out of line while the
+    // unit was compiled with machine LICM (inlined, its hoisted constants
+    // spilled: config 5 -13 %); without the pass inlined is +0.7 %
+    // (profiles/r06/long/ab_sincospi_inline_nolicm.txt)
+    double esn, ecs;
+    sincospi(2.0 * phc, &esn, &ecs);
+    const double2 e = make_double2(esn, ecs);
     const double Scs = Dk * e.y, Ssn = Dk * e.x;
     const double srs1 = fma(Scs, double(U.vx), -Ssn * double(U.vy)), srs2 = S * double(U.vz);
     const double bc = fma(K.nbs0, e.y, fma(K.nbs1, e.x, K.nbc));  // b at the centre: its sign in the window
