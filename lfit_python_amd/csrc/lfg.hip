@@ -4633,6 +4633,7 @@ __device__ __forceinline__ double gp_pinf(int i, int j, double ain, double aout,
 __global__ __launch_bounds__(GP_BLOCK) __attribute__((amdgpu_waves_per_eu(2))) void k_gp_like(LikeArgs L)
 {
     __shared__ double sel[GP_PAIRS][GP_SEG][4][GP_EL];
+    __shared__ double sgap[GP_PAIRS][GP_SEG][4];  // the gap into each segment (the combine's transition)
     const int nw = L.npairs / L.E, nwb = (nw + GP_PAIRS - 1) / GP_PAIRS;
     const int e = int(blockIdx.x) / nwb;
     const int lane = int(threadIdx.x), pp = lane / GP_LPP, sg = (lane / 4) % GP_SEG, r = lane & 3;
@@ -4677,6 +4678,13 @@ __global__ __launch_bounds__(GP_BLOCK) __attribute__((amdgpu_waves_per_eu(2))) v
             }
         };
         if (i1 > i0) fetch(i0);
+        if (i1 > i0) {  // the gap into this segment (the combine's transition): lane r of the quad
+            // writes entry r (d, e^{-lam d}, block start), read back in the combine
+            // instead of a dependent global load per segment (k_gp_like 42.0 -> 40.4 us,
+            // profiles/r06/ab_gp_combine.txt)
+            const bool fr = cb[0] >= 0 && cb[0] != bp;
+            sgap[pp][sg][r] = r == 0 ? cx[0] - xprev : (r == 1 ? ce[0] : (fr ? 1.0 : 0.0));
+        }
         for (int p0 = i0; p0 < i1; p0 += GP_CHUNK) {
             double dk[GP_CHUNK], ek[GP_CHUNK], Ek[GP_CHUNK], ye2[GP_CHUNK], rv[GP_CHUNK];
             int blk[GP_CHUNK];
@@ -4792,9 +4800,8 @@ __global__ __launch_bounds__(GP_BLOCK) __attribute__((amdgpu_waves_per_eu(2))) v
         const double* El = &sel[pp][s][0][0];
         bad = bad || El[15] != 0.0 || El[GP_EL + 15] != 0.0;
         if (s > 0 && i0 > 0) {  // the gap from the previous segment's last point
-            const double d = xs[i0] - xs[i0 - 1], ex = gx[i0], E = ex * ex;
-            const int b1 = gb[i0];
-            const bool fresh = b1 >= 0 && b1 != gb[i0 - 1];
+            const double d = sgap[pp][s][0], ex = sgap[pp][s][1], E = ex * ex;
+            const bool fresh = sgap[pp][s][2] != 0.0;
             mu[0] = ex * fma(d, mu[1], mu[0]);
             mu[1] = ex * mu[1];
             mu[2] = fresh ? 0.0 : ex * fma(d, mu[3], mu[2]);
